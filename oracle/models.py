@@ -1,0 +1,231 @@
+"""ORACLE (test infrastructure only) — network restatement in torch-CPU float32 (functional form).
+
+Rows A6 (Whisper encoder), A10 (conditioner), A11 (DiffSVC), A12 (samplers), A14 (BigVGAN) of
+SURVEY.md §8(a). Parameters are dicts in the reference's state_dict naming (see
+svc_inference_pipeline_amd/weights.py); values may be numpy or torch.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def _t(sd, k):
+    v = sd[k]
+    return v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v))
+
+
+# ============================================================================ Whisper AudioEncoder
+
+
+def whisper_encoder(sd, mel, n_head):
+    """utils/whisper_extractor/model.py:132-160 (AudioEncoder.forward) with
+    MultiHeadAttention.qkv_attention :88-101 and ResidualAttentionBlock :104-129. mel f32[B,80,3000]."""
+    x = F.gelu(F.conv1d(mel, _t(sd, "encoder.conv1.weight"), _t(sd, "encoder.conv1.bias"), padding=1))
+    x = F.gelu(F.conv1d(x, _t(sd, "encoder.conv2.weight"), _t(sd, "encoder.conv2.bias"), stride=2, padding=1))
+    x = x.permute(0, 2, 1)
+    x = x + _t(sd, "encoder.positional_embedding")
+    i = 0
+    while f"encoder.blocks.{i}.attn.query.weight" in sd:
+        p = f"encoder.blocks.{i}."
+        h = F.layer_norm(x, (x.shape[-1],), _t(sd, p + "attn_ln.weight"), _t(sd, p + "attn_ln.bias"))
+        q = F.linear(h, _t(sd, p + "attn.query.weight"), _t(sd, p + "attn.query.bias"))
+        k = F.linear(h, _t(sd, p + "attn.key.weight"))
+        v = F.linear(h, _t(sd, p + "attn.value.weight"), _t(sd, p + "attn.value.bias"))
+        nb, nc, ns = q.shape
+        scale = (ns // n_head) ** -0.25
+        q = q.view(nb, nc, n_head, -1).permute(0, 2, 1, 3) * scale
+        k = k.view(nb, nc, n_head, -1).permute(0, 2, 3, 1) * scale
+        v = v.view(nb, nc, n_head, -1).permute(0, 2, 1, 3)
+        w = F.softmax((q @ k).float(), dim=-1)
+        wv = (w @ v).permute(0, 2, 1, 3).flatten(start_dim=2)
+        x = x + F.linear(wv, _t(sd, p + "attn.out.weight"), _t(sd, p + "attn.out.bias"))
+        h = F.layer_norm(x, (x.shape[-1],), _t(sd, p + "mlp_ln.weight"), _t(sd, p + "mlp_ln.bias"))
+        h = F.gelu(F.linear(h, _t(sd, p + "mlp.0.weight"), _t(sd, p + "mlp.0.bias")))
+        x = x + F.linear(h, _t(sd, p + "mlp.2.weight"), _t(sd, p + "mlp.2.bias"))
+        i += 1
+    return F.layer_norm(x, (x.shape[-1],), _t(sd, "encoder.ln_post.weight"), _t(sd, "encoder.ln_post.bias"))
+
+
+# ============================================================================ conditioner
+
+
+def bucketize_indices(values, bins):
+    """torch.bucketize(x, bins) (right=False) as in modules/encoder.py:70,115: count of bins < x."""
+    return torch.bucketize(values, bins)
+
+
+def conditioner(sd, content, f0, energy, singer, content_type="whisper"):
+    """modules/encoder.py:165-201, merge_mode "add". content f32[B,T,D], f0 f64[B,T], energy f32[B,T],
+    singer int[B,1]. Summation order: content, melody, loudness, singer (ModuleDict order)."""
+    p = "0.registered_modules_dict."
+    c = F.linear(content, _t(sd, p + f"content_{content_type}.nn.weight"), _t(sd, p + f"content_{content_type}.nn.bias"))
+    m = F.embedding(torch.bucketize(f0, _t(sd, p + "melody.melody_bins")), _t(sd, p + "melody.nn.weight"))
+    l = F.embedding(torch.bucketize(energy, _t(sd, p + "loudness.energy_bins")), _t(sd, p + "loudness.nn.weight"))
+    s = F.embedding(singer, _t(sd, p + "singer.nn.weight")).expand(-1, c.shape[1], -1)
+    return torch.sum(torch.cat([o[None] for o in (c, m, l, s)], dim=0), dim=0)
+
+
+# ============================================================================ DiffSVC epsilon predictor
+
+
+def diffsvc_forward(sd, mcfg, x, cond, t, step_table):
+    """modules/diffsvc.py:284-321 (+ StepEncoder :67-94, ResidualBlock :192-232, Preprocessor :111-125).
+    x f32[B,T,100], cond f32[B,T,384], t int64[B] -> eps f32[B,T,100]."""
+    q = "1."
+    h = F.relu(F.conv1d(x.transpose(1, 2), _t(sd, q + "mel_preprocess.projection.weight"), _t(sd, q + "mel_preprocess.projection.bias")))
+    e = step_table[t.unsqueeze(1)]  # [B,1,128]
+    e = F.silu(F.linear(e, _t(sd, q + "diffusion_embedding.projection1.weight"), _t(sd, q + "diffusion_embedding.projection1.bias")))
+    e = F.silu(F.linear(e, _t(sd, q + "diffusion_embedding.projection2.weight"), _t(sd, q + "diffusion_embedding.projection2.bias")))
+    condT = cond.transpose(1, 2)
+    skip = None
+    n = mcfg.residual_layer_num
+    for i in range(n):
+        r = q + f"residual_layers.{i}."
+        d = F.linear(e, _t(sd, r + "diffusion_projection.weight"), _t(sd, r + "diffusion_projection.bias"))
+        y = h + d.transpose(1, 2)
+        cp = F.conv1d(condT, _t(sd, r + "conditioner_projection.weight"), _t(sd, r + "conditioner_projection.bias"))
+        dil = 2 ** (i % mcfg.dilation_cycle_length)
+        y = F.conv1d(y, _t(sd, r + "dilated_conv.weight"), _t(sd, r + "dilated_conv.bias"), padding=dil, dilation=dil) + cp
+        gate, filt = torch.chunk(y, 2, dim=1)
+        y = torch.sigmoid(gate) * torch.tanh(filt)
+        y = F.conv1d(y, _t(sd, r + "output_projection.weight"), _t(sd, r + "output_projection.bias"))
+        res, sk = torch.chunk(y, 2, dim=1)
+        h = (h + res) / math.sqrt(2.0)
+        skip = sk if skip is None else sk + skip
+    h = skip / math.sqrt(n)
+    h = F.relu(F.conv1d(h, _t(sd, q + "skip_projection.weight"), _t(sd, q + "skip_projection.bias")))
+    h = F.conv1d(h, _t(sd, q + "output_projection.weight"), _t(sd, q + "output_projection.bias"))
+    return h.transpose(1, 2)
+
+
+# ============================================================================ samplers
+
+
+def schedule_constants(betas):
+    """modules/diffsvcrepo_inference.py:163-197: numpy f64 -> torch f32."""
+    to = lambda a: torch.tensor(a, dtype=torch.float32)
+    alphas = 1.0 - betas
+    ac = np.cumprod(alphas, axis=0)
+    ac_prev = np.append(1.0, ac[:-1])
+    post_var = betas * (1.0 - ac_prev) / (1.0 - ac)
+    return {
+        "alphas_cumprod": to(ac),
+        "sqrt_recip_alphas_cumprod": to(np.sqrt(1.0 / ac)),
+        "sqrt_recipm1_alphas_cumprod": to(np.sqrt(1.0 / ac - 1)),
+        "posterior_mean_coef1": to(betas * np.sqrt(ac_prev) / (1.0 - ac)),
+        "posterior_mean_coef2": to((1.0 - ac_prev) * np.sqrt(alphas) / (1.0 - ac)),
+        "posterior_log_variance_clipped": to(np.log(np.maximum(post_var, 1e-20))),
+    }
+
+
+def plms_x_pred(x, noise_t, t, interval, ac):
+    """p_sample_plms.get_x_pred, modules/diffsvcrepo_inference.py:96-113 (x in [B,T,100] layout;
+    the update is elementwise so the reference's [B,1,100,T] layout does not change values)."""
+    a_t = ac[t].view(-1, 1, 1)
+    a_prev = ac[torch.clamp(t - interval, min=0)].view(-1, 1, 1)
+    a_t_sq, a_prev_sq = a_t.sqrt(), a_prev.sqrt()
+    x_delta = (a_prev - a_t) * ((1 / (a_t_sq * (a_t_sq + a_prev_sq))) * x
+                                - 1 / (a_t_sq * (((1 - a_prev) * a_t).sqrt() + ((1 - a_t) * a_prev).sqrt())) * noise_t)
+    return x + x_delta
+
+
+def sample_plms(denoise, x, B, T, steps, interval, consts):
+    """modules/diffsvcrepo_inference.py:91-151,216-231 (fast_inference=True). `denoise(x, t)` returns
+    the epsilon tensor (the reference's denoise_fn returns (eps, stats); A12 — the oracle takes [0]).
+    x: x_T f32[B,T,100]. Returns x_0 f32[B,T,100]."""
+    ac = consts["alphas_cumprod"]
+    hist = []
+    for i in reversed(range(0, steps, interval)):
+        t = torch.full((B,), i, dtype=torch.long)
+        eps = denoise(x, t)
+        if len(hist) == 0:
+            x_pred = plms_x_pred(x, eps, t, interval, ac)
+            t_prev = torch.full((B,), max(i - interval, 0), dtype=torch.long)
+            eps_prev = denoise(x_pred, t_prev)
+            e = (eps + eps_prev) / 2
+        elif len(hist) == 1:
+            e = (3 * eps - hist[-1]) / 2
+        elif len(hist) == 2:
+            e = (23 * eps - 16 * hist[-1] + 5 * hist[-2]) / 12
+        else:
+            e = (55 * eps - 59 * hist[-1] + 37 * hist[-2] - 9 * hist[-3]) / 24
+        x = plms_x_pred(x, e, t, interval, ac)
+        hist.append(eps)
+        hist = hist[-4:]
+    return x
+
+
+def ddpm_step(x, eps, t, z, consts):
+    """p_sample / p_mean_variance / q_posterior (modules/diffsvcrepo_inference.py:36-88),
+    clip_denoised=True. x, eps, z f32[B,T,100]; t python int (same for the whole batch)."""
+    x_recon = consts["sqrt_recip_alphas_cumprod"][t] * x - consts["sqrt_recipm1_alphas_cumprod"][t] * eps
+    x_recon = x_recon.clamp(-1.0, 1.0)
+    mean = consts["posterior_mean_coef1"][t] * x_recon + consts["posterior_mean_coef2"][t] * x
+    nonzero = 0.0 if t == 0 else 1.0
+    return mean + nonzero * (0.5 * consts["posterior_log_variance_clipped"][t]).exp() * z
+
+
+def sample_ddpm(denoise, x, B, T, steps, consts, noise_fn):
+    """modules/diffsvcrepo_inference.py:233-235. noise_fn(i) -> z f32[B,T,100] for step i (the
+    reference draws randn([B,1,100,T]) each step, t = 0 included; callers transpose to [B,T,100])."""
+    for i in reversed(range(0, steps)):
+        t = torch.full((B,), i, dtype=torch.long)
+        eps = denoise(x, t)
+        x = ddpm_step(x, eps, i, noise_fn(i), consts)
+    return x
+
+
+# ============================================================================ BigVGAN generator
+
+
+def _wn(sd, name):
+    """weight_norm fold, dim=0 (torch._weight_norm: v * g / ||v|| over all dims but 0)."""
+    return torch._weight_norm(_t(sd, name + ".weight_v"), _t(sd, name + ".weight_g"), 0)
+
+
+def activation1d(x, alpha_log, beta_log, filt):
+    """modules/bigvgan.py:234-307 (Activation1d = UpSample1d(2,12) -> SnakeBeta(logscale) -> DownSample1d(2,12))
+    with SnakeBeta :146-159. x f32[B,C,T]."""
+    C = x.shape[1]
+    f = filt.view(1, 1, -1)
+    # UpSample1d :277-287  (ratio 2, kernel 12: pad 5, pad_left 15, pad_right 15)
+    xu = F.pad(x, (5, 5), mode="replicate")
+    xu = 2 * F.conv_transpose1d(xu, f.expand(C, -1, -1), stride=2, groups=C)
+    xu = xu[..., 15:-15]
+    # SnakeBeta :146-159
+    alpha = torch.exp(alpha_log).view(1, -1, 1)
+    beta = torch.exp(beta_log).view(1, -1, 1)
+    xu = xu + (1.0 / (beta + 0.000000001)) * torch.pow(torch.sin(xu * alpha), 2)
+    # DownSample1d -> LowPassFilter1d :224-231 (pad_left 5, pad_right 6, stride 2)
+    xd = F.pad(xu, (5, 6), mode="replicate")
+    return F.conv1d(xd, f.expand(C, -1, -1), stride=2, groups=C)
+
+
+def _act(sd, name, x):
+    return activation1d(x, _t(sd, name + ".act.alpha"), _t(sd, name + ".act.beta"), _t(sd, name + ".upsample.filter"))
+
+
+def bigvgan_forward(sd, vcfg, mel):
+    """modules/bigvgan.py:600-622 (Generator.forward) with AMPBlock1.forward :424-433.
+    mel f32[B,100,T] -> f32[B,1,256T]."""
+    x = F.conv1d(mel, _wn(sd, "conv_pre"), _t(sd, "conv_pre.bias"), padding=3)
+    nk = len(vcfg.resblock_kernel_sizes)
+    for i, (u, k) in enumerate(zip(vcfg.upsample_rates, vcfg.upsample_kernel_sizes)):
+        x = F.conv_transpose1d(x, _wn(sd, f"ups.{i}.0"), _t(sd, f"ups.{i}.0.bias"), stride=u, padding=(k - u) // 2)
+        xs = None
+        for j, (kk, dd) in enumerate(zip(vcfg.resblock_kernel_sizes, vcfg.resblock_dilation_sizes)):
+            rb = f"resblocks.{i * nk + j}."
+            xr = x
+            for l, d in enumerate(dd):
+                xt = _act(sd, rb + f"activations.{2 * l}", xr)
+                xt = F.conv1d(xt, _wn(sd, rb + f"convs1.{l}"), _t(sd, rb + f"convs1.{l}.bias"), dilation=d, padding=(kk * d - d) // 2)
+                xt = _act(sd, rb + f"activations.{2 * l + 1}", xt)
+                xt = F.conv1d(xt, _wn(sd, rb + f"convs2.{l}"), _t(sd, rb + f"convs2.{l}.bias"), padding=(kk - 1) // 2)
+                xr = xt + xr
+            xs = xr if xs is None else xs + xr
+        x = xs / nk
+    x = _act(sd, "activation_post", x)
+    x = F.conv1d(x, _wn(sd, "conv_post"), _t(sd, "conv_post.bias"), padding=3)
+    return torch.tanh(x)

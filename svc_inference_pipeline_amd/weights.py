@@ -1,0 +1,247 @@
+"""Model parameters in the reference's own state_dict format.
+
+No trained checkpoints exist offline (`/mnt/workspace/...` paths in config.json:7-10, Whisper
+download at utils/whisper_extractor/__init__.py:26,103), so this module builds seeded random
+parameters whose NAMES and SHAPES are exactly the reference's state_dict keys:
+
+  mapper   : torch.nn.ModuleList([EncoderFramework, DiffSVC])   (utils/load_models.py:17-20)
+  vocoder  : bigvgan.Generator                                   (modules/bigvgan.py:519-622)
+  whisper  : Whisper.encoder (AudioEncoder)                      (utils/whisper_extractor/model.py:132-160)
+
+Random tensors come from numpy PCG64 keyed by (seed, crc32(name)), so any subset is reproducible
+independently of generation order. Model BUFFERS the reference builds at construction time
+(melody/energy bins, Kaiser-sinc filters, Whisper sinusoid positions, DiffSVC step table) are built
+with torch-CPU float32 using the reference's own formulas, because that is how the reference
+materialises them before `.cuda()` (they are then bit-identical).
+
+`load_state_dict_checkpoint` is the loader for real checkpoints (utils/load_models.py:23-79) but,
+unlike the reference, it fails loudly on missing/mismatched keys.
+"""
+import math
+import zlib
+
+import numpy as np
+import torch
+
+# ----------------------------------------------------------------------------- helpers
+
+
+def _rng(seed, name):
+    return np.random.Generator(np.random.PCG64([int(seed) & 0xFFFFFFFF, zlib.crc32(name.encode())]))
+
+
+def _normal(seed, name, shape, std, mean=0.0):
+    a = _rng(seed, name).standard_normal(size=shape, dtype=np.float32)
+    a *= np.float32(std)
+    if mean:
+        a += np.float32(mean)
+    return a
+
+
+def _uniform(seed, name, shape, lo, hi):
+    return _rng(seed, name).uniform(lo, hi, size=shape).astype(np.float32)
+
+
+def note_to_hz(note):
+    """librosa.note_to_hz for the two notes the reference uses (modules/encoder.py:38-39)."""
+    midi = {"C1": 24, "C7": 96}[note]
+    return float(440.0 * (2.0 ** ((midi - 69.0) / 12.0)))
+
+
+# ----------------------------------------------------------------------------- buffers (torch-CPU f32)
+
+
+def melody_bins(n_bins):
+    """modules/encoder.py:47-57."""
+    f0_min, f0_max = note_to_hz("C1"), note_to_hz("C7")
+    return torch.exp(torch.linspace(np.log(f0_min - 0.1), np.log(f0_max), n_bins - 1))
+
+
+def energy_bins(n_bins):
+    """modules/encoder.py:89-102."""
+    return torch.exp(torch.linspace(np.log(1e-30), np.log(1.5), n_bins - 1))
+
+
+def step_embedding_table(max_steps):
+    """modules/diffsvc.py:45-54 (StepEncoder.build_embedding)."""
+    steps = torch.arange(max_steps).unsqueeze(1)
+    dims = torch.arange(64).unsqueeze(0)
+    table = steps * 10.0 ** (dims * 4.0 / 63.0)
+    return torch.cat([torch.sin(table), torch.cos(table)], dim=1)
+
+
+def kaiser_sinc_filter1d(cutoff, half_width, kernel_size):
+    """modules/bigvgan.py:162-193 -> [1,1,kernel_size] f32."""
+    even = kernel_size % 2 == 0
+    half_size = kernel_size // 2
+    delta_f = 4 * half_width
+    A = 2.285 * (half_size - 1) * math.pi * delta_f + 7.95
+    if A > 50.0:
+        beta = 0.1102 * (A - 8.7)
+    elif A >= 21.0:
+        beta = 0.5842 * (A - 21) ** 0.4 + 0.07886 * (A - 21.0)
+    else:
+        beta = 0.0
+    window = torch.kaiser_window(kernel_size, beta=beta, periodic=False)
+    if even:
+        time = torch.arange(-half_size, half_size) + 0.5
+    else:
+        time = torch.arange(kernel_size) - half_size
+    filt = 2 * cutoff * window * torch.sinc(2 * cutoff * time)
+    filt /= filt.sum()
+    return filt.view(1, 1, kernel_size)
+
+
+def sinusoids(length, channels, max_timescale=10000):
+    """utils/whisper_extractor/model.py:48-54."""
+    log_timescale_increment = np.log(max_timescale) / (channels // 2 - 1)
+    inv_timescales = torch.exp(-log_timescale_increment * torch.arange(channels // 2))
+    scaled_time = torch.arange(length)[:, np.newaxis] * inv_timescales[np.newaxis, :]
+    return torch.cat([torch.sin(scaled_time), torch.cos(scaled_time)], dim=1)
+
+
+def fade_out_table(n):
+    """modules/bigvgan_inference.py:37-39: torch.linspace(1, 0, steps=n) (f32)."""
+    return torch.linspace(1, 0, steps=n)
+
+
+# ----------------------------------------------------------------------------- random parameter sets
+
+
+def _conv(sd, seed, name, cout, cin, k, gain=1.0, bias_std=0.02):
+    sd[name + ".weight"] = _normal(seed, name + ".weight", (cout, cin, k), gain / math.sqrt(cin * k))
+    sd[name + ".bias"] = _normal(seed, name + ".bias", (cout,), bias_std)
+
+
+def _linear(sd, seed, name, cout, cin, gain=1.0, bias=True, bias_std=0.02):
+    sd[name + ".weight"] = _normal(seed, name + ".weight", (cout, cin), gain / math.sqrt(cin))
+    if bias:
+        sd[name + ".bias"] = _normal(seed, name + ".bias", (cout,), bias_std)
+
+
+def make_mapper_state(mcfg, seed=0):
+    """State dict of ModuleList([EncoderFramework, DiffSVC]) (utils/load_models.py:17-20;
+    modules/encoder.py:138-163; modules/diffsvc.py:240-282). DiffSVC.output_projection is zero-
+    initialised by the reference (diffsvc.py:282), which would make every epsilon prediction a
+    constant; here it is random like every other layer."""
+    sd = {}
+    C = mcfg.residual_channels
+    ct = mcfg.content_feature[0]
+    p = "0.registered_modules_dict."
+    _linear(sd, seed, p + f"content_{ct}.nn", mcfg.encoder_content_dim, mcfg.input_content_dim[ct])
+    sd[p + "melody.melody_bins"] = melody_bins(mcfg.n_bins_melody).numpy()
+    sd[p + "melody.nn.weight"] = _normal(seed, p + "melody.nn.weight", (mcfg.n_bins_melody, mcfg.encoder_melody_dim), 0.5)
+    sd[p + "loudness.energy_bins"] = energy_bins(mcfg.n_bins_loudness).numpy()
+    sd[p + "loudness.nn.weight"] = _normal(seed, p + "loudness.nn.weight", (mcfg.n_bins_loudness, mcfg.encoder_loudness_dim), 0.5)
+    sd[p + "singer.nn.weight"] = _normal(seed, p + "singer.nn.weight", (mcfg.singer_table_size, mcfg.encoder_singer_dim), 0.5)
+    q = "1."
+    _conv(sd, seed, q + "mel_preprocess.projection", C, mcfg.n_mel, 1, gain=math.sqrt(2.0))
+    _linear(sd, seed, q + "diffusion_embedding.projection1", mcfg.diffusion_fc_size, 128)
+    _linear(sd, seed, q + "diffusion_embedding.projection2", mcfg.diffusion_fc_size, mcfg.diffusion_fc_size)
+    for i in range(mcfg.residual_layer_num):
+        r = q + f"residual_layers.{i}."
+        _conv(sd, seed, r + "dilated_conv", 2 * C, C, mcfg.residual_kernel_size)
+        _linear(sd, seed, r + "diffusion_projection", C, mcfg.diffusion_fc_size)
+        _conv(sd, seed, r + "conditioner_projection", 2 * C, mcfg.conditioner_size, 1)
+        _conv(sd, seed, r + "output_projection", 2 * C, C, 1)
+    _conv(sd, seed, q + "skip_projection", C, C, 1, gain=math.sqrt(2.0))
+    _conv(sd, seed, q + "output_projection", mcfg.n_mel, C, 1)
+    return sd
+
+
+def _wn_conv(sd, seed, name, w_shape, fan_in, bias_n):
+    """weight_norm(Conv) params: weight_g [dim0,1,1], weight_v, bias (modules/bigvgan.py:529-593)."""
+    v = _normal(seed, name + ".weight_v", w_shape, 1.0 / math.sqrt(fan_in))
+    norm = np.sqrt((v.astype(np.float64) ** 2).reshape(w_shape[0], -1).sum(1)).astype(np.float32)
+    g = norm * _uniform(seed, name + ".weight_g", (w_shape[0],), 0.8, 1.2)
+    sd[name + ".weight_v"] = v
+    sd[name + ".weight_g"] = g.reshape(w_shape[0], 1, 1)
+    sd[name + ".bias"] = _normal(seed, name + ".bias", (bias_n,), 0.02)
+
+
+def _act(sd, seed, name, ch):
+    f = kaiser_sinc_filter1d(0.25, 0.3, 12).numpy()
+    sd[name + ".act.alpha"] = _normal(seed, name + ".act.alpha", (ch,), 0.3)
+    sd[name + ".act.beta"] = _normal(seed, name + ".act.beta", (ch,), 0.3)
+    sd[name + ".upsample.filter"] = f.copy()
+    sd[name + ".downsample.lowpass.filter"] = f.copy()
+
+
+def make_vocoder_state(vcfg, seed=0):
+    """State dict of bigvgan.Generator (modules/bigvgan.py:519-598), AMPBlock1 + SnakeBeta."""
+    assert vcfg.resblock == "1" and vcfg.activation == "snakebeta"
+    sd = {}
+    C0 = vcfg.upsample_initial_channel
+    _wn_conv(sd, seed, "conv_pre", (C0, vcfg.input_dim, 7), vcfg.input_dim * 7, C0)
+    nk = len(vcfg.resblock_kernel_sizes)
+    for i, (u, k) in enumerate(zip(vcfg.upsample_rates, vcfg.upsample_kernel_sizes)):
+        cin, cout = C0 // (2 ** i), C0 // (2 ** (i + 1))
+        _wn_conv(sd, seed, f"ups.{i}.0", (cin, cout, k), cin * k // u, cout)
+    for i in range(len(vcfg.upsample_rates)):
+        ch = C0 // (2 ** (i + 1))
+        for j, (k, d) in enumerate(zip(vcfg.resblock_kernel_sizes, vcfg.resblock_dilation_sizes)):
+            rb = f"resblocks.{i * nk + j}."
+            for l in range(len(d)):
+                _wn_conv(sd, seed, rb + f"convs1.{l}", (ch, ch, k), ch * k, ch)
+                _wn_conv(sd, seed, rb + f"convs2.{l}", (ch, ch, k), ch * k, ch)
+            for a in range(2 * len(d)):
+                _act(sd, seed, rb + f"activations.{a}", ch)
+    ch = C0 // (2 ** len(vcfg.upsample_rates))
+    _act(sd, seed, "activation_post", ch)
+    _wn_conv(sd, seed, "conv_post", (1, ch, 7), ch * 7, 1)
+    return sd
+
+
+WHISPER_DIMS = {
+    # utils/whisper_extractor/__init__.py:18-30 model table; medium = n_audio_state 1024, 16 heads, 24 layers
+    "medium": dict(n_mels=80, n_audio_ctx=1500, n_audio_state=1024, n_audio_head=16, n_audio_layer=24),
+    "tiny-test": dict(n_mels=80, n_audio_ctx=1500, n_audio_state=128, n_audio_head=2, n_audio_layer=2),
+}
+
+
+def make_whisper_state(dims, seed=0):
+    """State dict of AudioEncoder with the 'encoder.' prefix Whisper uses
+    (utils/whisper_extractor/model.py:132-142, 104-116)."""
+    sd = {}
+    D, L = dims["n_audio_state"], dims["n_audio_layer"]
+    p = "encoder."
+    _conv(sd, seed, p + "conv1", D, dims["n_mels"], 3)
+    _conv(sd, seed, p + "conv2", D, D, 3)
+    sd[p + "positional_embedding"] = sinusoids(dims["n_audio_ctx"], D).numpy()
+    for i in range(L):
+        b = p + f"blocks.{i}."
+        _linear(sd, seed, b + "attn.query", D, D)
+        _linear(sd, seed, b + "attn.key", D, D, bias=False)
+        _linear(sd, seed, b + "attn.value", D, D)
+        _linear(sd, seed, b + "attn.out", D, D, gain=0.5)
+        for ln in ("attn_ln", "mlp_ln"):
+            sd[b + ln + ".weight"] = _normal(seed, b + ln + ".weight", (D,), 0.05, mean=1.0)
+            sd[b + ln + ".bias"] = _normal(seed, b + ln + ".bias", (D,), 0.02)
+        _linear(sd, seed, b + "mlp.0", 4 * D, D)
+        _linear(sd, seed, b + "mlp.2", D, 4 * D, gain=0.5)
+    sd[p + "ln_post.weight"] = _normal(seed, p + "ln_post.weight", (D,), 0.05, mean=1.0)
+    sd[p + "ln_post.bias"] = _normal(seed, p + "ln_post.bias", (D,), 0.02)
+    return sd
+
+
+def whisper_dims_from_state(sd):
+    D = sd["encoder.conv1.weight"].shape[0]
+    n_layer = 1 + max(int(k.split(".")[2]) for k in sd if k.startswith("encoder.blocks."))
+    return dict(n_mels=sd["encoder.conv1.weight"].shape[1], n_audio_ctx=sd["encoder.positional_embedding"].shape[0],
+                n_audio_state=D, n_audio_head=D // 64, n_audio_layer=n_layer)
+
+
+# ----------------------------------------------------------------------------- real checkpoints (F2)
+
+
+def load_state_dict_checkpoint(path, key, expected):
+    """utils/load_models.py:23-79 semantics (strip 'module.'), but every expected key must be present
+    with the expected shape, or ValueError is raised (the reference silently keeps random init)."""
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    sd = ckpt[key] if key else ckpt
+    sd = {k.split("module.")[-1]: v for k, v in sd.items()}
+    missing = [k for k in expected if k not in sd]
+    bad = [k for k in expected if k in sd and tuple(sd[k].shape) != tuple(expected[k].shape)]
+    if missing or bad:
+        raise ValueError(f"checkpoint {path}: missing {missing[:5]}..., shape-mismatch {bad[:5]}...")
+    return {k: sd[k].float().numpy() for k in expected}
