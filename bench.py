@@ -1,0 +1,168 @@
+"""Throughput benchmark: converted audio seconds per second (RTF^-1), end-to-end, 10 s clips.
+
+BASELINE.json configs[1]: batch = 32 synthetic 10 s clips per GPU, Whisper-medium content + 100-step
+DiffSVC (the reference's PLMS path, speedup 10 = 101 denoiser calls) + BigVGAN. One "step" = the
+whole hot path over one batch already resident in HBM: mel/energy, Praat-AC F0, pitch shift,
+Whisper log-mel + encoder, content map, conditioner, PLMS-100 sampler, de-normalisation, BigVGAN,
+fade-out, and (N > 1) the RCCL gather of every rank's waveforms to rank 0.
+
+    python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torch.distributed.run)
+
+Weights are seeded random tensors of the reference architectures (no checkpoints offline); inputs
+are synthetic harmonic clips. Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from svc_inference_pipeline_amd import _lib  # noqa: E402
+from svc_inference_pipeline_amd import config as C  # noqa: E402
+from svc_inference_pipeline_amd import weights as W  # noqa: E402
+from svc_inference_pipeline_amd.parallel import DistContext  # noqa: E402
+from svc_inference_pipeline_amd.pipeline import SVCPipeline  # noqa: E402
+from svc_inference_pipeline_amd.runtime import SVCEngine  # noqa: E402
+
+PEAK_F16_TFLOPS = 2500.0   # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E spec
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def synth_inputs(uids, seconds):
+    from svc_inference_pipeline_amd.synth import synth_clip, synth_clip_16k_quantised
+    w24 = np.stack([synth_clip(int(u), seconds, 24000) for u in uids])
+    w16 = np.stack([synth_clip_16k_quantised(int(u), seconds) for u in uids])
+    return w24, w16
+
+
+def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads):
+    """The oracle (CPU restatement of the reference path, torch-CPU fp32) on ONE clip of the same
+    workload, timed on this host: mel/energy, F0, pitch shift, Whisper-medium, map, conditioner,
+    PLMS (speedup 10 = 101 denoiser calls), de-normalisation, BigVGAN, fade."""
+    from oracle import pipeline as OP
+    torch.set_num_threads(threads)
+    w24, w16 = synth_inputs([0], seconds)
+    t0 = time.time()
+    OP.convert(cfg, ws, ms, vs, w24[0], w16[0], singer=1, speedup=speedup, seed=0)
+    dt = time.time() - t0
+    return {"value": round(seconds / dt, 4), "unit": "audio-s/s", "cores": threads, "kind": "port",
+            "sample": f"1 x {seconds:g} s clip, full oracle path (PLMS speedup {speedup}), torch-CPU fp32, {threads} threads, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
+    ap.add_argument("--seconds", type=float, default=10.0)
+    ap.add_argument("--speedup", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    args = ap.parse_args()
+
+    dist = DistContext.from_env()
+    torch.cuda.set_device(dist.local_rank)
+    cfg = C.load_config()
+    t_setup = time.time()
+    ws = W.make_whisper_state(W.WHISPER_DIMS["medium"], seed=0)
+    ms = W.make_mapper_state(cfg.mapper, seed=0)
+    vs = W.make_vocoder_state(cfg.vocoder, seed=0)
+    eng = SVCEngine(cfg, dist.local_rank, whisper_state=ws, mapper_state=ms, vocoder_state=vs)
+    pipe = SVCPipeline(eng)
+    B = args.batch
+    uids = np.arange(dist.rank * B, (dist.rank + 1) * B)
+    w24, w16 = synth_inputs(uids, args.seconds)
+    d24 = torch.from_numpy(w24).cuda()
+    d16 = torch.from_numpy(w16).cuda()
+    singer = torch.from_numpy((uids % 5).astype(np.int32)).cuda()
+    utt = torch.from_numpy(uids.astype(np.int32)).cuda()
+    log(f"rank {dist.rank}/{dist.world}: setup {time.time() - t_setup:.1f}s, weights {eng.memory()[0] / 1e9:.2f} GB")
+
+    def step():
+        res = pipe.convert(d24, d16, singer, fast_inference=True, speedup=args.speedup, seed=1234, utt_ids=utt)
+        return dist.gather_waveforms(res.wav)
+
+    for i in range(args.warmup):
+        step()
+        torch.cuda.synchronize()
+        log(f"warmup {i + 1}/{args.warmup}")
+    dist.barrier()
+    torch.cuda.synchronize()
+    _lib.profile_enable(True)
+    t0 = time.time()
+    for i in range(args.steps):
+        out = step()
+        torch.cuda.synchronize()
+        log(f"step {i + 1}/{args.steps} {time.time() - t0:.2f}s")
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = dist.max_over_ranks(time.time() - t0)
+    prof = _lib.profile_read()
+    _lib.profile_enable(False)
+    ms_per_step = 1000.0 * elapsed / args.steps
+    audio_s = dist.world * B * args.seconds
+    value = audio_s / (elapsed / args.steps)
+    if out is not None:
+        assert out.shape[0] == dist.world * B and bool(torch.isfinite(out).all())
+
+    # roofline for the dominant kernel (largest share of measured kernel time)
+    dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    per_launch_s = dom["ms"] / 1000.0 / dom["launches"]
+    if dom["flops"] > 0:
+        achieved = dom["flops"] / dom["launches"] / per_launch_s / 1e12
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s"}
+    else:
+        achieved = dom["bytes"] / dom["launches"] / per_launch_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
+    roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+    roof["kernel"] = dom_name
+    roof["avg_launch_us"] = round(per_launch_s * 1e6, 2)
+    roof["share_of_kernel_time"] = round(dom["ms"] / sum(v["ms"] for v in prof.values()), 3)
+    roof["traffic"] = None
+    if os.path.exists(args.pmc_json):
+        pmc = json.load(open(args.pmc_json))
+        if dom_name in pmc.get("kernels", {}):
+            roof["traffic"] = pmc["kernels"][dom_name].get("hbm_bytes_per_launch")
+    total_flops = sum(v["flops"] for v in prof.values()) / args.steps
+    kernels = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] // args.steps,
+                   "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 1) if v["flops"] else None,
+                   "gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1) if v["bytes"] else None}
+               for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+
+    cpu = None
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        log("cpu baseline (oracle, 1 clip)...")
+        cpu = cpu_baseline(cfg, ws, ms, vs, args.seconds, args.speedup, args.cpu_threads)
+    if dist.rank == 0:
+        line = {
+            "metric": "converted audio sec/sec (RTF^-1) end-to-end, 10 s clips",
+            "value": round(value, 2), "unit": "audio-s/s", "n_gpus": dist.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
+            "config": {"workload": f"batch={B}/GPU x {args.seconds:g} s synthetic clips, Whisper-medium + PLMS-100 "
+                                   f"DiffSVC (speedup {args.speedup}) + BigVGAN, fp16 MFMA operands / fp32 accumulate",
+                       "global_batch": dist.world * B, "seq_len_frames": int(d24.shape[1] // 256 - 2),
+                       "parallelism": f"dp{dist.world} (per-utterance shards, RCCL gather)"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "algorithmic_tflops_per_step": round(total_flops / 1e12, 2),
+            "sustained_tflops": round(total_flops / 1e12 / (ms_per_step / 1000.0), 1),
+            "kernels": kernels,
+        }
+        print(json.dumps(line), flush=True)
+    dist.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,120 @@
+/*
+ * svc_hip.h — C-ABI of libsvc_hip.so, the MI355X (gfx950) singing-voice-conversion hot path.
+ *
+ * The reference (WallaceRao/svc_inference_pipeline) has no FFI: its boundary is the set of Python
+ * functions infer.py calls. Each entry point below replaces one of them (file:line in the reference):
+ *
+ *   svc_mel_energy      <- utils/mel.py:179-201 extract_mel_features (mel_spectrogram :130-174, energy :199)
+ *   svc_f0_ac           <- utils/f0.py:120-161 get_f0_features_using_parselmouth (Praat to_pitch_ac + pad)
+ *   svc_pitch_shift     <- utils/acoustic_feature_extraction.py:48-52 pitch_shift
+ *   svc_whisper_encode  <- utils/whisper.py:13-28 whisper_encoder (log_mel_spectrogram + AudioEncoder)
+ *   svc_map_content     <- utils/whisper.py:31-81 get_mapped_whisper_features
+ *   svc_condition       <- modules/encoder.py:165-201 EncoderFramework.forward
+ *   svc_diffsvc_sample  <- modules/diffsvcrepo_inference.py:154-240 svc_model_inference (DDPM or PLMS)
+ *   svc_bigvgan         <- utils/acoustic_feature_extraction.py:83-97 denormalize_mel_channel
+ *                          + modules/bigvgan_inference.py:29-44 synthesis_audios (Generator + trim + fade)
+ *
+ * Conventions
+ *   - Tensors are caller-owned DEVICE buffers, time-major: row = b*T + t, channels contiguous.
+ *   - Every call is asynchronous and ordered on `stream` (a hipStream_t; NULL = default stream).
+ *   - One context per device; a context is not thread-safe.
+ *   - Parameters are given in the reference's own state_dict naming with a model prefix
+ *     ("mapper.", "vocoder.", "whisper.") as host float32 arrays; they are folded (weight_norm),
+ *     packed into MFMA layouts and uploaded by svc_ctx_finalize. Host arrays must stay valid until
+ *     svc_ctx_finalize returns. A missing or mis-shaped parameter makes finalize fail (the reference
+ *     silently keeps random init, utils/load_models.py:34-43).
+ *   - Status codes instead of exceptions; svc_last_error() describes the last failure of this thread.
+ */
+#ifndef SVC_HIP_H
+#define SVC_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct svc_ctx svc_ctx;
+typedef int svc_status; /* 0 = ok, 1 = invalid argument, 2 = HIP error, 3 = bad state */
+
+#define SVC_MODE_DDPM 0
+#define SVC_MODE_PLMS 1
+
+const char* svc_last_error(void);
+int svc_abi_version(void);
+
+svc_status svc_ctx_create(int device, svc_ctx** out);
+svc_status svc_ctx_destroy(svc_ctx* ctx);
+/* numeric configuration (config.json keys): e.g. "mapper.residual_layer_num", "fs", "vocoder.n_stages" */
+svc_status svc_ctx_set_config(svc_ctx* ctx, const char* key, double value);
+svc_status svc_ctx_add_param(svc_ctx* ctx, const char* name, const float* host, int ndim, const int64_t* shape);
+svc_status svc_ctx_finalize(svc_ctx* ctx);
+/* bytes of device memory held by packed weights / by the workspace arena */
+svc_status svc_ctx_memory(svc_ctx* ctx, int64_t* weight_bytes, int64_t* workspace_bytes);
+
+/* A2/A3-energy: wav24k [B][n_samples] f32 -> mel [B*T][n_mels] f32 (log-mel, time-major), energy [B*T] f32.
+   T = (n_samples + n_fft - hop - n_fft)/hop + 1 (bit-exact frame count, utils/mel.py:148-167). */
+svc_status svc_mel_energy(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, float* mel, float* energy,
+                          void* stream);
+
+/* A3-F0: Praat autocorrelation pitch (to_pitch_ac, voicing 0.6, floor f0_min, ceiling f0_max, time step hop/fs),
+   padded to T frames as utils/f0.py:156-157; unvoiced = 0. f0 [B*T] float64. */
+svc_status svc_f0_ac(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, int T, double* f0, void* stream);
+
+/* A4: in place, f0 [B*T] float64 *= target_median / median(voiced f0 of that utterance)
+   (utils/acoustic_feature_extraction.py:33-52; np.median semantics, NaN when no frame is voiced). */
+svc_status svc_pitch_shift(svc_ctx* ctx, double* f0, int B, int T, double target_median, void* stream);
+
+/* A5+A6: wav16k [B][n_samples] f32 (int16-quantised, <= 480000 samples; zero-padded to 30 s)
+   -> Whisper encoder output feats [B*n_ctx][n_state] f32. */
+svc_status svc_whisper_encode(svc_ctx* ctx, const float* wav16k, int B, int64_t n_samples, float* feats, void* stream);
+
+/* A7: feats [B*src_rows][D] f32 -> content [B*T][D] f16 (IEEE binary16 bits), 15:8 repeat/average. T <= 2812. */
+svc_status svc_map_content(svc_ctx* ctx, const float* feats, int B, int src_rows, int T, int D, void* content_f16,
+                           void* stream);
+
+/* A10: content f16 [B*T][D], f0 f64 [B*T], energy f32 [B*T], singer int32 [B] -> cond f32 [B*T][384]. */
+svc_status svc_condition(svc_ctx* ctx, const void* content_f16, const double* f0, const float* energy,
+                         const int32_t* singer, int B, int T, float* cond, void* stream);
+
+/* A11+A12: cond f32 [B*T][384] -> x_0 f32 [B*T][n_mel] (normalised mel, time-major).
+   mode SVC_MODE_DDPM: `interval` ignored, 1000 steps; SVC_MODE_PLMS: reference speedup (e.g. 10).
+   x_T f32 [B*T][n_mel] or NULL (then drawn on device from `seed` and `utt_ids`).
+   noise (DDPM only) f32 [steps][B*T][n_mel] (already in time-major order) or NULL (device Philox noise). */
+svc_status svc_diffsvc_sample(svc_ctx* ctx, const float* cond, int B, int T, int mode, int interval, const float* x_T,
+                              const float* noise, uint64_t seed, const int32_t* utt_ids, float* x0, void* stream);
+
+/* single epsilon prediction (DiffSVC.forward, modules/diffsvc.py:284-321) for testing: x f32 [B*T][n_mel], step t */
+svc_status svc_diffsvc_eps(svc_ctx* ctx, const float* cond, const float* x, int B, int T, int t, float* eps,
+                           void* stream);
+
+/* A13+A14+A15: x0 f32 [B*T][n_mel] (normalised) -> wav [B][T*256] f32 (denorm, Generator, tanh, fade-out).
+   mel_denorm_out (optional, f32 [B*T][n_mel]) receives the de-normalised mel. */
+svc_status svc_bigvgan(svc_ctx* ctx, const float* x0, int B, int T, float* wav, float* mel_denorm_out, void* stream);
+
+/* ---------------- op-level entry points (used by the parity tests; weights are unpacked f32 device arrays) */
+/* y[B*T_out][Cout] = conv1d(x[B*T_in][Cin]) ; w [Cout][Cin][k] ; act 0 none / 1 gelu / 2 relu */
+svc_status svc_op_conv1d(const float* x, int B, int T_in, int Cin, const float* w, const float* bias, int Cout, int k,
+                         int stride, int dilation, int pad, int act, float* y, void* stream);
+/* ConvTranspose1d, w [Cin][Cout][k]; T_out = (T_in-1)*stride - 2*pad + k */
+svc_status svc_op_conv_transpose1d(const float* x, int B, int T_in, int Cin, const float* w, const float* bias,
+                                   int Cout, int k, int stride, int pad, float* y, void* stream);
+/* Activation1d(SnakeBeta, logscale): x f32 [B*L][C] -> y f32 [B*L][C] */
+svc_status svc_op_activation1d(const float* x, int B, int L, int C, const float* alpha_log, const float* beta_log,
+                               const float* filt12, float* y, void* stream);
+/* attention on f32 q,k,v [B*L][D] (already projected; scaled inside by dh^-1/4 each) -> out f32 [B*L][D] */
+svc_status svc_op_attention(const float* q, const float* k, const float* v, int B, int L, int D, float* out,
+                            void* stream);
+svc_status svc_op_layernorm(const float* x, const float* g, const float* b, int rows, int D, float* y, void* stream);
+/* live per-kernel timing: enable(1) clears and starts recording (hipEvents around each launch),
+   read(idx, ...) synchronises and returns kernel idx's name, total ms, launches, algorithmic FLOPs/bytes;
+   n_kernels receives the number of distinct kernels. */
+svc_status svc_profile_enable(int enable);
+svc_status svc_profile_read(int idx, char* name, int name_len, double* total_ms, int64_t* launches, double* flops,
+                            double* bytes, int* n_kernels);
+/* slaney mel filterbank (librosa.filters.mel, htk=False, norm='slaney') computed natively, host output */
+svc_status svc_mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double fmax, float* out_host);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

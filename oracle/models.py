@@ -229,3 +229,33 @@ def bigvgan_forward(sd, vcfg, mel):
     x = _act(sd, "activation_post", x)
     x = F.conv1d(x, _wn(sd, "conv_post"), _t(sd, "conv_post.bias"), padding=3)
     return torch.tanh(x)
+
+
+# ============================================================================ fp16-operand emulation
+class Fp16Operands:
+    """Context manager: dense convolutions round their input and weight to binary16 (fp32 accumulate),
+    emulating the MFMA operand precision of the HIP path. Used to derive tolerances for chaotic
+    random-weight regimes (tests/test_gpu_stages.py::test_bigvgan); depthwise (grouped) convs are
+    untouched because the HIP path computes them in fp32."""
+
+    def __enter__(self):
+        self._c, self._t = F.conv1d, F.conv_transpose1d
+        r = lambda t: t.half().float()
+        c, tr = self._c, self._t
+
+        def conv1d(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+            if groups > 1:
+                return c(x, w, b, stride, padding, dilation, groups)
+            return c(r(x), r(w), b, stride, padding, dilation, groups)
+
+        def conv_t(x, w, b=None, stride=1, padding=0, output_padding=0, groups=1, dilation=1):
+            if groups > 1:
+                return tr(x, w, b, stride, padding, output_padding, groups, dilation)
+            return tr(r(x), r(w), b, stride, padding, output_padding, groups, dilation)
+
+        F.conv1d, F.conv_transpose1d = conv1d, conv_t
+        return self
+
+    def __exit__(self, *a):
+        F.conv1d, F.conv_transpose1d = self._c, self._t
+        return False

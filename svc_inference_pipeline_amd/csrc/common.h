@@ -1,0 +1,114 @@
+// Shared definitions for the gfx950 (MI355X / CDNA4) SVC kernels.
+// Layout convention for every activation tensor on the device: TIME-MAJOR ("channels-last"),
+// row = b * T + t, channels contiguous. This makes every Conv1d an implicit GEMM whose A-operand
+// rows are contiguous channel vectors (see gemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 f16;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+#define SVC_OK 0
+#define SVC_ERR_INVALID 1
+#define SVC_ERR_HIP 2
+#define SVC_ERR_STATE 3
+
+namespace svc {
+
+void set_error(const char* fmt, ...);
+const char* get_error();
+
+#define SVC_HIP_CHECK(expr)                                                              \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess) {                                                              \
+      ::svc::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
+      return SVC_ERR_HIP;                                                                \
+    }                                                                                    \
+  } while (0)
+
+#define SVC_REQUIRE(cond, ...)        \
+  do {                                \
+    if (!(cond)) {                    \
+      ::svc::set_error(__VA_ARGS__);  \
+      return SVC_ERR_INVALID;         \
+    }                                 \
+  } while (0)
+
+#define SVC_LAUNCH_CHECK()                                                          \
+  do {                                                                              \
+    hipError_t _e = hipGetLastError();                                              \
+    if (_e != hipSuccess) {                                                         \
+      ::svc::set_error("%s:%d launch failed: %s", __FILE__, __LINE__, hipGetErrorString(_e)); \
+      return SVC_ERR_HIP;                                                           \
+    }                                                                               \
+  } while (0)
+
+static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
+static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ------------------------------------------------------------------ implicit-GEMM descriptors
+// Y[m, n] = epilogue( sum_{tap, c} X[in_row(m, tap), c] * Wp[n, tap*Cp + c] )
+//   m = b*T_out + t  (b < B, t < T_out);   in_row = b*T_in + t*istride + tap*tap_mul + tap_add
+//   rows outside [0, T_in) of utterance b read as zero (Conv1d zero padding, per utterance).
+struct ConvGemmArgs {
+  const f16* X;  // [B*T_in rows][ldx] f16
+  int ldx;       // row stride (elements), multiple of 8
+  int T_in;
+  int Cp;        // channels per tap in the K index (multiple of 8)
+  int Cvalid;    // channels >= Cvalid read as zero
+  const f16* W;  // packed [Npad][Kpad]
+  int K;         // ntaps * Cp
+  int Kpad;      // multiple of 64
+  int tap_mul, tap_add, istride;
+  int B, T_out;
+  int N;         // valid (packed) output columns
+  int ntiles_n;
+};
+
+// Epilogue kinds (runtime-selected inside one kernel family)
+enum EpiKind : int {
+  EPI_GENERIC = 0,  // v = act(acc + bias[n]) (*col_scale) (+add_t) (+add_row) ((acc32+v)/acc_div)
+  EPI_GATE = 1,     // DiffSVC: sigmoid(gate+cp) * tanh(filter+cp)          (paired columns)
+  EPI_RESSKIP = 2,  // DiffSVC: x=(x+res)/sqrt2 ; skip(+)=sk ; next-layer f16 input (paired columns)
+  EPI_COND = 3,     // conditioner: acc + bias + emb_m[idx_m] + emb_l[idx_l] + emb_s[singer]
+};
+
+enum ActKind : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2 };
+
+struct EpiArgs {
+  int kind;
+  const float* bias;  // [Npad] packed order
+  int act;
+  // output row mapping: orow = b*T_ostore + t*ostride + ophase
+  int T_ostore, ostride, ophase;
+  float* out32; int ld32;                   // f32 output (may alias acc32 / add_row element-wise)
+  const float* acc32; int ld_acc; float acc_div;  // v = (acc32[orow][n] + v) / acc_div   (resblock mean)
+  f16* out16; int ld16; const float* add16; // out16 = f16(v + add16[n])  (next-layer input)
+  const float* add_t; int ld_add_t;         // added after act, indexed by t (positional embedding)
+  const float* add_row; int ld_add_row;     // added after act, indexed by orow (residual input)
+  int scale_cols; float col_scale;          // columns < scale_cols multiplied by col_scale (q/k scaling)
+  // DiffSVC gate / residual-skip
+  const f16* cp; int ld_cp;                 // conditioner projection (packed order, bias folded)
+  float* x32; float* skip32; int ldx32;     // residual stream and skip accumulator [rows][C]
+  const float* dnext;                       // next layer diffusion projection [C] (shared by batch) or null
+  f16* y16; int ldy16;                      // next layer input f16
+  int skip_first, last_layer; float skip_scale;
+  // conditioner
+  const int* idx_m; const int* idx_l; const int* singer;
+  const float* emb_m; const float* emb_l; const float* emb_s; int ld_emb;
+};
+
+int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
+
+// live per-kernel timing (bench roofline): when enabled, launches are bracketed by hipEvents and
+// aggregated by kernel name together with their algorithmic FLOPs / bytes.
+int prof_begin(const char* name, double flops, double bytes, hipStream_t s);  // returns token or -1
+void prof_end(int token, hipStream_t s);
+
+}  // namespace svc

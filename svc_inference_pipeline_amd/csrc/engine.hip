@@ -1,0 +1,1547 @@
+// Native runtime of the SVC hot path: context, weight packing (weight_norm fold, MFMA layouts),
+// device workspace arena and the stage orchestration behind the C-ABI (include/svc_hip.h).
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/svc_hip.h"
+#include "common.h"
+
+namespace svc {
+
+// ---------------------------------------------------------------------------- errors
+static thread_local char g_err[1024] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+const char* get_error() { return g_err; }
+
+// ---------------------------------------------------------------------------- live profiling
+struct ProfRec {
+  std::string name;
+  hipEvent_t a, b;
+  double flops, bytes;
+};
+static bool g_prof = false;
+static std::vector<ProfRec> g_prof_recs;
+static std::vector<hipEvent_t> g_ev_pool;
+
+static hipEvent_t ev_get() {
+  if (!g_ev_pool.empty()) {
+    hipEvent_t e = g_ev_pool.back();
+    g_ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+int prof_begin(const char* name, double flops, double bytes, hipStream_t s) {
+  if (!g_prof) return -1;
+  ProfRec r{name, ev_get(), ev_get(), flops, bytes};
+  if (!r.a || !r.b) return -1;
+  (void)hipEventRecord(r.a, s);
+  g_prof_recs.push_back(r);
+  return (int)g_prof_recs.size() - 1;
+}
+
+void prof_end(int tok, hipStream_t s) {
+  if (tok >= 0 && tok < (int)g_prof_recs.size()) (void)hipEventRecord(g_prof_recs[tok].b, s);
+}
+
+// kernels in other translation units
+int attention(const f16* qkv, f16* out, int B, int L, int D, hipStream_t s);
+int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int rows, int D, int ldy, hipStream_t s);
+int layernorm_f32(const float* x, const float* g, const float* b, float* y, int rows, int D, int ldy, hipStream_t s);
+int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const float* alpha_log, const float* beta_log,
+                 const float* filt, hipStream_t s);
+int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s);
+int denorm_mel(const float* x, f16* y, float* y32, int ldy, int rows, int C, const float* mn, const float* mx,
+               hipStream_t s);
+int content_map(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst, hipStream_t s);
+int bucketize(const double* f0, const float* en, const float* mbins, const float* ebins, int nb, int* im, int* ie,
+              int n, hipStream_t s);
+struct PlmsArgs {
+  const float* e[4]; float c[4]; int ne; float div;
+  float d, A, Bc;
+  const float* xin;
+  float* xout; f16* x16; int ld16;
+  float* e_avg_out;
+};
+int plms_update(const PlmsArgs& p, int rows, int C, hipStream_t s);
+struct DdpmArgs {
+  float sra, srm1, c1, c2, sigma;
+  const float* z; uint64_t seed; const int* utt_ids; int step;
+};
+int ddpm_update(float* x, const float* eps, f16* x16, int ld16, int B, int T, int C, const DdpmArgs& a, hipStream_t s);
+int init_noise(float* x, f16* x16, int ld16, int B, int T, int C, uint64_t seed, const int* utt_ids, float std,
+               hipStream_t s);
+int conv_post(const f16* a, int lda, int B, int L, int C, const float* w, float bias, const float* fade, int nfade,
+              float* out, hipStream_t s);
+struct DftArgs {
+  const float* wav; int64_t wav_stride; int64_t n_valid; int64_t n_logical;
+  int n_fft, hop, pad, n_frames, nbins;
+  const float* window; int mode; float* out;
+};
+int dft_frames(const DftArgs& a, int B, hipStream_t s);
+int mel_log(const float* spec, int nbins, const float* fb, int n_mels, float* out, int rows, int mode, hipStream_t s);
+int energy_from_mel(const float* mel, int n_mels, float* en, int rows, hipStream_t s);
+int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s);
+int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
+int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
+int pack_qkv(const float* q, const float* k, const float* v, f16* qkv, int64_t rows, int D, float scale, hipStream_t s);
+int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double time_step, double floor_hz,
+                double ceiling_hz, double voicing_threshold, int T, double* f0_out, void* workspace, size_t ws_bytes,
+                hipStream_t s);
+size_t f0_workspace_bytes(int B, int64_t n_samples, double fs, double time_step, double floor_hz);
+
+// ---------------------------------------------------------------------------- host helpers
+static std::vector<float> slaney_mel(int sr, int n_fft, int n_mels, double f_lo, double f_hi) {
+  auto hz2mel = [](double f) {
+    const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = log(6.4) / 27.0;
+    return f >= min_log_hz ? min_log_mel + log(f / min_log_hz) / logstep : f / f_sp;
+  };
+  auto mel2hz = [](double m) {
+    const double f_sp = 200.0 / 3, min_log_hz = 1000.0, min_log_mel = min_log_hz / f_sp, logstep = log(6.4) / 27.0;
+    return m >= min_log_mel ? min_log_hz * exp(logstep * (m - min_log_mel)) : f_sp * m;
+  };
+  const int nb = 1 + n_fft / 2;
+  std::vector<double> fftf(nb), melf(n_mels + 2);
+  // np.fft.rfftfreq(n, 1/sr) = k * (1 / (n * (1/sr)))
+  const double val = 1.0 / ((double)n_fft * (1.0 / (double)sr));
+  for (int k = 0; k < nb; ++k) fftf[k] = k * val;
+  const double m0 = hz2mel(f_lo), m1 = hz2mel(f_hi);
+  // np.linspace(start, stop, num): step = (stop-start)/(num-1); y = arange*step + start; y[-1] = stop
+  const int num = n_mels + 2;
+  const double step = (m1 - m0) / (num - 1);
+  for (int i = 0; i < num; ++i) melf[i] = mel2hz(i == num - 1 ? m1 : i * step + m0);
+  std::vector<float> w((size_t)n_mels * nb);
+  for (int i = 0; i < n_mels; ++i) {
+    const double fd0 = melf[i + 1] - melf[i], fd1 = melf[i + 2] - melf[i + 1];
+    const double enorm = 2.0 / (melf[i + 2] - melf[i]);
+    for (int k = 0; k < nb; ++k) {
+      double lower = -(melf[i] - fftf[k]) / fd0;
+      double upper = (melf[i + 2] - fftf[k]) / fd1;
+      double v = fmax(0.0, fmin(lower, upper));
+      float vf = (float)v;                      // weights[i] = ... stored in the f32 array
+      w[(size_t)i * nb + k] = (float)((double)vf * enorm);  // weights *= enorm (f32 *= f64)
+    }
+  }
+  return w;
+}
+
+static std::vector<float> hann_periodic(int n) {
+  std::vector<float> w(n);
+  for (int j = 0; j < n; ++j) w[j] = (float)(0.5 - 0.5 * cos(2.0 * M_PI * j / n));
+  return w;
+}
+
+// ---------------------------------------------------------------------------- arena
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, off = 0, peak = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= cap) return SVC_OK;
+    if (base) SVC_HIP_CHECK(hipFree(base));
+    base = nullptr;
+    cap = 0;
+    SVC_HIP_CHECK(hipMalloc(&base, bytes));
+    cap = bytes;
+    return SVC_OK;
+  }
+  void reset() { off = 0; }
+  template <typename T>
+  T* get(size_t n) {
+    size_t bytes = (n * sizeof(T) + 255) & ~(size_t)255;
+    if (off + bytes > cap) return nullptr;
+    T* p = reinterpret_cast<T*>(base + off);
+    off += bytes;
+    if (off > peak) peak = off;
+    return p;
+  }
+};
+
+struct PackedGemm {
+  f16* W = nullptr;
+  float* bias = nullptr;
+  int N = 0, Npad = 0, K = 0, Kpad = 0, Cp = 0, Cin = 0, taps = 0;
+  int tap_mul = 1, tap_add = 0, istride = 1;
+};
+
+struct Param {
+  const float* host = nullptr;
+  std::vector<int64_t> shape;
+  int64_t numel = 0;
+};
+
+struct WBlock {
+  float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+  PackedGemm qkv, out, fc1, fc2;
+};
+
+struct ActP {
+  float *alpha, *beta, *filt;
+};
+
+struct VStage {
+  int cin, cout, rate, k;
+  std::vector<PackedGemm> phases;
+  // resblocks j: convs1[l], convs2[l], acts[2l], acts[2l+1]
+  std::vector<std::vector<PackedGemm>> c1, c2;
+  std::vector<std::vector<ActP>> acts;
+  std::vector<int> rk;
+  std::vector<std::vector<int>> rd;
+};
+
+}  // namespace svc
+
+using namespace svc;
+
+struct svc_ctx {
+  int device = 0;
+  std::map<std::string, Param> params;
+  std::map<std::string, double> cfg;
+  bool finalized = false;
+  std::vector<void*> allocs;
+  int64_t weight_bytes = 0;
+  Arena ws;
+
+  // features
+  float *fb24 = nullptr, *fb16 = nullptr, *win_mel = nullptr, *win16 = nullptr;
+  int n_fft = 1024, hop = 256, n_mels = 100, fs = 24000;
+  double fmin = 0, fmax = 12000, f0_min = 65, f0_max = 800;
+  // whisper
+  bool has_whisper = false;
+  int wD = 0, wH = 0, wL = 0, wctx = 0, wmels = 80;
+  PackedGemm wconv1, wconv2;
+  float *wpos = nullptr, *wlnp_g = nullptr, *wlnp_b = nullptr;
+  std::vector<WBlock> wblocks;
+  // mapper
+  bool has_mapper = false;
+  int C = 384, n_mel = 100, n_layers = 20, dil_cycle = 4, steps = 1000, content_dim = 1024, n_bins = 256;
+  PackedGemm content_lin, cp_all, melpre, skipproj, outproj;
+  std::vector<PackedGemm> dil, outp;
+  float *emb_m = nullptr, *emb_l = nullptr, *emb_s = nullptr, *mbins = nullptr, *ebins = nullptr;
+  float* dproj = nullptr;  // [steps][layers][C]
+  std::vector<float> alphas_cumprod_f32, sra, srm1, pc1, pc2, plogvar;
+  float *mel_min = nullptr, *mel_max = nullptr;
+  // vocoder
+  bool has_vocoder = false;
+  int v_in = 100, v_c0 = 1536;
+  PackedGemm vpre;
+  std::vector<VStage> vstages;
+  ActP vact_post;
+  float* vpost_w = nullptr;
+  float vpost_b = 0;
+  float* fade = nullptr;
+  int nfade = 5120;
+  int hop_out = 256;
+};
+
+namespace {
+
+int dev_upload(svc_ctx* c, const void* host, size_t bytes, void** out) {
+  void* p = nullptr;
+  SVC_HIP_CHECK(hipMalloc(&p, bytes > 0 ? bytes : 16));
+  if (bytes) SVC_HIP_CHECK(hipMemcpy(p, host, bytes, hipMemcpyHostToDevice));
+  c->allocs.push_back(p);
+  c->weight_bytes += (int64_t)bytes;
+  *out = p;
+  return SVC_OK;
+}
+
+template <typename T>
+int upload_vec(svc_ctx* c, const std::vector<T>& v, T** out) {
+  return dev_upload(c, v.data(), v.size() * sizeof(T), reinterpret_cast<void**>(out));
+}
+
+const Param* getp(svc_ctx* c, const std::string& name, std::initializer_list<int64_t> shape) {
+  auto it = c->params.find(name);
+  if (it == c->params.end()) {
+    set_error("missing parameter '%s'", name.c_str());
+    return nullptr;
+  }
+  std::vector<int64_t> want(shape);
+  if (want.size() != it->second.shape.size()) {
+    set_error("parameter '%s': expected %zu dims, got %zu", name.c_str(), want.size(), it->second.shape.size());
+    return nullptr;
+  }
+  for (size_t i = 0; i < want.size(); ++i)
+    if (want[i] >= 0 && want[i] != it->second.shape[i]) {
+      set_error("parameter '%s': dim %zu expected %lld got %lld", name.c_str(), i, (long long)want[i],
+                (long long)it->second.shape[i]);
+      return nullptr;
+    }
+  return &it->second;
+}
+
+#define GETP(var, name, ...)                           \
+  const Param* var = getp(c, (name), {__VA_ARGS__});   \
+  if (!var) return SVC_ERR_INVALID;
+
+int upload_param(svc_ctx* c, const Param* p, float** out) {
+  return dev_upload(c, p->host, (size_t)p->numel * sizeof(float), reinterpret_cast<void**>(out));
+}
+
+// generic packer: W16[n][tap*Cp + ci] = wget(n, ci, tap), bias[n] = bget(n)
+template <typename WG, typename BG>
+int pack_gemm(svc_ctx* c, PackedGemm& g, int N, int Cin, int Cp, int taps, WG wget, BG bget) {
+  g.N = N;
+  g.Cin = Cin;
+  g.Cp = Cp;
+  g.taps = taps;
+  g.K = taps * Cp;
+  g.Kpad = (int)round_up(g.K, 64);
+  g.Npad = (int)round_up(N, 128);
+  std::vector<f16> w((size_t)g.Npad * g.Kpad, (f16)0.0f);
+  std::vector<float> b((size_t)g.Npad, 0.0f);
+  for (int n = 0; n < N; ++n) {
+    for (int t = 0; t < taps; ++t)
+      for (int ci = 0; ci < Cin; ++ci) w[(size_t)n * g.Kpad + (size_t)t * Cp + ci] = (f16)wget(n, ci, t);
+    b[n] = bget(n);
+  }
+  int st = upload_vec(c, w, &g.W);
+  if (st) return st;
+  return upload_vec(c, b, &g.bias);
+}
+
+// Conv1d weight [Cout][Cin][k] (optionally weight-normed along dim 0) into a packed GEMM
+int pack_conv1d(svc_ctx* c, PackedGemm& g, const float* w, const float* bias, int Cout, int Cin, int k, int Cp,
+                int dil, int pad, int stride, const std::vector<int>* perm = nullptr, const float* wn_g = nullptr) {
+  std::vector<double> scale(Cout, 1.0);
+  if (wn_g) {
+    for (int o = 0; o < Cout; ++o) {
+      double s = 0;
+      for (int64_t i = 0; i < (int64_t)Cin * k; ++i) {
+        double v = w[(int64_t)o * Cin * k + i];
+        s += v * v;
+      }
+      scale[o] = (double)wn_g[o] / sqrt(s);
+    }
+  }
+  auto src = [&](int n) { return perm ? (*perm)[n] : n; };
+  int st = pack_gemm(
+      c, g, Cout, Cin, Cp, k,
+      [&](int n, int ci, int t) {
+        int o = src(n);
+        return (float)((double)w[((int64_t)o * Cin + ci) * k + t] * scale[o]);
+      },
+      [&](int n) { return bias ? bias[src(n)] : 0.0f; });
+  g.tap_mul = dil;
+  g.tap_add = -pad;
+  g.istride = stride;
+  return st;
+}
+
+// ConvTranspose1d weight [Cin][Cout][k] (weight-normed along dim 0 = Cin) into `stride` phase GEMMs
+int pack_conv_transpose(svc_ctx* c, std::vector<PackedGemm>& phases, const float* v, const float* wn_g,
+                        const float* bias, int Cin, int Cout, int k, int s, int pad) {
+  std::vector<double> scale(Cin, 1.0);
+  if (wn_g) {
+    for (int i = 0; i < Cin; ++i) {
+      double acc = 0;
+      for (int64_t j = 0; j < (int64_t)Cout * k; ++j) {
+        double x = v[(int64_t)i * Cout * k + j];
+        acc += x * x;
+      }
+      scale[i] = (double)wn_g[i] / sqrt(acc);
+    }
+  }
+  if (k % s != 0) {
+    set_error("conv_transpose: kernel %d not a multiple of stride %d", k, s);
+    return SVC_ERR_INVALID;
+  }
+  phases.assign(s, PackedGemm());
+  for (int r = 0; r < s; ++r) {
+    const int base = (r + pad) % s, add = (r + pad) / s;
+    int st = pack_gemm(
+        c, phases[r], Cout, Cin, Cin, k / s,
+        [&](int n, int ci, int j) {
+          int kk = base + s * j;
+          return (float)((double)v[((int64_t)ci * Cout + n) * k + kk] * scale[ci]);
+        },
+        [&](int n) { return bias ? bias[n] : 0.0f; });
+    if (st) return st;
+    phases[r].tap_mul = -1;
+    phases[r].tap_add = add;
+    phases[r].istride = 1;
+  }
+  return SVC_OK;
+}
+
+// paired packing order: packed n -> original channel ((n & 16) ? C : 0) + (n >> 5) * 16 + (n & 15)
+std::vector<int> pair_perm(int C) {
+  std::vector<int> p(2 * C);
+  for (int n = 0; n < 2 * C; ++n) p[n] = ((n & 16) ? C : 0) + (n >> 5) * 16 + (n & 15);
+  return p;
+}
+
+double cfgv(svc_ctx* c, const char* k, double d) {
+  auto it = c->cfg.find(k);
+  return it == c->cfg.end() ? d : it->second;
+}
+
+int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
+             hipStream_t s) {
+  ConvGemmArgs a{};
+  a.X = X;
+  a.ldx = ldx;
+  a.T_in = T_in;
+  a.Cp = g.Cp;
+  a.Cvalid = Cvalid;
+  a.W = g.W;
+  a.K = g.K;
+  a.Kpad = g.Kpad;
+  a.tap_mul = g.tap_mul;
+  a.tap_add = g.tap_add;
+  a.istride = g.istride;
+  a.B = B;
+  a.T_out = T_out;
+  a.N = g.N;
+  if (e.T_ostore == 0) {
+    e.T_ostore = T_out;
+    e.ostride = 1;
+    e.ophase = 0;
+  }
+  if (!e.bias) e.bias = g.bias;
+  return conv_gemm(a, e, s);
+}
+
+EpiArgs epi() {
+  EpiArgs e{};
+  e.kind = EPI_GENERIC;
+  e.acc_div = 1.0f;
+  return e;
+}
+
+// ---------------------------------------------------------------------------- finalize: whisper
+int build_whisper(svc_ctx* c) {
+  GETP(c1w, "whisper.encoder.conv1.weight", -1, -1, 3);
+  const int D = (int)c1w->shape[0];
+  const int nm = (int)c1w->shape[1];
+  GETP(pos, "whisper.encoder.positional_embedding", -1, D);
+  c->wD = D;
+  c->wH = D / 64;
+  c->wmels = nm;
+  c->wctx = (int)pos->shape[0];
+  int L = 0;
+  while (c->params.count("whisper.encoder.blocks." + std::to_string(L) + ".attn.query.weight")) ++L;
+  c->wL = L;
+  GETP(c1b, "whisper.encoder.conv1.bias", D);
+  GETP(c2w, "whisper.encoder.conv2.weight", D, D, 3);
+  GETP(c2b, "whisper.encoder.conv2.bias", D);
+  int st = pack_conv1d(c, c->wconv1, c1w->host, c1b->host, D, nm, 3, (int)round_up(nm, 8), 1, 1, 1);
+  if (st) return st;
+  st = pack_conv1d(c, c->wconv2, c2w->host, c2b->host, D, D, 3, D, 1, 1, 2);
+  if (st) return st;
+  if ((st = upload_param(c, pos, &c->wpos))) return st;
+  c->wblocks.resize(L);
+  for (int i = 0; i < L; ++i) {
+    std::string p = "whisper.encoder.blocks." + std::to_string(i) + ".";
+    WBlock& b = c->wblocks[i];
+    GETP(qw, p + "attn.query.weight", D, D);
+    GETP(qb, p + "attn.query.bias", D);
+    GETP(kw, p + "attn.key.weight", D, D);
+    GETP(vw, p + "attn.value.weight", D, D);
+    GETP(vb, p + "attn.value.bias", D);
+    GETP(ow, p + "attn.out.weight", D, D);
+    GETP(ob, p + "attn.out.bias", D);
+    GETP(l1g, p + "attn_ln.weight", D);
+    GETP(l1b, p + "attn_ln.bias", D);
+    GETP(l2g, p + "mlp_ln.weight", D);
+    GETP(l2b, p + "mlp_ln.bias", D);
+    GETP(f1w, p + "mlp.0.weight", 4 * D, D);
+    GETP(f1b, p + "mlp.0.bias", 4 * D);
+    GETP(f2w, p + "mlp.2.weight", D, 4 * D);
+    GETP(f2b, p + "mlp.2.bias", D);
+    st = pack_gemm(
+        c, b.qkv, 3 * D, D, D, 1,
+        [&](int n, int ci, int) {
+          const Param* w = n < D ? qw : (n < 2 * D ? kw : vw);
+          return w->host[(int64_t)(n % D) * D + ci];
+        },
+        [&](int n) { return n < D ? qb->host[n] : (n < 2 * D ? 0.0f : vb->host[n - 2 * D]); });
+    if (st) return st;
+    if ((st = pack_conv1d(c, b.out, ow->host, ob->host, D, D, 1, D, 1, 0, 1))) return st;
+    if ((st = pack_conv1d(c, b.fc1, f1w->host, f1b->host, 4 * D, D, 1, D, 1, 0, 1))) return st;
+    if ((st = pack_conv1d(c, b.fc2, f2w->host, f2b->host, D, 4 * D, 1, 4 * D, 1, 0, 1))) return st;
+    if ((st = upload_param(c, l1g, &b.ln1_g)) || (st = upload_param(c, l1b, &b.ln1_b)) ||
+        (st = upload_param(c, l2g, &b.ln2_g)) || (st = upload_param(c, l2b, &b.ln2_b)))
+      return st;
+  }
+  GETP(lpg, "whisper.encoder.ln_post.weight", D);
+  GETP(lpb, "whisper.encoder.ln_post.bias", D);
+  if ((st = upload_param(c, lpg, &c->wlnp_g)) || (st = upload_param(c, lpb, &c->wlnp_b))) return st;
+  c->has_whisper = true;
+  return SVC_OK;
+}
+
+// ---------------------------------------------------------------------------- finalize: mapper
+int build_mapper(svc_ctx* c) {
+  const int C = (int)cfgv(c, "mapper.residual_channels", 384);
+  const int NL = (int)cfgv(c, "mapper.residual_layer_num", 20);
+  const int nmel = (int)cfgv(c, "mapper.n_mel", 100);
+  const int fc = (int)cfgv(c, "mapper.diffusion_fc_size", 128);
+  c->C = C;
+  c->n_layers = NL;
+  c->n_mel = nmel;
+  c->dil_cycle = (int)cfgv(c, "mapper.dilation_cycle_length", 4);
+  const int ks = (int)cfgv(c, "mapper.residual_kernel_size", 3);
+  if (ks != 3) {
+    set_error("mapper: residual_kernel_size %d unsupported", ks);
+    return SVC_ERR_INVALID;
+  }
+  const std::string p = "mapper.0.registered_modules_dict.";
+  GETP(cw, p + "content_whisper.nn.weight", C, -1);
+  GETP(cb, p + "content_whisper.nn.bias", C);
+  c->content_dim = (int)cw->shape[1];
+  GETP(mb, p + "melody.melody_bins", -1);
+  GETP(me, p + "melody.nn.weight", -1, C);
+  GETP(eb, p + "loudness.energy_bins", mb->shape[0]);
+  GETP(le, p + "loudness.nn.weight", me->shape[0], C);
+  GETP(se, p + "singer.nn.weight", -1, C);
+  c->n_bins = (int)me->shape[0];
+  if (mb->shape[0] != c->n_bins - 1) {
+    set_error("mapper: melody bins %lld vs embedding %d", (long long)mb->shape[0], c->n_bins);
+    return SVC_ERR_INVALID;
+  }
+  int st;
+  if ((st = pack_conv1d(c, c->content_lin, cw->host, cb->host, C, c->content_dim, 1, c->content_dim, 1, 0, 1)))
+    return st;
+  if ((st = upload_param(c, mb, &c->mbins)) || (st = upload_param(c, eb, &c->ebins)) ||
+      (st = upload_param(c, me, &c->emb_m)) || (st = upload_param(c, le, &c->emb_l)) ||
+      (st = upload_param(c, se, &c->emb_s)))
+    return st;
+
+  const std::string q = "mapper.1.";
+  GETP(mpw, q + "mel_preprocess.projection.weight", C, nmel, 1);
+  GETP(mpb, q + "mel_preprocess.projection.bias", C);
+  if ((st = pack_conv1d(c, c->melpre, mpw->host, mpb->host, C, nmel, 1, (int)round_up(nmel, 8), 1, 0, 1))) return st;
+  GETP(p1w, q + "diffusion_embedding.projection1.weight", fc, 128);
+  GETP(p1b, q + "diffusion_embedding.projection1.bias", fc);
+  GETP(p2w, q + "diffusion_embedding.projection2.weight", fc, fc);
+  GETP(p2b, q + "diffusion_embedding.projection2.bias", fc);
+  GETP(table, "mapper.step_table", -1, 128);
+  const int steps = (int)table->shape[0];
+  c->steps = steps;
+  std::vector<int> perm = pair_perm(C);
+  c->dil.resize(NL);
+  c->outp.resize(NL);
+  std::vector<const Param*> cpw(NL), cpb(NL), dpw(NL), dpb(NL);
+  for (int i = 0; i < NL; ++i) {
+    std::string r = q + "residual_layers." + std::to_string(i) + ".";
+    GETP(dw, r + "dilated_conv.weight", 2 * C, C, 3);
+    GETP(db, r + "dilated_conv.bias", 2 * C);
+    GETP(ow, r + "output_projection.weight", 2 * C, C, 1);
+    GETP(ob, r + "output_projection.bias", 2 * C);
+    GETP(cw2, r + "conditioner_projection.weight", 2 * C, -1, 1);
+    GETP(cb2, r + "conditioner_projection.bias", 2 * C);
+    GETP(pw, r + "diffusion_projection.weight", C, fc);
+    GETP(pb, r + "diffusion_projection.bias", C);
+    cpw[i] = cw2;
+    cpb[i] = cb2;
+    dpw[i] = pw;
+    dpb[i] = pb;
+    const int d = 1 << (i % c->dil_cycle);
+    if ((st = pack_conv1d(c, c->dil[i], dw->host, db->host, 2 * C, C, 3, C, d, d, 1, &perm))) return st;
+    if ((st = pack_conv1d(c, c->outp[i], ow->host, ob->host, 2 * C, C, 1, C, 1, 0, 1, &perm))) return st;
+  }
+  const int cond_sz = (int)cpw[0]->shape[1];
+  // all 20 conditioner projections as one GEMM (loop-invariant over diffusion steps: hoisted)
+  st = pack_gemm(
+      c, c->cp_all, NL * 2 * C, cond_sz, cond_sz, 1,
+      [&](int n, int ci, int) {
+        int layer = n / (2 * C), o = perm[n % (2 * C)];
+        return cpw[layer]->host[(int64_t)o * cond_sz + ci];
+      },
+      [&](int n) {
+        int layer = n / (2 * C), o = perm[n % (2 * C)];
+        return cpb[layer]->host[o];
+      });
+  if (st) return st;
+  GETP(spw, q + "skip_projection.weight", C, C, 1);
+  GETP(spb, q + "skip_projection.bias", C);
+  GETP(opw, q + "output_projection.weight", nmel, C, 1);
+  GETP(opb, q + "output_projection.bias", nmel);
+  if ((st = pack_conv1d(c, c->skipproj, spw->host, spb->host, C, C, 1, C, 1, 0, 1))) return st;
+  if ((st = pack_conv1d(c, c->outproj, opw->host, opb->host, nmel, C, 1, C, 1, 0, 1))) return st;
+
+  // step MLP + per-layer diffusion projections for every step (input-independent: precomputed)
+  std::vector<float> dp((size_t)steps * NL * C);
+  std::vector<double> h1(fc), h2(fc);
+  auto silu = [](double x) { return x / (1.0 + exp(-x)); };
+  for (int t = 0; t < steps; ++t) {
+    const float* e = table->host + (size_t)t * 128;
+    for (int o = 0; o < fc; ++o) {
+      double a = p1b->host[o];
+      for (int i = 0; i < 128; ++i) a += (double)p1w->host[o * 128 + i] * e[i];
+      h1[o] = (float)silu((float)a);
+    }
+    for (int o = 0; o < fc; ++o) {
+      double a = p2b->host[o];
+      for (int i = 0; i < fc; ++i) a += (double)p2w->host[o * fc + i] * h1[i];
+      h2[o] = (float)silu((float)a);
+    }
+    for (int l = 0; l < NL; ++l)
+      for (int o = 0; o < C; ++o) {
+        double a = dpb[l]->host[o];
+        for (int i = 0; i < fc; ++i) a += (double)dpw[l]->host[o * fc + i] * h2[i];
+        dp[((size_t)t * NL + l) * C + o] = (float)a;
+      }
+  }
+  if ((st = upload_vec(c, dp, &c->dproj))) return st;
+
+  // noise schedule constants (modules/diffsvcrepo_inference.py:163-197: numpy f64 -> f32)
+  const double b0 = cfgv(c, "mapper.noise_schedule_factors.0", 1e-4);
+  const double b1 = cfgv(c, "mapper.noise_schedule_factors.1", 0.02);
+  std::vector<double> betas(steps);
+  const double stp = (b1 - b0) / (steps - 1);
+  for (int i = 0; i < steps; ++i) betas[i] = (i == steps - 1) ? b1 : i * stp + b0;
+  c->alphas_cumprod_f32.resize(steps);
+  c->sra.resize(steps);
+  c->srm1.resize(steps);
+  c->pc1.resize(steps);
+  c->pc2.resize(steps);
+  c->plogvar.resize(steps);
+  double ac = 1.0;
+  for (int i = 0; i < steps; ++i) {
+    const double alpha = 1.0 - betas[i];
+    const double prev = ac;
+    ac = ac * alpha;
+    c->alphas_cumprod_f32[i] = (float)ac;
+    c->sra[i] = (float)sqrt(1.0 / ac);
+    c->srm1[i] = (float)sqrt(1.0 / ac - 1);
+    c->pc1[i] = (float)(betas[i] * sqrt(prev) / (1.0 - ac));
+    c->pc2[i] = (float)((1.0 - prev) * sqrt(alpha) / (1.0 - ac));
+    const double pv = betas[i] * (1.0 - prev) / (1.0 - ac);
+    c->plogvar[i] = (float)log(pv > 1e-20 ? pv : 1e-20);
+  }
+  GETP(mn, "stats.mel_min", nmel);
+  GETP(mx, "stats.mel_max", nmel);
+  if ((st = upload_param(c, mn, &c->mel_min)) || (st = upload_param(c, mx, &c->mel_max))) return st;
+  c->has_mapper = true;
+  return SVC_OK;
+}
+
+// ---------------------------------------------------------------------------- finalize: vocoder
+int get_act(svc_ctx* c, const std::string& name, int ch, ActP& a) {
+  GETP(al, name + ".act.alpha", ch);
+  GETP(be, name + ".act.beta", ch);
+  GETP(fu, name + ".upsample.filter", 1, 1, 12);
+  GETP(fd, name + ".downsample.lowpass.filter", 1, 1, 12);
+  for (int i = 0; i < 12; ++i)
+    if (fu->host[i] != fd->host[i]) {
+      set_error("%s: up/down filters differ (unsupported)", name.c_str());
+      return SVC_ERR_INVALID;
+    }
+  int st;
+  if ((st = upload_param(c, al, &a.alpha)) || (st = upload_param(c, be, &a.beta)) || (st = upload_param(c, fu, &a.filt)))
+    return st;
+  return SVC_OK;
+}
+
+int build_vocoder(svc_ctx* c) {
+  const int ns = (int)cfgv(c, "vocoder.n_stages", 6);
+  const int nk = (int)cfgv(c, "vocoder.n_kernels", 3);
+  const int C0 = (int)cfgv(c, "vocoder.upsample_initial_channel", 1536);
+  const int vin = (int)cfgv(c, "vocoder.input_dim", 100);
+  c->v_c0 = C0;
+  c->v_in = vin;
+  int st;
+  GETP(pv, "vocoder.conv_pre.weight_v", C0, vin, 7);
+  GETP(pg, "vocoder.conv_pre.weight_g", C0, 1, 1);
+  GETP(pb, "vocoder.conv_pre.bias", C0);
+  if ((st = pack_conv1d(c, c->vpre, pv->host, pb->host, C0, vin, 7, (int)round_up(vin, 8), 1, 3, 1, nullptr, pg->host)))
+    return st;
+  c->vstages.resize(ns);
+  int hop = 1;
+  for (int i = 0; i < ns; ++i) {
+    VStage& S = c->vstages[i];
+    S.cin = C0 >> i;
+    S.cout = C0 >> (i + 1);
+    S.rate = (int)cfgv(c, ("vocoder.upsample_rates." + std::to_string(i)).c_str(), 2);
+    S.k = (int)cfgv(c, ("vocoder.upsample_kernel_sizes." + std::to_string(i)).c_str(), 4);
+    hop *= S.rate;
+    std::string u = "vocoder.ups." + std::to_string(i) + ".0.";
+    GETP(uv, u + "weight_v", S.cin, S.cout, S.k);
+    GETP(ug, u + "weight_g", S.cin, 1, 1);
+    GETP(ub, u + "bias", S.cout);
+    if ((st = pack_conv_transpose(c, S.phases, uv->host, ug->host, ub->host, S.cin, S.cout, S.k, S.rate,
+                                  (S.k - S.rate) / 2)))
+      return st;
+    S.c1.resize(nk);
+    S.c2.resize(nk);
+    S.acts.resize(nk);
+    S.rk.resize(nk);
+    S.rd.resize(nk);
+    const int ch = S.cout;
+    for (int j = 0; j < nk; ++j) {
+      const int kk = (int)cfgv(c, ("vocoder.resblock_kernel_sizes." + std::to_string(j)).c_str(), 3);
+      S.rk[j] = kk;
+      std::string rb = "vocoder.resblocks." + std::to_string(i * nk + j) + ".";
+      const int nd = (int)cfgv(c, ("vocoder.resblock_dilation_sizes." + std::to_string(j) + ".n").c_str(), 3);
+      S.c1[j].resize(nd);
+      S.c2[j].resize(nd);
+      S.acts[j].resize(2 * nd);
+      S.rd[j].resize(nd);
+      for (int l = 0; l < nd; ++l) {
+        const int d =
+            (int)cfgv(c, ("vocoder.resblock_dilation_sizes." + std::to_string(j) + "." + std::to_string(l)).c_str(), 1);
+        S.rd[j][l] = d;
+        std::string n1 = rb + "convs1." + std::to_string(l) + ".", n2 = rb + "convs2." + std::to_string(l) + ".";
+        GETP(v1, n1 + "weight_v", ch, ch, kk);
+        GETP(g1, n1 + "weight_g", ch, 1, 1);
+        GETP(b1, n1 + "bias", ch);
+        GETP(v2, n2 + "weight_v", ch, ch, kk);
+        GETP(g2, n2 + "weight_g", ch, 1, 1);
+        GETP(b2, n2 + "bias", ch);
+        if ((st = pack_conv1d(c, S.c1[j][l], v1->host, b1->host, ch, ch, kk, ch, d, (kk * d - d) / 2, 1, nullptr,
+                              g1->host)))
+          return st;
+        if ((st = pack_conv1d(c, S.c2[j][l], v2->host, b2->host, ch, ch, kk, ch, 1, (kk - 1) / 2, 1, nullptr,
+                              g2->host)))
+          return st;
+        if ((st = get_act(c, rb + "activations." + std::to_string(2 * l), ch, S.acts[j][2 * l]))) return st;
+        if ((st = get_act(c, rb + "activations." + std::to_string(2 * l + 1), ch, S.acts[j][2 * l + 1]))) return st;
+      }
+    }
+  }
+  c->hop_out = hop;
+  const int chl = C0 >> ns;
+  if ((st = get_act(c, "vocoder.activation_post", chl, c->vact_post))) return st;
+  GETP(qv, "vocoder.conv_post.weight_v", 1, chl, 7);
+  GETP(qg, "vocoder.conv_post.weight_g", 1, 1, 1);
+  GETP(qb, "vocoder.conv_post.bias", 1);
+  {
+    double s = 0;
+    for (int i = 0; i < chl * 7; ++i) s += (double)qv->host[i] * qv->host[i];
+    const double sc = qg->host[0] / sqrt(s);
+    std::vector<float> w(chl * 7);
+    for (int i = 0; i < chl * 7; ++i) w[i] = (float)(qv->host[i] * sc);
+    if ((st = upload_vec(c, w, &c->vpost_w))) return st;
+    c->vpost_b = qb->host[0];
+  }
+  GETP(fade, "vocoder.fade_out", -1);
+  c->nfade = (int)fade->shape[0];
+  if ((st = upload_param(c, fade, &c->fade))) return st;
+  c->has_vocoder = true;
+  return SVC_OK;
+}
+
+int build_features(svc_ctx* c) {
+  c->fs = (int)cfgv(c, "fs", 24000);
+  c->n_fft = (int)cfgv(c, "n_fft", 1024);
+  c->hop = (int)cfgv(c, "hop_length", 256);
+  c->n_mels = (int)cfgv(c, "n_mels", 100);
+  c->fmin = cfgv(c, "fmin", 0);
+  c->fmax = cfgv(c, "fmax", 12000);
+  c->f0_min = cfgv(c, "f0_min", 65);
+  c->f0_max = cfgv(c, "f0_max", 800);
+  if ((int)cfgv(c, "win_length", 1024) != c->n_fft) {
+    set_error("win_length != n_fft unsupported");
+    return SVC_ERR_INVALID;
+  }
+  int st;
+  if ((st = upload_vec(c, slaney_mel(c->fs, c->n_fft, c->n_mels, c->fmin, c->fmax), &c->fb24))) return st;
+  if ((st = upload_vec(c, slaney_mel(16000, 400, 80, 0.0, 8000.0), &c->fb16))) return st;
+  if ((st = upload_vec(c, hann_periodic(c->n_fft), &c->win_mel))) return st;
+  if ((st = upload_vec(c, hann_periodic(400), &c->win16))) return st;
+  return SVC_OK;
+}
+
+}  // namespace
+
+// ============================================================================ C-ABI
+extern "C" {
+
+const char* svc_last_error(void) { return get_error(); }
+int svc_abi_version(void) { return 1; }
+
+svc_status svc_ctx_create(int device, svc_ctx** out) {
+  SVC_REQUIRE(out, "svc_ctx_create: null out");
+  int n = 0;
+  SVC_HIP_CHECK(hipGetDeviceCount(&n));
+  SVC_REQUIRE(device >= 0 && device < n, "svc_ctx_create: device %d of %d", device, n);
+  SVC_HIP_CHECK(hipSetDevice(device));
+  svc_ctx* c = new svc_ctx();
+  c->device = device;
+  *out = c;
+  return SVC_OK;
+}
+
+svc_status svc_ctx_destroy(svc_ctx* c) {
+  if (!c) return SVC_OK;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  for (void* p : c->allocs) (void)hipFree(p);
+  if (c->ws.base) (void)hipFree(c->ws.base);
+  delete c;
+  return SVC_OK;
+}
+
+svc_status svc_ctx_set_config(svc_ctx* c, const char* key, double value) {
+  SVC_REQUIRE(c && key, "set_config: null");
+  c->cfg[key] = value;
+  return SVC_OK;
+}
+
+svc_status svc_ctx_add_param(svc_ctx* c, const char* name, const float* host, int ndim, const int64_t* shape) {
+  SVC_REQUIRE(c && name && host && ndim >= 0 && ndim <= 8, "add_param: bad args");
+  if (c->finalized) {
+    set_error("add_param after finalize");
+    return SVC_ERR_STATE;
+  }
+  Param p;
+  p.host = host;
+  p.numel = 1;
+  for (int i = 0; i < ndim; ++i) {
+    p.shape.push_back(shape[i]);
+    p.numel *= shape[i];
+  }
+  c->params[name] = p;
+  return SVC_OK;
+}
+
+svc_status svc_ctx_finalize(svc_ctx* c) {
+  SVC_REQUIRE(c, "finalize: null");
+  if (c->finalized) {
+    set_error("finalize called twice");
+    return SVC_ERR_STATE;
+  }
+  SVC_HIP_CHECK(hipSetDevice(c->device));
+  int st;
+  if ((st = build_features(c))) return st;
+  bool any_w = false, any_m = false, any_v = false;
+  for (auto& kv : c->params) {
+    any_w |= kv.first.rfind("whisper.", 0) == 0;
+    any_m |= kv.first.rfind("mapper.", 0) == 0;
+    any_v |= kv.first.rfind("vocoder.", 0) == 0;
+  }
+  if (any_w && (st = build_whisper(c))) return st;
+  if (any_m && (st = build_mapper(c))) return st;
+  if (any_v && (st = build_vocoder(c))) return st;
+  c->params.clear();  // host arrays are no longer referenced
+  c->finalized = true;
+  return SVC_OK;
+}
+
+svc_status svc_ctx_memory(svc_ctx* c, int64_t* wb, int64_t* wsb) {
+  SVC_REQUIRE(c, "memory: null");
+  if (wb) *wb = c->weight_bytes;
+  if (wsb) *wsb = (int64_t)c->ws.cap;
+  return SVC_OK;
+}
+
+svc_status svc_profile_enable(int enable) {
+  if (!enable || !g_prof) {
+    for (auto& r : g_prof_recs) {
+      g_ev_pool.push_back(r.a);
+      g_ev_pool.push_back(r.b);
+    }
+    g_prof_recs.clear();
+  }
+  g_prof = enable != 0;
+  return SVC_OK;
+}
+
+svc_status svc_profile_read(int idx, char* name, int name_len, double* total_ms, int64_t* launches, double* flops,
+                            double* bytes, int* n_kernels) {
+  // aggregate by kernel name (synchronises on the recorded events)
+  std::vector<std::string> names;
+  std::map<std::string, std::tuple<double, int64_t, double, double>> agg;
+  for (auto& r : g_prof_recs) {
+    SVC_HIP_CHECK(hipEventSynchronize(r.b));
+    float ms = 0;
+    SVC_HIP_CHECK(hipEventElapsedTime(&ms, r.a, r.b));
+    if (!agg.count(r.name)) names.push_back(r.name);
+    auto& t = agg[r.name];
+    std::get<0>(t) += ms;
+    std::get<1>(t) += 1;
+    std::get<2>(t) += r.flops;
+    std::get<3>(t) += r.bytes;
+  }
+  if (n_kernels) *n_kernels = (int)names.size();
+  if (idx < 0 || idx >= (int)names.size()) return SVC_OK;
+  auto& t = agg[names[idx]];
+  if (name && name_len > 0) snprintf(name, name_len, "%s", names[idx].c_str());
+  if (total_ms) *total_ms = std::get<0>(t);
+  if (launches) *launches = std::get<1>(t);
+  if (flops) *flops = std::get<2>(t);
+  if (bytes) *bytes = std::get<3>(t);
+  return SVC_OK;
+}
+
+svc_status svc_mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double fmax, float* out) {
+  SVC_REQUIRE(out && n_fft > 0 && n_mels > 0, "mel_filterbank: bad args");
+  auto w = slaney_mel(sr, n_fft, n_mels, fmin, fmax);
+  memcpy(out, w.data(), w.size() * sizeof(float));
+  return SVC_OK;
+}
+
+#define CTX_READY(c)                                                        \
+  do {                                                                      \
+    SVC_REQUIRE((c), "null context");                                       \
+    if (!(c)->finalized) {                                                  \
+      set_error("context not finalized");                                   \
+      return SVC_ERR_STATE;                                                 \
+    }                                                                       \
+    SVC_HIP_CHECK(hipSetDevice((c)->device));                               \
+  } while (0)
+
+#define WS_GET(T, var, n)                                                               \
+  T* var = c->ws.get<T>((size_t)(n));                                                   \
+  if (!var) {                                                                           \
+    set_error("workspace exhausted at %s (need %zu bytes more)", #var, (size_t)(n) * sizeof(T)); \
+    return SVC_ERR_STATE;                                                               \
+  }
+
+// ---------------------------------------------------------------------------- mel + energy
+svc_status svc_mel_energy(svc_ctx* c, const float* wav, int B, int64_t n, float* mel, float* energy, void* stream) {
+  CTX_READY(c);
+  hipStream_t s = (hipStream_t)stream;
+  const int pad = (c->n_fft - c->hop) / 2;
+  const int64_t T64 = (n + 2 * pad - c->n_fft) / c->hop + 1;
+  SVC_REQUIRE(B > 0 && n > pad && T64 > 0 && T64 < (1 << 30), "mel_energy: n=%lld", (long long)n);
+  const int T = (int)T64, nb = c->n_fft / 2 + 1;
+  size_t need = (size_t)B * T * nb * 4 + 4096;
+  int st;
+  if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
+  c->ws.reset();
+  WS_GET(float, spec, (size_t)B * T * nb);
+  DftArgs a{};
+  a.wav = wav;
+  a.wav_stride = n;
+  a.n_valid = n;
+  a.n_logical = n;
+  a.n_fft = c->n_fft;
+  a.hop = c->hop;
+  a.pad = pad;
+  a.n_frames = T;
+  a.nbins = nb;
+  a.window = c->win_mel;
+  a.mode = 0;
+  a.out = spec;
+  if ((st = dft_frames(a, B, s))) return st;
+  if ((st = mel_log(spec, nb, c->fb24, c->n_mels, mel, B * T, 0, s))) return st;
+  return energy_from_mel(mel, c->n_mels, energy, B * T, s);
+}
+
+// ---------------------------------------------------------------------------- F0
+svc_status svc_f0_ac(svc_ctx* c, const float* wav, int B, int64_t n, int T, double* f0, void* stream) {
+  CTX_READY(c);
+  const double ts = (double)c->hop / c->fs;
+  size_t need = f0_workspace_bytes(B, n, c->fs, ts, c->f0_min);
+  int st;
+  if ((st = c->ws.reserve(std::max(need + 4096, c->ws.cap)))) return st;
+  c->ws.reset();
+  return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->ws.base, c->ws.cap,
+                     (hipStream_t)stream);
+}
+
+svc_status svc_pitch_shift(svc_ctx* c, double* f0, int B, int T, double target_median, void* stream) {
+  SVC_REQUIRE(c && f0 && B > 0 && T > 0, "pitch_shift: bad args");
+  SVC_HIP_CHECK(hipSetDevice(c->device));
+  return pitch_shift(f0, B, T, target_median, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------- whisper
+svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, float* feats, void* stream) {
+  CTX_READY(c);
+  SVC_REQUIRE(c->has_whisper, "whisper weights not loaded");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t NS = 480000;  // utils/whisper_extractor/audio.py:18 (30 s @ 16 kHz)
+  const int F = 3000, D = c->wD, L = c->wctx;
+  SVC_REQUIRE(B > 0 && n > 0, "whisper: B=%d n=%lld", B, (long long)n);
+  SVC_REQUIRE(L * 2 == F, "whisper: n_ctx %d != 1500", L);
+  const int nb = 201;
+  const size_t rows1 = (size_t)B * F, rows2 = (size_t)B * L;
+  size_t need = rows1 * nb * 4 + rows1 * c->wmels * 4 + rows1 * c->wmels * 2 + rows1 * D * 2 /*h1*/ + rows2 * D * 4 +
+                rows2 * D * 2 + rows2 * 3 * D * 2 + rows2 * D * 2 + rows2 * 4 * D * 2 + 64 * 4096;
+  int st;
+  if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
+  c->ws.reset();
+  WS_GET(float, spec, rows1 * nb);
+  WS_GET(float, ls, rows1 * c->wmels);
+  WS_GET(f16, lm16, rows1 * c->wmels);
+  WS_GET(float, mx, B);
+  DftArgs a{};
+  a.wav = wav16;
+  a.wav_stride = n;
+  a.n_valid = std::min<int64_t>(n, NS);
+  a.n_logical = NS;
+  a.n_fft = 400;
+  a.hop = 160;
+  a.pad = 200;
+  a.n_frames = F;
+  a.nbins = nb;
+  a.window = c->win16;
+  a.mode = 1;
+  a.out = spec;
+  if ((st = dft_frames(a, B, s))) return st;
+  if ((st = mel_log(spec, nb, c->fb16, c->wmels, ls, (int)rows1, 1, s))) return st;
+  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s))) return st;
+  // conv stem
+  WS_GET(f16, h1, rows1 * D);
+  EpiArgs e = epi();
+  e.act = ACT_GELU;
+  e.out16 = h1;
+  e.ld16 = D;
+  if ((st = run_gemm(c->wconv1, lm16, c->wmels, c->wmels, B, F, F, e, s))) return st;
+  WS_GET(float, x, rows2 * D);
+  e = epi();
+  e.act = ACT_GELU;
+  e.add_t = c->wpos;
+  e.ld_add_t = D;
+  e.out32 = x;
+  e.ld32 = D;
+  if ((st = run_gemm(c->wconv2, h1, D, D, B, F, L, e, s))) return st;
+  WS_GET(f16, n16, rows2 * D);
+  WS_GET(f16, qkv, rows2 * 3 * D);
+  WS_GET(f16, o16, rows2 * D);
+  WS_GET(f16, h16, rows2 * 4 * D);
+  const float qk_scale = powf((float)(D / c->wH), -0.25f);
+  for (int i = 0; i < c->wL; ++i) {
+    WBlock& b = c->wblocks[i];
+    if ((st = layernorm_f16(x, b.ln1_g, b.ln1_b, n16, (int)rows2, D, D, s))) return st;
+    e = epi();
+    e.out16 = qkv;
+    e.ld16 = 3 * D;
+    e.scale_cols = 2 * D;
+    e.col_scale = qk_scale;
+    if ((st = run_gemm(b.qkv, n16, D, D, B, L, L, e, s))) return st;
+    if ((st = attention(qkv, o16, B, L, D, s))) return st;
+    e = epi();
+    e.add_row = x;
+    e.ld_add_row = D;
+    e.out32 = x;
+    e.ld32 = D;
+    if ((st = run_gemm(b.out, o16, D, D, B, L, L, e, s))) return st;
+    if ((st = layernorm_f16(x, b.ln2_g, b.ln2_b, n16, (int)rows2, D, D, s))) return st;
+    e = epi();
+    e.act = ACT_GELU;
+    e.out16 = h16;
+    e.ld16 = 4 * D;
+    if ((st = run_gemm(b.fc1, n16, D, D, B, L, L, e, s))) return st;
+    e = epi();
+    e.add_row = x;
+    e.ld_add_row = D;
+    e.out32 = x;
+    e.ld32 = D;
+    if ((st = run_gemm(b.fc2, h16, 4 * D, 4 * D, B, L, L, e, s))) return st;
+  }
+  return layernorm_f32(x, c->wlnp_g, c->wlnp_b, feats, (int)rows2, D, D, s);
+}
+
+svc_status svc_map_content(svc_ctx* c, const float* feats, int B, int src_rows, int T, int D, void* out, void* stream) {
+  SVC_REQUIRE(c && feats && out, "map_content: null");
+  SVC_HIP_CHECK(hipSetDevice(c->device));
+  return content_map(feats, B, src_rows, D, T, D, (f16*)out, D, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------- conditioner
+static int condition_impl(svc_ctx* c, const void* content16, const double* f0, const float* energy,
+                          const int32_t* singer, int B, int T, float* cond, f16* cond16, hipStream_t s) {
+  const int rows = B * T;
+  WS_GET(int, im, rows);
+  WS_GET(int, ie, rows);
+  int st;
+  if ((st = bucketize(f0, energy, c->mbins, c->ebins, c->n_bins - 1, im, ie, rows, s))) return st;
+  EpiArgs e = epi();
+  e.kind = EPI_COND;
+  e.idx_m = im;
+  e.idx_l = ie;
+  e.singer = singer;
+  e.emb_m = c->emb_m;
+  e.emb_l = c->emb_l;
+  e.emb_s = c->emb_s;
+  e.ld_emb = c->C;
+  e.out32 = cond;
+  e.ld32 = c->C;
+  e.out16 = cond16;
+  e.ld16 = c->C;
+  return run_gemm(c->content_lin, (const f16*)content16, c->content_dim, c->content_dim, B, T, T, e, s);
+}
+
+svc_status svc_condition(svc_ctx* c, const void* content16, const double* f0, const float* energy,
+                         const int32_t* singer, int B, int T, float* cond, void* stream) {
+  CTX_READY(c);
+  SVC_REQUIRE(c->has_mapper, "mapper weights not loaded");
+  int st;
+  if ((st = c->ws.reserve(std::max((size_t)B * T * 8 + 4096, c->ws.cap)))) return st;
+  c->ws.reset();
+  return condition_impl(c, content16, f0, energy, singer, B, T, cond, nullptr, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------- DiffSVC denoiser
+struct DenoiseBufs {
+  f16* cp16;     // [rows][NL*2C]
+  float* h32;    // [rows][C]
+  float* skip32; // [rows][C]
+  f16* y16;      // [rows][C]
+  f16* g16;      // [rows][C]
+  f16* s16;      // [rows][C] (skip / sqrt(NL), then skip_projection output)
+  f16* u16;
+};
+
+static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s) {
+  const int C = c->C, NL = c->n_layers, rows = B * T;
+  const int ldx16 = (int)round_up(c->n_mel, 8);
+  const float* dp = c->dproj + (size_t)t * NL * C;
+  int st;
+  EpiArgs e = epi();
+  e.act = ACT_RELU;
+  e.out32 = bb.h32;
+  e.ld32 = C;
+  e.out16 = bb.y16;
+  e.ld16 = C;
+  e.add16 = dp;  // layer 0 diffusion projection
+  if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s))) return st;
+  for (int i = 0; i < NL; ++i) {
+    EpiArgs g = epi();
+    g.kind = EPI_GATE;
+    g.cp = bb.cp16 + (size_t)i * 2 * C;
+    g.ld_cp = NL * 2 * C;
+    g.y16 = bb.g16;
+    g.ldy16 = C;
+    if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s))) return st;
+    EpiArgs r = epi();
+    r.kind = EPI_RESSKIP;
+    r.x32 = bb.h32;
+    r.skip32 = bb.skip32;
+    r.ldx32 = C;
+    r.skip_first = i == 0;
+    r.last_layer = i == NL - 1;
+    r.skip_scale = sqrtf((float)NL);
+    r.dnext = (i + 1 < NL) ? dp + (size_t)(i + 1) * C : nullptr;
+    r.y16 = (i + 1 < NL) ? bb.y16 : bb.s16;
+    r.ldy16 = C;
+    if ((st = run_gemm(c->outp[i], bb.g16, C, C, B, T, T, r, s))) return st;
+  }
+  e = epi();
+  e.act = ACT_RELU;
+  e.out16 = bb.u16;
+  e.ld16 = C;
+  if ((st = run_gemm(c->skipproj, bb.s16, C, C, B, T, T, e, s))) return st;
+  e = epi();
+  e.out32 = eps;
+  e.ld32 = c->n_mel;
+  (void)rows;
+  return run_gemm(c->outproj, bb.u16, C, C, B, T, T, e, s);
+}
+
+static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
+  const size_t rows = (size_t)B * T, C = c->C;
+  WS_GET(f16, cp16, rows * c->n_layers * 2 * C);
+  WS_GET(float, h32, rows * C);
+  WS_GET(float, sk, rows * C);
+  WS_GET(f16, y16, rows * C);
+  WS_GET(f16, g16, rows * C);
+  WS_GET(f16, s16, rows * C);
+  WS_GET(f16, u16, rows * C);
+  bb = DenoiseBufs{cp16, h32, sk, y16, g16, s16, u16};
+  return SVC_OK;
+}
+
+static size_t denoise_bytes(svc_ctx* c, int B, int T) {
+  const size_t rows = (size_t)B * T, C = c->C;
+  return rows * c->n_layers * 2 * C * 2 + rows * C * (4 + 4 + 2 * 4) + 16 * 4096;
+}
+
+static int project_cond(svc_ctx* c, const float* cond, int B, int T, const DenoiseBufs& bb, hipStream_t s) {
+  const int rows = B * T, C = c->C;
+  WS_GET(f16, cond16, (size_t)rows * C);
+  int st;
+  if ((st = f32_to_f16(cond, C, cond16, C, rows, C, C, s))) return st;
+  EpiArgs e = epi();
+  e.out16 = bb.cp16;
+  e.ld16 = c->n_layers * 2 * C;
+  return run_gemm(c->cp_all, cond16, C, C, B, T, T, e, s);
+}
+
+svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B, int T, int t, float* eps,
+                           void* stream) {
+  CTX_READY(c);
+  SVC_REQUIRE(c->has_mapper, "mapper weights not loaded");
+  SVC_REQUIRE(t >= 0 && t < c->steps, "eps: t=%d", t);
+  hipStream_t s = (hipStream_t)stream;
+  const int rows = B * T, ld16 = (int)round_up(c->n_mel, 8);
+  int st;
+  if ((st = c->ws.reserve(std::max(denoise_bytes(c, B, T) + (size_t)rows * (ld16 * 2 + c->C * 2) + 8192, c->ws.cap))))
+    return st;
+  c->ws.reset();
+  DenoiseBufs bb;
+  if ((st = alloc_denoise(c, B, T, bb))) return st;
+  if ((st = project_cond(c, cond, B, T, bb, s))) return st;
+  WS_GET(f16, x16, (size_t)rows * ld16);
+  if ((st = f32_to_f16(x, c->n_mel, x16, ld16, rows, c->n_mel, ld16, s))) return st;
+  return denoise(c, bb, x16, B, T, t, eps, s);
+}
+
+svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int mode, int interval, const float* x_T,
+                              const float* noise, uint64_t seed, const int32_t* utt_ids, float* x0, void* stream) {
+  CTX_READY(c);
+  SVC_REQUIRE(c->has_mapper, "mapper weights not loaded");
+  SVC_REQUIRE(mode == SVC_MODE_DDPM || (mode == SVC_MODE_PLMS && interval >= 1), "sample: mode %d interval %d", mode,
+              interval);
+  SVC_REQUIRE(x_T || utt_ids, "sample: need x_T or utt_ids for device noise");
+  hipStream_t s = (hipStream_t)stream;
+  const int rows = B * T, nm = c->n_mel, ld16 = (int)round_up(nm, 8);
+  int st;
+  const size_t extra = (size_t)rows * (ld16 * 2 * 2 + nm * 4 * 8 + c->C * 2) + 32 * 4096;
+  if ((st = c->ws.reserve(std::max(denoise_bytes(c, B, T) + extra, c->ws.cap)))) return st;
+  c->ws.reset();
+  DenoiseBufs bb;
+  if ((st = alloc_denoise(c, B, T, bb))) return st;
+  if ((st = project_cond(c, cond, B, T, bb, s))) return st;
+  float* x = x0;  // the sampler state lives in the output buffer
+  WS_GET(f16, x16, (size_t)rows * ld16);
+  if (x_T) {
+    SVC_HIP_CHECK(hipMemcpyAsync(x, x_T, (size_t)rows * nm * 4, hipMemcpyDeviceToDevice, s));
+    if ((st = f32_to_f16(x, nm, x16, ld16, rows, nm, ld16, s))) return st;
+  } else {
+    if ((st = init_noise(x, x16, ld16, B, T, nm, seed, utt_ids, 1.0f / 1.2f, s))) return st;
+  }
+  WS_GET(float, eps, (size_t)rows * nm);
+  if (mode == SVC_MODE_DDPM) {
+    for (int i = c->steps - 1; i >= 0; --i) {
+      if ((st = denoise(c, bb, x16, B, T, i, eps, s))) return st;
+      DdpmArgs a{};
+      a.sra = c->sra[i];
+      a.srm1 = c->srm1[i];
+      a.c1 = c->pc1[i];
+      a.c2 = c->pc2[i];
+      a.sigma = i > 0 ? expf(0.5f * c->plogvar[i]) : 0.0f;
+      a.z = noise ? noise + (size_t)(c->steps - 1 - i) * rows * nm : nullptr;
+      a.seed = seed;
+      a.utt_ids = utt_ids;
+      a.step = i;
+      if ((st = ddpm_update(x, eps, x16, ld16, B, T, nm, a, s))) return st;
+    }
+    return SVC_OK;
+  }
+  // PLMS: history ring of 4 epsilons + the first step's predictor buffers
+  float* hist[5];
+  for (int k = 0; k < 5; ++k) {
+    WS_GET(float, hb, (size_t)rows * nm);
+    hist[k] = hb;
+  }
+  WS_GET(float, xp, (size_t)rows * nm);
+  WS_GET(f16, xp16, (size_t)rows * ld16);
+  int nh = 0, head = 0;  // hist slots: newest at hist[(head - 1) mod 5]
+  const std::vector<float>& ac = c->alphas_cumprod_f32;
+  for (int i = ((c->steps - 1) / interval) * interval; i >= 0; i -= interval) {
+    const int tp = i - interval > 0 ? i - interval : 0;
+    // get_x_pred coefficients in f32 exactly as the reference's tensor ops (:96-113)
+    const float a_t = ac[i], a_prev = ac[tp];
+    const float a_t_sq = sqrtf(a_t), a_prev_sq = sqrtf(a_prev);
+    const float A = 1.0f / (a_t_sq * (a_t_sq + a_prev_sq));
+    const float Bc = 1.0f / (a_t_sq * (sqrtf((1.0f - a_prev) * a_t) + sqrtf((1.0f - a_t) * a_prev)));
+    const float d = a_prev - a_t;
+    float* ecur = hist[head];
+    if ((st = denoise(c, bb, x16, B, T, i, ecur, s))) return st;
+    PlmsArgs p{};
+    p.d = d;
+    p.A = A;
+    p.Bc = Bc;
+    p.xin = x;
+    p.xout = x;
+    p.x16 = x16;
+    p.ld16 = ld16;
+    auto H = [&](int back) { return hist[((head - back) % 5 + 5) % 5]; };
+    if (nh == 0) {
+      PlmsArgs q = p;
+      q.e[0] = ecur;
+      q.c[0] = 1.0f;
+      q.ne = 1;
+      q.div = 1.0f;
+      q.xout = xp;
+      q.x16 = xp16;
+      if ((st = plms_update(q, rows, nm, s))) return st;
+      float* eprev = hist[(head + 1) % 5];
+      if ((st = denoise(c, bb, xp16, B, T, tp, eprev, s))) return st;
+      p.e[0] = ecur;
+      p.e[1] = eprev;
+      p.c[0] = 1.0f;
+      p.c[1] = 1.0f;
+      p.ne = 2;
+      p.div = 2.0f;
+    } else if (nh == 1) {
+      p.e[0] = ecur;
+      p.e[1] = H(1);
+      p.c[0] = 3.0f;
+      p.c[1] = -1.0f;
+      p.ne = 2;
+      p.div = 2.0f;
+    } else if (nh == 2) {
+      p.e[0] = ecur;
+      p.e[1] = H(1);
+      p.e[2] = H(2);
+      p.c[0] = 23.0f;
+      p.c[1] = -16.0f;
+      p.c[2] = 5.0f;
+      p.ne = 3;
+      p.div = 12.0f;
+    } else {
+      p.e[0] = ecur;
+      p.e[1] = H(1);
+      p.e[2] = H(2);
+      p.e[3] = H(3);
+      p.c[0] = 55.0f;
+      p.c[1] = -59.0f;
+      p.c[2] = 37.0f;
+      p.c[3] = -9.0f;
+      p.ne = 4;
+      p.div = 24.0f;
+    }
+    if ((st = plms_update(p, rows, nm, s))) return st;
+    head = (head + 1) % 5;
+    nh = nh < 4 ? nh + 1 : 4;
+  }
+  return SVC_OK;
+}
+
+// ---------------------------------------------------------------------------- BigVGAN
+svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, float* mel_out, void* stream) {
+  CTX_READY(c);
+  SVC_REQUIRE(c->has_vocoder && c->has_mapper, "vocoder (and mapper stats) not loaded");
+  hipStream_t s = (hipStream_t)stream;
+  const int nm = c->v_in, ldm = (int)round_up(nm, 8);
+  const int Lmax_c = c->v_c0 * 2;  // max over stages of L_i*C_i / T  (6144 for the reference config)
+  int maxLC = 0, Lr = T;
+  for (auto& S : c->vstages) {
+    Lr *= S.rate;
+    maxLC = std::max(maxLC, (Lr / T) * S.cout);
+  }
+  (void)Lmax_c;
+  const size_t big = (size_t)B * T * maxLC;
+  const size_t need = (size_t)B * T * ldm * 2 + (size_t)B * T * c->v_c0 * 2 + big * (4 * 4 + 2 * 2) + 32 * 4096;
+  int st;
+  if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
+  c->ws.reset();
+  SVC_REQUIRE(T * c->hop_out >= c->nfade, "bigvgan: T=%d shorter than the fade-out", T);
+  WS_GET(f16, mel16, (size_t)B * T * ldm);
+  if ((st = denorm_mel(x0, mel16, mel_out, ldm, B * T, nm, c->mel_min, c->mel_max, s))) return st;
+  WS_GET(f16, pre16, (size_t)B * T * c->v_c0);
+  EpiArgs e = epi();
+  e.out16 = pre16;
+  e.ld16 = c->v_c0;
+  if ((st = run_gemm(c->vpre, mel16, ldm, nm, B, T, T, e, s))) return st;
+  WS_GET(float, X, big);
+  WS_GET(float, Xj, big);
+  WS_GET(float, tmp, big);
+  WS_GET(float, XS, big);
+  WS_GET(f16, a16, big);
+  WS_GET(f16, next16, big);
+  const f16* in16 = pre16;
+  int L = T;
+  const int ns = (int)c->vstages.size();
+  for (int i = 0; i < ns; ++i) {
+    VStage& S = c->vstages[i];
+    const int Lin = L;
+    L = Lin * S.rate;
+    const int ch = S.cout;
+    // ConvTranspose1d as `rate` phase GEMMs writing rows t*rate + r
+    for (int r = 0; r < S.rate; ++r) {
+      EpiArgs u = epi();
+      u.T_ostore = L;
+      u.ostride = S.rate;
+      u.ophase = r;
+      u.out32 = X;
+      u.ld32 = ch;
+      if ((st = run_gemm(S.phases[r], in16, S.cin, S.cin, B, Lin, Lin, u, s))) return st;
+    }
+    const int nk = (int)S.c1.size();
+    for (int j = 0; j < nk; ++j) {
+      const int nd = (int)S.c1[j].size();
+      for (int l = 0; l < nd; ++l) {
+        const float* src = (l == 0) ? X : Xj;
+        if ((st = activation1d(src, a16, B, L, ch, ch, S.acts[j][2 * l].alpha, S.acts[j][2 * l].beta,
+                               S.acts[j][2 * l].filt, s)))
+          return st;
+        EpiArgs e1 = epi();
+        e1.out32 = tmp;
+        e1.ld32 = ch;
+        if ((st = run_gemm(S.c1[j][l], a16, ch, ch, B, L, L, e1, s))) return st;
+        if ((st = activation1d(tmp, a16, B, L, ch, ch, S.acts[j][2 * l + 1].alpha, S.acts[j][2 * l + 1].beta,
+                               S.acts[j][2 * l + 1].filt, s)))
+          return st;
+        EpiArgs e2 = epi();
+        e2.add_row = src;
+        e2.ld_add_row = ch;
+        if (l + 1 < nd) {
+          e2.out32 = Xj;
+          e2.ld32 = ch;
+        } else if (j == 0) {
+          e2.out32 = XS;
+          e2.ld32 = ch;
+        } else {
+          e2.acc32 = XS;
+          e2.ld_acc = ch;
+          if (j + 1 == nk) {
+            e2.acc_div = (float)nk;
+            if (i + 1 < ns) {
+              e2.out16 = next16;
+              e2.ld16 = ch;
+            } else {
+              e2.out32 = XS;
+              e2.ld32 = ch;
+            }
+          } else {
+            e2.out32 = XS;
+            e2.ld32 = ch;
+          }
+        }
+        if ((st = run_gemm(S.c2[j][l], a16, ch, ch, B, L, L, e2, s))) return st;
+      }
+    }
+    in16 = next16;  // stage output (f16) feeds the next ConvTranspose; it is rewritten only after that ran
+  }
+  const int chl = c->vstages.back().cout;
+  if ((st = activation1d(XS, a16, B, L, chl, chl, c->vact_post.alpha, c->vact_post.beta, c->vact_post.filt, s)))
+    return st;
+  return conv_post(a16, chl, B, L, chl, c->vpost_w, c->vpost_b, c->fade, c->nfade, wav, s);
+}
+
+// ---------------------------------------------------------------------------- op-level (tests)
+static int op_ws(svc_ctx** tmp) {
+  static svc_ctx* g = nullptr;
+  if (!g) {
+    g = new svc_ctx();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    g->device = dev;
+    g->finalized = true;
+  }
+  *tmp = g;
+  return SVC_OK;
+}
+
+static int pack_from_device(svc_ctx* c, PackedGemm& g, const float* w_dev, size_t wn, const float* b_dev, int bn,
+                            std::vector<float>& wh, std::vector<float>& bh) {
+  wh.resize(wn);
+  bh.assign(bn, 0.0f);
+  SVC_HIP_CHECK(hipDeviceSynchronize());
+  SVC_HIP_CHECK(hipMemcpy(wh.data(), w_dev, wn * 4, hipMemcpyDeviceToHost));
+  if (b_dev) SVC_HIP_CHECK(hipMemcpy(bh.data(), b_dev, bn * 4, hipMemcpyDeviceToHost));
+  (void)c;
+  (void)g;
+  return SVC_OK;
+}
+
+static void free_packed(svc_ctx* c, PackedGemm& g) {
+  // op-level packs are temporary: release the two allocations made by pack_gemm
+  for (void* p : {(void*)g.W, (void*)g.bias}) {
+    for (auto it = c->allocs.begin(); it != c->allocs.end(); ++it)
+      if (*it == p) {
+        c->allocs.erase(it);
+        break;
+      }
+    (void)hipFree(p);
+  }
+}
+
+svc_status svc_op_conv1d(const float* x, int B, int T_in, int Cin, const float* w, const float* bias, int Cout, int k,
+                         int stride, int dilation, int pad, int act, float* y, void* stream) {
+  svc_ctx* c;
+  op_ws(&c);
+  hipStream_t s = (hipStream_t)stream;
+  const int T_out = (T_in + 2 * pad - dilation * (k - 1) - 1) / stride + 1;
+  SVC_REQUIRE(T_out > 0, "op_conv1d: T_out=%d", T_out);
+  std::vector<float> wh, bh;
+  PackedGemm g;
+  int st;
+  if ((st = pack_from_device(c, g, w, (size_t)Cout * Cin * k, bias, Cout, wh, bh))) return st;
+  const int Cp = (int)round_up(Cin, 8);
+  if ((st = pack_conv1d(c, g, wh.data(), bh.data(), Cout, Cin, k, Cp, dilation, pad, stride))) return st;
+  if ((st = c->ws.reserve(std::max((size_t)B * T_in * Cp * 2 + 4096, c->ws.cap)))) return st;
+  c->ws.reset();
+  WS_GET(f16, x16, (size_t)B * T_in * Cp);
+  if ((st = f32_to_f16(x, Cin, x16, Cp, B * T_in, Cin, Cp, s))) return st;
+  EpiArgs e = epi();
+  e.act = act;
+  e.out32 = y;
+  e.ld32 = Cout;
+  st = run_gemm(g, x16, Cp, Cin, B, T_in, T_out, e, s);
+  (void)hipStreamSynchronize(s);
+  free_packed(c, g);
+  return st;
+}
+
+svc_status svc_op_conv_transpose1d(const float* x, int B, int T_in, int Cin, const float* w, const float* bias,
+                                   int Cout, int k, int stride, int pad, float* y, void* stream) {
+  svc_ctx* c;
+  op_ws(&c);
+  hipStream_t s = (hipStream_t)stream;
+  const int T_out = (T_in - 1) * stride - 2 * pad + k;
+  SVC_REQUIRE(T_out == T_in * stride, "op_conv_transpose1d: only T_out = T_in*stride supported (got %d)", T_out);
+  SVC_REQUIRE(Cin % 8 == 0, "op_conv_transpose1d: Cin %% 8");
+  std::vector<float> wh, bh;
+  PackedGemm g;
+  int st;
+  if ((st = pack_from_device(c, g, w, (size_t)Cout * Cin * k, bias, Cout, wh, bh))) return st;
+  std::vector<PackedGemm> ph;
+  if ((st = pack_conv_transpose(c, ph, wh.data(), nullptr, bh.data(), Cin, Cout, k, stride, pad))) return st;
+  if ((st = c->ws.reserve(std::max((size_t)B * T_in * Cin * 2 + 4096, c->ws.cap)))) return st;
+  c->ws.reset();
+  WS_GET(f16, x16, (size_t)B * T_in * Cin);
+  if ((st = f32_to_f16(x, Cin, x16, Cin, B * T_in, Cin, Cin, s))) return st;
+  for (int r = 0; r < stride && !st; ++r) {
+    EpiArgs e = epi();
+    e.T_ostore = T_out;
+    e.ostride = stride;
+    e.ophase = r;
+    e.out32 = y;
+    e.ld32 = Cout;
+    st = run_gemm(ph[r], x16, Cin, Cin, B, T_in, T_in, e, s);
+  }
+  (void)hipStreamSynchronize(s);
+  for (auto& p : ph) free_packed(c, p);
+  return st;
+}
+
+svc_status svc_op_activation1d(const float* x, int B, int L, int C, const float* al, const float* be, const float* f,
+                               float* y, void* stream) {
+  svc_ctx* c;
+  op_ws(&c);
+  hipStream_t s = (hipStream_t)stream;
+  int st;
+  if ((st = c->ws.reserve(std::max((size_t)B * L * C * 2 + 4096, c->ws.cap)))) return st;
+  c->ws.reset();
+  WS_GET(f16, y16, (size_t)B * L * C);
+  if ((st = activation1d(x, y16, B, L, C, C, al, be, f, s))) return st;
+  // widen for the caller (the product path feeds the f16 tensor straight into the next conv)
+  return f16_to_f32(y16, y, (int64_t)B * L * C, s);
+}
+
+svc_status svc_op_attention(const float* q, const float* k, const float* v, int B, int L, int D, float* out,
+                            void* stream) {
+  svc_ctx* c;
+  op_ws(&c);
+  hipStream_t s = (hipStream_t)stream;
+  int st;
+  const size_t rows = (size_t)B * L;
+  if ((st = c->ws.reserve(std::max(rows * D * 2 * 4 + 4096, c->ws.cap)))) return st;
+  c->ws.reset();
+  WS_GET(f16, qkv, rows * 3 * D);
+  WS_GET(f16, o16, rows * D);
+  if ((st = pack_qkv(q, k, v, qkv, (int64_t)rows, D, powf(64.0f, -0.25f), s))) return st;
+  if ((st = attention(qkv, o16, B, L, D, s))) return st;
+  return f16_to_f32(o16, out, (int64_t)rows * D, s);
+}
+
+svc_status svc_op_layernorm(const float* x, const float* g, const float* b, int rows, int D, float* y, void* stream) {
+  return layernorm_f32(x, g, b, y, rows, D, D, (hipStream_t)stream);
+}
+
+}  // extern "C"

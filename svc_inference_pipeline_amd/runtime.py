@@ -1,0 +1,189 @@
+"""Host-side engine: owns one libsvc_hip context per device and exposes each hot-path stage on
+torch device tensors (PyTorch supplies device memory and the HIP stream; all compute is in
+libsvc_hip.so). Layout of every tensor is time-major [B, T, C] (row = b*T + t).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import weights as W
+from .config import load_stats, noise_schedule
+
+MODE_DDPM, MODE_PLMS = 0, 1
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    assert t.is_cuda and t.is_contiguous(), "libsvc_hip takes contiguous device tensors"
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def mel_frames(n_samples, n_fft=1024, hop=256):
+    """utils/mel.py:148-167 frame count (reflect pad (n_fft-hop)/2 each side, center=False)."""
+    return (n_samples + (n_fft - hop) - n_fft) // hop + 1
+
+
+class SVCEngine:
+    """Stages of infer.py on one GPU. `whisper_state`, `mapper_state`, `vocoder_state` are dicts in the
+    reference's state_dict naming (svc_inference_pipeline_amd.weights); any subset may be given."""
+
+    def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None):
+        _lib.load()
+        self.cfg = cfg
+        self.device = device
+        self._ctx = ctypes.c_void_p()
+        torch.cuda.set_device(device)
+        _lib.call("svc_ctx_create", device, ctypes.byref(self._ctx))
+        self._keep = []
+        self._set_config()
+        if whisper_state is not None:
+            self._add_state("whisper.", whisper_state)
+            self.whisper_dims = W.whisper_dims_from_state(whisper_state)
+        if mapper_state is not None:
+            self._add_state("mapper.", mapper_state)
+            self._add("mapper.step_table", W.step_embedding_table(len(noise_schedule(cfg.mapper))).numpy())
+            st = load_stats(cfg)
+            self._add("stats.mel_min", st["mel_min"])
+            self._add("stats.mel_max", st["mel_max"])
+            self.target_f0_median = st["target_f0_median"]
+        if vocoder_state is not None:
+            self._add_state("vocoder.", vocoder_state)
+            self._add("vocoder.fade_out", W.fade_out_table(20 * cfg.hop_length).numpy())
+        _lib.call("svc_ctx_finalize", self._ctx)
+        self._keep = []
+
+    # ------------------------------------------------------------------ setup
+    def _set_config(self):
+        c = self.cfg
+        kv = {k: getattr(c, k) for k in ("fs", "n_fft", "hop_length", "win_length", "n_mels", "fmin", "fmax", "f0_min", "f0_max")}
+        m = c.mapper
+        for k in ("residual_channels", "residual_layer_num", "n_mel", "diffusion_fc_size", "dilation_cycle_length",
+                  "residual_kernel_size"):
+            kv["mapper." + k] = m[k]
+        kv["mapper.noise_schedule_factors.0"] = m.noise_schedule_factors[0]
+        kv["mapper.noise_schedule_factors.1"] = m.noise_schedule_factors[1]
+        v = c.vocoder
+        kv["vocoder.n_stages"] = len(v.upsample_rates)
+        kv["vocoder.n_kernels"] = len(v.resblock_kernel_sizes)
+        kv["vocoder.upsample_initial_channel"] = v.upsample_initial_channel
+        kv["vocoder.input_dim"] = v.input_dim
+        for i, (u, k) in enumerate(zip(v.upsample_rates, v.upsample_kernel_sizes)):
+            kv[f"vocoder.upsample_rates.{i}"] = u
+            kv[f"vocoder.upsample_kernel_sizes.{i}"] = k
+        for j, (k, ds) in enumerate(zip(v.resblock_kernel_sizes, v.resblock_dilation_sizes)):
+            kv[f"vocoder.resblock_kernel_sizes.{j}"] = k
+            kv[f"vocoder.resblock_dilation_sizes.{j}.n"] = len(ds)
+            for l, d in enumerate(ds):
+                kv[f"vocoder.resblock_dilation_sizes.{j}.{l}"] = d
+        for k, val in kv.items():
+            _lib.call("svc_ctx_set_config", self._ctx, k.encode(), float(val))
+
+    def _add(self, name, arr):
+        a = np.ascontiguousarray(np.asarray(arr, dtype=np.float32))
+        self._keep.append(a)
+        shape = (ctypes.c_int64 * max(a.ndim, 1))(*a.shape)
+        _lib.call("svc_ctx_add_param", self._ctx, name.encode(), a.ctypes.data_as(ctypes.c_void_p), a.ndim, shape)
+
+    def _add_state(self, prefix, sd):
+        for k, v in sd.items():
+            self._add(prefix + k, v.numpy() if isinstance(v, torch.Tensor) else v)
+
+    def close(self):
+        if self._ctx:
+            _lib.call("svc_ctx_destroy", self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def memory(self):
+        wb, wsb = ctypes.c_int64(), ctypes.c_int64()
+        _lib.call("svc_ctx_memory", self._ctx, ctypes.byref(wb), ctypes.byref(wsb))
+        return wb.value, wsb.value
+
+    # ------------------------------------------------------------------ stages
+    def mel_energy(self, wav24):
+        """wav24 f32 [B, N] -> (log-mel f32 [B, T, n_mels], energy f32 [B, T]) — utils/mel.py:179-201."""
+        B, N = wav24.shape
+        T = mel_frames(N, self.cfg.n_fft, self.cfg.hop_length)
+        mel = torch.empty(B, T, self.cfg.n_mels, device=wav24.device, dtype=torch.float32)
+        en = torch.empty(B, T, device=wav24.device, dtype=torch.float32)
+        _lib.call("svc_mel_energy", self._ctx, _ptr(wav24), B, N, _ptr(mel), _ptr(en), _stream())
+        return mel, en
+
+    def f0(self, wav24, T):
+        """Praat-AC F0 padded to T frames (utils/f0.py:120-161) -> f64 [B, T]."""
+        B, N = wav24.shape
+        f0 = torch.empty(B, T, device=wav24.device, dtype=torch.float64)
+        _lib.call("svc_f0_ac", self._ctx, _ptr(wav24), B, N, T, _ptr(f0), _stream())
+        return f0
+
+    def pitch_shift(self, f0, target_median=None):
+        """In place: f0 *= target_median / median(voiced f0) per utterance
+        (utils/acoustic_feature_extraction.py:33-52). f0 f64 [B, T]."""
+        B, T = f0.shape
+        tm = self.target_f0_median if target_median is None else target_median
+        _lib.call("svc_pitch_shift", self._ctx, _ptr(f0), B, T, float(tm), _stream())
+        return f0
+
+    def whisper_encode(self, wav16):
+        """wav16 f32 [B, N16] -> Whisper encoder output f32 [B, n_ctx, D] (utils/whisper.py:13-28)."""
+        B, N = wav16.shape
+        d = self.whisper_dims
+        feats = torch.empty(B, d["n_audio_ctx"], d["n_audio_state"], device=wav16.device, dtype=torch.float32)
+        _lib.call("svc_whisper_encode", self._ctx, _ptr(wav16), B, N, _ptr(feats), _stream())
+        return feats
+
+    def map_content(self, feats, T):
+        """15:8 repeat/average to mel frames (utils/whisper.py:31-81) -> f16 [B, T, D]."""
+        B, S, D = feats.shape
+        out = torch.empty(B, T, D, device=feats.device, dtype=torch.float16)
+        _lib.call("svc_map_content", self._ctx, _ptr(feats), B, S, T, D, _ptr(out), _stream())
+        return out
+
+    def condition(self, content16, f0, energy, singer):
+        """EncoderFramework.forward (modules/encoder.py:165-201) -> cond f32 [B, T, C]."""
+        B, T, _ = content16.shape
+        cond = torch.empty(B, T, self.cfg.mapper.residual_channels, device=content16.device, dtype=torch.float32)
+        singer = singer.to(torch.int32).contiguous()
+        _lib.call("svc_condition", self._ctx, _ptr(content16), _ptr(f0.contiguous()), _ptr(energy.contiguous()),
+                  _ptr(singer), B, T, _ptr(cond), _stream())
+        return cond
+
+    def diffsvc_eps(self, cond, x, t):
+        B, T, _ = cond.shape
+        eps = torch.empty_like(x)
+        _lib.call("svc_diffsvc_eps", self._ctx, _ptr(cond), _ptr(x), B, T, int(t), _ptr(eps), _stream())
+        return eps
+
+    def diffsvc_sample(self, cond, fast_inference=False, speedup=10, x_T=None, noise=None, seed=0, utt_ids=None):
+        """svc_model_inference (modules/diffsvcrepo_inference.py:154-240) -> normalised mel x_0 f32 [B, T, n_mel]."""
+        B, T, _ = cond.shape
+        x0 = torch.empty(B, T, self.cfg.mapper.n_mel, device=cond.device, dtype=torch.float32)
+        if x_T is None and utt_ids is None:
+            utt_ids = torch.arange(B, device=cond.device, dtype=torch.int32)
+        uid = utt_ids.to(torch.int32).contiguous() if utt_ids is not None else None
+        mode = MODE_PLMS if fast_inference else MODE_DDPM
+        _lib.call("svc_diffsvc_sample", self._ctx, _ptr(cond), B, T, mode, int(speedup),
+                  _ptr(x_T.contiguous()) if x_T is not None else None,
+                  _ptr(noise.contiguous()) if noise is not None else None, ctypes.c_uint64(seed), _ptr(uid),
+                  _ptr(x0), _stream())
+        return x0
+
+    def bigvgan(self, x0, return_mel=False):
+        """denormalize_mel_channel + synthesis_audios (Generator, trim, fade) -> wav f32 [B, T*hop]."""
+        B, T, _ = x0.shape
+        wav = torch.empty(B, T * self.cfg.hop_length, device=x0.device, dtype=torch.float32)
+        mel = torch.empty_like(x0) if return_mel else None
+        _lib.call("svc_bigvgan", self._ctx, _ptr(x0.contiguous()), B, T, _ptr(wav), _ptr(mel), _stream())
+        return (wav, mel) if return_mel else wav

@@ -1,0 +1,111 @@
+"""GPU parity, op level: every HIP kernel family against a torch-CPU fp32 reference of the same op.
+
+Tolerances: MFMA operands are fp16 (inputs and weights rounded to binary16, fp32 accumulation), so
+GEMM-shaped ops are checked with a relative L2 error <= 2e-3 (fp16 unit roundoff 4.9e-4, a few
+roundings per output); element-wise f32 ops with fp16 outputs <= 1e-3; frame counts and index maps
+bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from gpu_util import call, dev, ptr, rel_l2, stream  # noqa: E402
+from oracle import models as OM  # noqa: E402
+
+
+def _tm(x):  # [B, C, T] -> time-major [B*T, C]
+    return x.permute(0, 2, 1).contiguous()
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k,stride,dil,pad,act", [
+    (2, 93, 384, 768, 3, 1, 1, 1, 0),        # DiffSVC dilated conv, d=1
+    (2, 93, 384, 768, 3, 1, 8, 8, 0),        # d=8
+    (1, 200, 100, 384, 1, 1, 1, 0, 2),       # mel_preprocess (Cin not a multiple of 8/64), relu
+    (2, 60, 80, 128, 3, 1, 1, 1, 1),         # whisper conv1 (gelu)
+    (2, 60, 128, 128, 3, 2, 1, 1, 1),        # whisper conv2 (stride 2)
+    (1, 37, 100, 1536, 7, 1, 1, 3, 0),       # conv_pre
+    (2, 301, 24, 24, 11, 1, 5, 25, 0),       # last BigVGAN stage
+    (1, 130, 48, 48, 7, 1, 3, 9, 0),
+    (1, 70, 96, 96, 3, 1, 1, 1, 0),
+    (3, 17, 384, 100, 1, 1, 1, 0, 0),        # output projection (N=100)
+])
+def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(B, Cin, T, generator=g)
+    w = torch.randn(Cout, Cin, k, generator=g) / np.sqrt(Cin * k)
+    b = torch.randn(Cout, generator=g) * 0.1
+    ref = F.conv1d(x, w, b, stride=stride, padding=pad, dilation=dil)
+    ref = [ref, F.gelu(ref), F.relu(ref)][act]
+    To = ref.shape[-1]
+    y = torch.empty(B * To, Cout, device="cuda")
+    xd, wd, bd = dev(_tm(x)), dev(w), dev(b)  # keep device tensors alive across the call
+    call("svc_op_conv1d", ptr(xd), B, T, Cin, ptr(wd), ptr(bd), Cout, k, stride, dil, pad, act, ptr(y), stream())
+    out = y.cpu().view(B, To, Cout).permute(0, 2, 1).numpy()
+    assert rel_l2(out, ref.numpy()) < 2e-3
+
+
+@pytest.mark.parametrize("B,T,Cin,Cout,k,s", [(2, 25, 768, 384, 8, 4), (1, 40, 96, 48, 4, 2), (2, 33, 48, 24, 4, 2),
+                                              (1, 9, 1536, 768, 8, 4)])
+def test_conv_transpose1d(B, T, Cin, Cout, k, s):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(B, Cin, T, generator=g)
+    w = torch.randn(Cin, Cout, k, generator=g) / np.sqrt(Cin * k / s)
+    b = torch.randn(Cout, generator=g) * 0.1
+    pad = (k - s) // 2
+    ref = F.conv_transpose1d(x, w, b, stride=s, padding=pad)
+    To = ref.shape[-1]
+    assert To == T * s
+    y = torch.empty(B * To, Cout, device="cuda")
+    xd, wd, bd = dev(_tm(x)), dev(w), dev(b)
+    call("svc_op_conv_transpose1d", ptr(xd), B, T, Cin, ptr(wd), ptr(bd), Cout, k, s, pad, ptr(y), stream())
+    out = y.cpu().view(B, To, Cout).permute(0, 2, 1).numpy()
+    assert rel_l2(out, ref.numpy()) < 2e-3
+
+
+@pytest.mark.parametrize("B,L,C", [(2, 37, 24), (1, 1, 24), (1, 2, 48), (3, 129, 96), (1, 300, 768), (2, 64, 40)])
+def test_activation1d(B, L, C):
+    from svc_inference_pipeline_amd import weights as W
+    g = torch.Generator().manual_seed(2)
+    x = torch.randn(B, C, L, generator=g) * 2
+    al = torch.randn(C, generator=g) * 0.3
+    be = torch.randn(C, generator=g) * 0.3
+    f = W.kaiser_sinc_filter1d(0.25, 0.3, 12).view(-1)
+    ref = OM.activation1d(x, al, be, f)
+    y = torch.empty(B * L, C, device="cuda")
+    xd, ad, bd, fd = dev(_tm(x)), dev(al), dev(be), dev(f)
+    call("svc_op_activation1d", ptr(xd), B, L, C, ptr(ad), ptr(bd), ptr(fd), ptr(y), stream())
+    out = y.cpu().view(B, L, C).permute(0, 2, 1).numpy()
+    assert rel_l2(out, ref.numpy()) < 1e-3
+    # fp16 output rounding bound, element-wise
+    assert np.max(np.abs(out - ref.numpy()) / (np.abs(ref.numpy()) + 1e-2)) < 5e-3
+
+
+@pytest.mark.parametrize("B,L,D", [(1, 1500, 1024), (2, 100, 128), (1, 64, 64), (2, 1, 64), (1, 129, 256)])
+def test_attention(B, L, D):
+    g = torch.Generator().manual_seed(3)
+    q, k, v = (torch.randn(B, L, D, generator=g) for _ in range(3))
+    H = D // 64
+    sc = 64 ** -0.25
+    qh = q.view(B, L, H, 64).permute(0, 2, 1, 3) * sc
+    kh = k.view(B, L, H, 64).permute(0, 2, 3, 1) * sc
+    vh = v.view(B, L, H, 64).permute(0, 2, 1, 3)
+    ref = (F.softmax(qh @ kh, dim=-1) @ vh).permute(0, 2, 1, 3).reshape(B, L, D)
+    out = torch.empty(B * L, D, device="cuda")
+    qd, kd, vd = dev(q.reshape(B * L, D)), dev(k.reshape(B * L, D)), dev(v.reshape(B * L, D))
+    call("svc_op_attention", ptr(qd), ptr(kd), ptr(vd), B, L, D, ptr(out), stream())
+    assert rel_l2(out.cpu().view(B, L, D).numpy(), ref.numpy()) < 3e-3
+
+
+def test_layernorm():
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(300, 1024, generator=g) * 3 + 1
+    gm = torch.randn(1024, generator=g)
+    bt = torch.randn(1024, generator=g)
+    ref = F.layer_norm(x, (1024,), gm, bt)
+    y = torch.empty(300, 1024, device="cuda")
+    xd, gd, bd = dev(x), dev(gm), dev(bt)
+    call("svc_op_layernorm", ptr(xd), ptr(gd), ptr(bd), 300, 1024, ptr(y), stream())
+    np.testing.assert_allclose(y.cpu().numpy(), ref.numpy(), rtol=0, atol=2e-5)

@@ -1,0 +1,52 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol include/svc_hip.h declares; the
+native slaney filterbank matches the reference's mel_filters.npz known answer."""
+import ctypes
+import os
+import re
+
+import numpy as np
+
+from svc_inference_pipeline_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(REPO, "include", "svc_hip.h")).read()
+    return sorted(set(re.findall(r"^(?:svc_status|const char\*|int)\s+(svc_[a-z0-9_]+)\s*\(", txt, re.M)))
+
+
+def test_header_matches_binding():
+    assert header_symbols() == sorted(_lib.PROTOTYPES)
+
+
+def test_library_exports_all_symbols():
+    lib = _lib.load()
+    for name in header_symbols():
+        assert hasattr(lib, name), name
+    assert lib.svc_abi_version() == 1
+
+
+def test_native_mel_filterbank_kat(golden):
+    kat = golden("mel_filters_kat")["mel_80"]
+    out = np.zeros((80, 201), dtype=np.float32)
+    _lib.call("svc_mel_filterbank", 16000, 400, 80, 0.0, 8000.0, out.ctypes.data_as(ctypes.c_void_p))
+    assert np.max(np.abs(out - kat)) <= 2e-7 * np.abs(kat).max()
+
+
+def test_native_mel_filterbank_24k():
+    from oracle.features import slaney_mel_filterbank
+    ref = slaney_mel_filterbank(24000, 1024, 100, 0.0, 12000.0)
+    out = np.zeros_like(ref)
+    _lib.call("svc_mel_filterbank", 24000, 1024, 100, 0.0, 12000.0, out.ctypes.data_as(ctypes.c_void_p))
+    assert np.max(np.abs(out - ref)) <= 2e-7 * np.abs(ref).max()
+
+
+def test_no_gpu_error_is_loud():
+    """Without a GPU, creating a context fails with a status + message (no silent fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        return
+    ctx = ctypes.c_void_p()
+    st = _lib.load().svc_ctx_create(0, ctypes.byref(ctx))
+    assert st != 0 and _lib.load().svc_last_error()
