@@ -50,6 +50,8 @@ static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// saturating fp32 -> fp16 store (NaN stays NaN): random-weight regimes can exceed the fp16 range
+__device__ __forceinline__ f16 f16_sat(float v) { return (f16)(v > 65504.f ? 65504.f : (v < -65504.f ? -65504.f : v)); }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 // ------------------------------------------------------------------ implicit-GEMM descriptors

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void activation1d_kernel(const float* __restri
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 12; ++k) acc += f[k] * ss[2 * r + k][cl];
-    y[((int64_t)b * L + t) * ldy + c] = (f16)acc;
+    y[((int64_t)b * L + t) * ldy + c] = f16_sat(acc);
   }
 }
 
@@ -152,7 +152,7 @@ __global__ void f32_to_f16_kernel(const float* __restrict__ x, int ldx, f16* __r
   int64_t n = (int64_t)rows * Cpad;
   if (i >= n) return;
   int r = (int)(i / Cpad), c = (int)(i - (int64_t)r * Cpad);
-  y[(int64_t)r * ldy + c] = c < C ? (f16)x[(int64_t)r * ldx + c] : (f16)0.0f;
+  y[(int64_t)r * ldy + c] = c < C ? f16_sat(x[(int64_t)r * ldx + c]) : (f16)0.0f;
 }
 
 int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s) {
@@ -202,7 +202,7 @@ __global__ void denorm_mel_kernel(const float* __restrict__ x, f16* __restrict__
     v = (x[(int64_t)r * C + c] + 1.0f) / 2.0f * (mx[c] - mn[c] + 1e-12f) + mn[c];
     if (y32) y32[(int64_t)r * C + c] = v;
   }
-  y[i] = (f16)v;
+  y[i] = f16_sat(v);
 }
 
 int denorm_mel(const float* x, f16* y, float* y32, int ldy, int rows, int C, const float* mn, const float* mx,
@@ -297,7 +297,7 @@ __global__ void plms_kernel(PlmsArgs p, int rows, int C) {
   if (p.x16) {
     int64_t r = i / C;
     int c = (int)(i - r * C);
-    p.x16[r * p.ld16 + c] = (f16)xn;
+    p.x16[r * p.ld16 + c] = f16_sat(xn);
   }
 }
 
@@ -343,7 +343,7 @@ __global__ void init_noise_kernel(float* x, f16* x16, int ld16, int T, int C, ui
   int b = (int)(r / T), t = (int)(r - (int64_t)b * T);
   float v = std * philox_normal(seed, (uint32_t)utt_ids[b], 0xFFFFFFFFu, (uint32_t)(t * C + c));
   x[i] = v;
-  x16[r * ld16 + c] = (f16)v;
+  x16[r * ld16 + c] = f16_sat(v);
 }
 
 int init_noise(float* x, f16* x16, int ld16, int B, int T, int C, uint64_t seed, const int* utt_ids, float std,
@@ -381,7 +381,7 @@ __global__ void ddpm_kernel(float* x, const float* eps, f16* x16, int ld16, int 
   }
   float xn = mean + a.sigma * z;
   x[i] = xn;
-  x16[r * ld16 + c] = (f16)xn;
+  x16[r * ld16 + c] = f16_sat(xn);
 }
 
 int ddpm_update(float* x, const float* eps, f16* x16, int ld16, int B, int T, int C, const DdpmArgs& a, hipStream_t s) {

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
             v = v + e.emb_l[(int64_t)e.idx_l[m] * e.ld_emb + n];
             v = v + e.emb_s[(int64_t)e.singer[b] * e.ld_emb + n];
             e.out32[orow * e.ld32 + n] = v;
-            if (e.out16) e.out16[orow * e.ld16 + n] = (f16)v;
+            if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(v);
             continue;
           }
           if (e.bias) v += e.bias[n];
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
             if (e.acc_div != 1.0f) v = v / e.acc_div;
           }
           if (e.out32) e.out32[orow * e.ld32 + n] = v;
-          if (e.out16) e.out16[orow * e.ld16 + n] = (f16)(e.add16 ? v + e.add16[n] : v);
+          if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(e.add16 ? v + e.add16[n] : v);
         }
       }
     }
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
             v1 += (float)cpr[n];
             v2 += (float)cpr[n + 16];
             float g = sigmoidf_(v1) * tanhf(v2);
-            e.y16[(int64_t)m * e.ldy16 + ch] = (f16)g;
+            e.y16[(int64_t)m * e.ldy16 + ch] = f16_sat(g);
           } else {  // EPI_RESSKIP
             const int64_t o = (int64_t)m * e.ldx32 + ch;
             float xn = (e.x32[o] + v1) / 1.41421356237309515f;
@@ -226,9 +226,9 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
             float sk = e.skip_first ? v2 : (v2 + e.skip32[o]);
             e.skip32[o] = sk;
             if (e.last_layer) {
-              e.y16[(int64_t)m * e.ldy16 + ch] = (f16)(sk / e.skip_scale);
+              e.y16[(int64_t)m * e.ldy16 + ch] = f16_sat(sk / e.skip_scale);
             } else {
-              e.y16[(int64_t)m * e.ldy16 + ch] = (f16)(xn + e.dnext[ch]);
+              e.y16[(int64_t)m * e.ldy16 + ch] = f16_sat(xn + e.dnext[ch]);
             }
           }
         }

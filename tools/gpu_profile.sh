@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round profiling on the GPU box (run from the repo root via gpurun):
+#   1. bench.py (N=1, with the CPU baseline)              -> gpurun_out/$TAG/bench.json
+#   2. rocprofv3 --kernel-trace --stats of the same bench -> gpurun_out/$TAG/trace/*kernel_stats.csv
+#   3. two separate PMC passes (FETCH_SIZE, WRITE_SIZE) on the dominant kernel family
+# Every GPU step has its own time limit; the script stops at the first failure.
+set -euo pipefail
+TAG=${1:-prof}
+R=$(pwd)
+OUT=$R/gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+STEPS=${STEPS:-3}
+timeout -k 10 900 python3 bench.py --steps $STEPS --warmup 1 > $OUT/bench.json 2> $OUT/bench.err
+echo "bench done"; tail -c 600 $OUT/bench.json
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/trace_bench.json 2> $OUT/trace_bench.err
+echo "trace done"
+KRE=${KRE:-conv_gemm_kernel<128, 128, true>}
+timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_fetch.err
+echo "pmc fetch done"
+timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/pmc_write -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_write.err
+echo "pmc write done"
+find $OUT -name "*.csv" | head -20

@@ -1,0 +1,76 @@
+"""Summarise a tools/gpu_profile.sh run into profiles/: kernel stats CSV + per-launch HBM traffic.
+
+HBM bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE reports exactly
+half of the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is
+exact for 16-B/lane stores (our epilogue stores are narrower: treat it as an estimate), both in KiB.
+Infinity-Cache hits are counted as fetches, so the figure is an upper bound on DRAM traffic.
+Usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<round-prefix>
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+NAME_MAP = {
+    "conv_gemm_kernel<128, 128, true>": "conv_gemm<128,128,pair>",
+    "conv_gemm_kernel<128, 128, false>": "conv_gemm<128,128>",
+    "conv_gemm_kernel<256, 64, false>": "conv_gemm<256,64>",
+    "conv_gemm_kernel<256, 32, false>": "conv_gemm<256,32>",
+    "attention_kernel": "attention",
+    "activation1d_kernel": "activation1d",
+}
+
+
+def short(name):
+    for k, v in NAME_MAP.items():
+        if k in name:
+            return v
+    return name
+
+
+def counter_rows(d):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    rows = []
+    for f in files:
+        with open(f) as fh:
+            rows += list(csv.DictReader(fh))
+    return rows
+
+
+def per_kernel(rows, counter):
+    acc = {}
+    for r in rows:
+        if r.get("Counter_Name") != counter:
+            continue
+        k = short(r.get("Kernel_Name", ""))
+        acc.setdefault(k, []).append(float(r["Counter_Value"]))
+    return acc
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    if stats:
+        shutil.copy(stats[0], dst + "_kernel_stats.csv")
+    fetch = per_kernel(counter_rows(os.path.join(src, "pmc_fetch")), "FETCH_SIZE")
+    write = per_kernel(counter_rows(os.path.join(src, "pmc_write")), "WRITE_SIZE")
+    out = {"method": __doc__.strip().splitlines()[2:5], "kernels": {}}
+    for k in sorted(set(fetch) | set(write)):
+        f = fetch.get(k, [])
+        w = write.get(k, [])
+        fk = sum(f) / len(f) if f else 0.0
+        wk = sum(w) / len(w) if w else 0.0
+        out["kernels"][k] = {"dispatches": max(len(f), len(w)), "fetch_kib_per_launch": fk, "write_kib_per_launch": wk,
+                             "hbm_bytes_per_launch": (2 * fk + wk) * 1024.0}
+    out["source_run"] = os.path.basename(os.path.normpath(src))
+    for path in (dst + "_pmc_traffic.json", os.path.join(os.path.dirname(dst) or ".", "pmc_traffic.json")):
+        with open(path, "w") as fh:
+            json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
