@@ -117,8 +117,14 @@ def main():
     if out is not None:
         assert out.shape[0] == dist.world * B and bool(torch.isfinite(out).all())
 
-    # roofline for the dominant kernel (largest share of measured kernel time)
-    dom_name, dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    # roofline for the dominant kernel (largest share of measured kernel time); sites are "kernel@site"
+    by_kernel = {}
+    for name, v in prof.items():
+        k = name.split("@")[0]
+        agg = by_kernel.setdefault(k, dict(ms=0.0, launches=0, flops=0.0, bytes=0.0))
+        for f in agg:
+            agg[f] += v[f]
+    dom_name, dom = max(by_kernel.items(), key=lambda kv: kv[1]["ms"])
     per_launch_s = dom["ms"] / 1000.0 / dom["launches"]
     if dom["flops"] > 0:
         achieved = dom["flops"] / dom["launches"] / per_launch_s / 1e12
@@ -129,12 +135,13 @@ def main():
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
     roof["kernel"] = dom_name
     roof["avg_launch_us"] = round(per_launch_s * 1e6, 2)
-    roof["share_of_kernel_time"] = round(dom["ms"] / sum(v["ms"] for v in prof.values()), 3)
+    roof["share_of_kernel_time"] = round(dom["ms"] / sum(v["ms"] for v in by_kernel.values()), 3)
     roof["traffic"] = None
     if os.path.exists(args.pmc_json):
         pmc = json.load(open(args.pmc_json))
         if dom_name in pmc.get("kernels", {}):
             roof["traffic"] = pmc["kernels"][dom_name].get("hbm_bytes_per_launch")
+            roof["traffic_source"] = os.path.relpath(args.pmc_json, REPO) + " (" + pmc.get("source_run", "?") + ")"
     total_flops = sum(v["flops"] for v in prof.values()) / args.steps
     kernels = {k: {"ms_per_step": round(v["ms"] / args.steps, 3), "launches_per_step": v["launches"] // args.steps,
                    "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 1) if v["flops"] else None,

@@ -111,6 +111,9 @@ svc_status svc_op_layernorm(const float* x, const float* g, const float* b, int 
 svc_status svc_profile_enable(int enable);
 svc_status svc_profile_read(int idx, char* name, int name_len, double* total_ms, int64_t* launches, double* flops,
                             double* bytes, int* n_kernels);
+/* GEMM microbenchmark on synthetic operands: average ms per launch of one implicit-GEMM configuration
+   (variant -1 = first-generation kernel, >= 0 = conv_gemm2 tile variants); epi 0 = f16 store, 1 = paired gate */
+svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi, int variant, int iters, double* ms_out);
 /* slaney mel filterbank (librosa.filters.mel, htk=False, norm='slaney') computed natively, host output */
 svc_status svc_mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double fmax, float* out_host);
 

@@ -39,6 +39,7 @@ PROTOTYPES = {
     "svc_profile_enable": (c_int, [c_int]),
     "svc_profile_read": (c_int, [c_int, ctypes.c_char_p, c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_int64),
                                  ctypes.POINTER(c_double), ctypes.POINTER(c_double), ctypes.POINTER(c_int)]),
+    "svc_gemm_bench": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_double)]),
     "svc_mel_filterbank": (c_int, [c_int, c_int, c_int, c_double, c_double, c_void_p]),
 }
 

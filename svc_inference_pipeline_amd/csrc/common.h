@@ -112,5 +112,6 @@ int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
 // aggregated by kernel name together with their algorithmic FLOPs / bytes.
 int prof_begin(const char* name, double flops, double bytes, hipStream_t s);  // returns token or -1
 void prof_end(int token, hipStream_t s);
+void prof_site(const char* site);  // label attached to the next launches ("kernel@site")
 
 }  // namespace svc

@@ -1,5 +1,5 @@
-// Bandwidth-bound kernels of the SVC path on gfx950: LayerNorm (fp32 statistics), the fused
-// anti-aliased SnakeBeta activation (BigVGAN Activation1d), content mapping, conditioner bucketize,
+// Bandwidth-bound kernels of the SVC path on gfx950: LayerNorm (fp32 statistics), content mapping,
+// conditioner bucketize,
 // sampler updates (DDPM / PLMS), mel de-normalisation, conv_post+tanh+fade.
 // All tensors are time-major [rows = b*T + t][channels].
 #include "common.h"
@@ -60,90 +60,7 @@ int layernorm_f32(const float* x, const float* g, const float* b, float* y, int 
   return SVC_OK;
 }
 
-// ============================================================================ Activation1d (SnakeBeta)
-// modules/bigvgan.py:234-307 + SnakeBeta :146-159, for one channel sequence x[0..L-1]:
-//   u[2q]   = 2 * sum_{a=0..5} x[clamp(q-3+a)] * f[11-2a]      (UpSample1d, replicate pad 5, crop 15)
-//   u[2q+1] = 2 * sum_{a=0..5} x[clamp(q-2+a)] * f[10-2a]
-//   s[j]    = u + 1/(exp(beta)+1e-9) * sin(u*exp(alpha))^2
-//   y[t]    = sum_{k=0..11} f[k] * s[clamp(2t+k-5, 0, 2L-1)]   (LowPassFilter1d, replicate pad (5,6), stride 2)
-// One workgroup = 64 outputs x 32 channels of one utterance; x rows [t0-6, t0+70) and the 140
-// needed s values are staged in LDS, so each input element is read once from HBM.
-constexpr int ACT_TT = 64, ACT_CC = 32;
-
-__global__ __launch_bounds__(256) void activation1d_kernel(const float* __restrict__ x, f16* __restrict__ y, int L,
-                                                           int C, int ldy, const float* __restrict__ alpha_log,
-                                                           const float* __restrict__ beta_log,
-                                                           const float* __restrict__ filt) {
-  __shared__ float xs[ACT_TT + 12][ACT_CC];
-  __shared__ float ss[2 * ACT_TT + 12][ACT_CC + 1];
-  const int cl = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 8 rows of 32 channels
-  const int t0 = blockIdx.x * ACT_TT;
-  const int c0 = blockIdx.y * ACT_CC;
-  const int b = blockIdx.z;
-  const int c = c0 + cl;
-  const bool cok = c < C;
-  const float* xb = x + (int64_t)b * L * C;
-  float f[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) f[k] = filt[k];
-  float a_s = 1.f, inv_b = 0.f;
-  if (cok) {
-    a_s = expf(alpha_log[c]);
-    inv_b = 1.0f / (expf(beta_log[c]) + 0.000000001f);
-  }
-  for (int r = ty; r < ACT_TT + 12; r += 8) {
-    int t = t0 - 6 + r;
-    t = t < 0 ? 0 : (t >= L ? L - 1 : t);
-    xs[r][cl] = cok ? xb[(int64_t)t * C + c] : 0.f;
-  }
-  __syncthreads();
-  // s index j in [2*t0-5, 2*t0+2*TT+6] -> jj = j - (2*t0 - 5)
-  for (int jj = ty; jj < 2 * ACT_TT + 12; jj += 8) {
-    int j = 2 * t0 - 5 + jj;
-    j = j < 0 ? 0 : (j >= 2 * L ? 2 * L - 1 : j);
-    const int qq = j >> 1;
-    float u = 0.f;
-    if ((j & 1) == 0) {
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        int xt = qq - 3 + a;
-        xt = xt < 0 ? 0 : (xt >= L ? L - 1 : xt);
-        u += xs[xt - (t0 - 6)][cl] * f[11 - 2 * a];
-      }
-    } else {
-#pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        int xt = qq - 2 + a;
-        xt = xt < 0 ? 0 : (xt >= L ? L - 1 : xt);
-        u += xs[xt - (t0 - 6)][cl] * f[10 - 2 * a];
-      }
-    }
-    u = 2.0f * u;
-    const float sn = sinf(u * a_s);
-    ss[jj][cl] = u + inv_b * (sn * sn);
-  }
-  __syncthreads();
-  for (int r = ty; r < ACT_TT; r += 8) {
-    const int t = t0 + r;
-    if (t >= L || !cok) continue;
-    float acc = 0.f;
-#pragma unroll
-    for (int k = 0; k < 12; ++k) acc += f[k] * ss[2 * r + k][cl];
-    y[((int64_t)b * L + t) * ldy + c] = f16_sat(acc);
-  }
-}
-
-int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const float* alpha_log, const float* beta_log,
-                 const float* filt, hipStream_t s) {
-  SVC_REQUIRE(L >= 1 && C >= 1, "activation1d: bad shape");
-  dim3 grid(cdiv(L, ACT_TT), cdiv(C, ACT_CC), B);
-  // algorithmic bytes: read x once (f32), write y once (f16)
-  const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * (4 + 2), s);
-  hipLaunchKernelGGL(activation1d_kernel, grid, dim3(256), 0, s, x, y, L, C, ldy, alpha_log, beta_log, filt);
-  prof_end(tok, s);
-  SVC_LAUNCH_CHECK();
-  return SVC_OK;
-}
+// Activation1d (anti-aliased SnakeBeta) lives in activation.hip.
 
 // ============================================================================ conversions
 __global__ void f32_to_f16_kernel(const float* __restrict__ x, int ldx, f16* __restrict__ y, int ldy, int rows, int C,

@@ -3,6 +3,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -47,9 +48,13 @@ static hipEvent_t ev_get() {
   return e;
 }
 
+static thread_local const char* g_site = "";
+void prof_site(const char* site) { g_site = site ? site : ""; }
+
 int prof_begin(const char* name, double flops, double bytes, hipStream_t s) {
   if (!g_prof) return -1;
-  ProfRec r{name, ev_get(), ev_get(), flops, bytes};
+  std::string full = std::string(name) + (g_site[0] ? std::string("@") + g_site : std::string());
+  ProfRec r{full, ev_get(), ev_get(), flops, bytes};
   if (!r.a || !r.b) return -1;
   (void)hipEventRecord(r.a, s);
   g_prof_recs.push_back(r);
@@ -99,6 +104,7 @@ int mel_log(const float* spec, int nbins, const float* fb, int n_mels, float* ou
 int energy_from_mel(const float* mel, int n_mels, float* en, int rows, hipStream_t s);
 int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s);
 int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
+int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int pack_qkv(const float* q, const float* k, const float* v, f16* qkv, int64_t rows, int D, float scale, hipStream_t s);
 int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double time_step, double floor_hz,
@@ -303,7 +309,7 @@ int pack_gemm(svc_ctx* c, PackedGemm& g, int N, int Cin, int Cp, int taps, WG wg
   g.taps = taps;
   g.K = taps * Cp;
   g.Kpad = (int)round_up(g.K, 64);
-  g.Npad = (int)round_up(N, 128);
+  g.Npad = (int)round_up(N, 256);
   std::vector<f16> w((size_t)g.Npad * g.Kpad, (f16)0.0f);
   std::vector<float> b((size_t)g.Npad, 0.0f);
   for (int n = 0; n < N; ++n) {
@@ -380,10 +386,10 @@ int pack_conv_transpose(svc_ctx* c, std::vector<PackedGemm>& phases, const float
   return SVC_OK;
 }
 
-// paired packing order: packed n -> original channel ((n & 16) ? C : 0) + (n >> 5) * 16 + (n & 15)
+// paired packing order (conv_gemm2 epilogue): packed n -> original channel ((n & 32) ? C : 0) + (n >> 6) * 32 + (n & 31)
 std::vector<int> pair_perm(int C) {
   std::vector<int> p(2 * C);
-  for (int n = 0; n < 2 * C; ++n) p[n] = ((n & 16) ? C : 0) + (n >> 5) * 16 + (n & 15);
+  for (int n = 0; n < 2 * C; ++n) p[n] = ((n & 32) ? C : 0) + (n >> 6) * 32 + (n & 31);
   return p;
 }
 
@@ -392,8 +398,19 @@ double cfgv(svc_ctx* c, const char* k, double d) {
   return it == c->cfg.end() ? d : it->second;
 }
 
+// 4 KiB of zeros: the LDS-DMA source of padded / out-of-range conv rows (conv_gemm2)
+const f16* zero_page() {
+  static f16* z = nullptr;
+  if (!z) {
+    if (hipMalloc(&z, 4096) != hipSuccess) return nullptr;
+    if (hipMemset(z, 0, 4096) != hipSuccess) return nullptr;
+  }
+  return z;
+}
+
 int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
-             hipStream_t s) {
+             hipStream_t s, const char* site = "") {
+  prof_site(site);
   ConvGemmArgs a{};
   a.X = X;
   a.ldx = ldx;
@@ -415,6 +432,15 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
     e.ophase = 0;
   }
   if (!e.bias) e.bias = g.bias;
+  const bool pair = (e.kind == EPI_GATE || e.kind == EPI_RESSKIP);
+  if (pair || g.N > 64) {
+    static int variant = -1;
+    if (variant < 0) {
+      const char* v = getenv("SVC_GEMM_VARIANT");
+      variant = v ? atoi(v) : 0;
+    }
+    if (pair || variant >= 0) return conv_gemm2(a, e, zero_page(), variant, s);
+  }
   return conv_gemm(a, e, s);
 }
 
@@ -997,7 +1023,7 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   e.act = ACT_GELU;
   e.out16 = h1;
   e.ld16 = D;
-  if ((st = run_gemm(c->wconv1, lm16, c->wmels, c->wmels, B, F, F, e, s))) return st;
+  if ((st = run_gemm(c->wconv1, lm16, c->wmels, c->wmels, B, F, F, e, s, "whisper.conv1"))) return st;
   WS_GET(float, x, rows2 * D);
   e = epi();
   e.act = ACT_GELU;
@@ -1005,7 +1031,7 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   e.ld_add_t = D;
   e.out32 = x;
   e.ld32 = D;
-  if ((st = run_gemm(c->wconv2, h1, D, D, B, F, L, e, s))) return st;
+  if ((st = run_gemm(c->wconv2, h1, D, D, B, F, L, e, s, "whisper.conv2"))) return st;
   WS_GET(f16, n16, rows2 * D);
   WS_GET(f16, qkv, rows2 * 3 * D);
   WS_GET(f16, o16, rows2 * D);
@@ -1019,26 +1045,26 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
     e.ld16 = 3 * D;
     e.scale_cols = 2 * D;
     e.col_scale = qk_scale;
-    if ((st = run_gemm(b.qkv, n16, D, D, B, L, L, e, s))) return st;
+    if ((st = run_gemm(b.qkv, n16, D, D, B, L, L, e, s, "whisper.qkv"))) return st;
     if ((st = attention(qkv, o16, B, L, D, s))) return st;
     e = epi();
     e.add_row = x;
     e.ld_add_row = D;
     e.out32 = x;
     e.ld32 = D;
-    if ((st = run_gemm(b.out, o16, D, D, B, L, L, e, s))) return st;
+    if ((st = run_gemm(b.out, o16, D, D, B, L, L, e, s, "whisper.out"))) return st;
     if ((st = layernorm_f16(x, b.ln2_g, b.ln2_b, n16, (int)rows2, D, D, s))) return st;
     e = epi();
     e.act = ACT_GELU;
     e.out16 = h16;
     e.ld16 = 4 * D;
-    if ((st = run_gemm(b.fc1, n16, D, D, B, L, L, e, s))) return st;
+    if ((st = run_gemm(b.fc1, n16, D, D, B, L, L, e, s, "whisper.fc1"))) return st;
     e = epi();
     e.add_row = x;
     e.ld_add_row = D;
     e.out32 = x;
     e.ld32 = D;
-    if ((st = run_gemm(b.fc2, h16, 4 * D, 4 * D, B, L, L, e, s))) return st;
+    if ((st = run_gemm(b.fc2, h16, 4 * D, 4 * D, B, L, L, e, s, "whisper.fc2"))) return st;
   }
   return layernorm_f32(x, c->wlnp_g, c->wlnp_b, feats, (int)rows2, D, D, s);
 }
@@ -1070,7 +1096,7 @@ static int condition_impl(svc_ctx* c, const void* content16, const double* f0, c
   e.ld32 = c->C;
   e.out16 = cond16;
   e.ld16 = c->C;
-  return run_gemm(c->content_lin, (const f16*)content16, c->content_dim, c->content_dim, B, T, T, e, s);
+  return run_gemm(c->content_lin, (const f16*)content16, c->content_dim, c->content_dim, B, T, T, e, s, "cond.content");
 }
 
 svc_status svc_condition(svc_ctx* c, const void* content16, const double* f0, const float* energy,
@@ -1106,7 +1132,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.out16 = bb.y16;
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
-  if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s))) return st;
+  if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
   for (int i = 0; i < NL; ++i) {
     EpiArgs g = epi();
     g.kind = EPI_GATE;
@@ -1114,7 +1140,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     g.ld_cp = NL * 2 * C;
     g.y16 = bb.g16;
     g.ldy16 = C;
-    if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s))) return st;
+    if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s, "diffsvc.dilated"))) return st;
     EpiArgs r = epi();
     r.kind = EPI_RESSKIP;
     r.x32 = bb.h32;
@@ -1126,18 +1152,18 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     r.dnext = (i + 1 < NL) ? dp + (size_t)(i + 1) * C : nullptr;
     r.y16 = (i + 1 < NL) ? bb.y16 : bb.s16;
     r.ldy16 = C;
-    if ((st = run_gemm(c->outp[i], bb.g16, C, C, B, T, T, r, s))) return st;
+    if ((st = run_gemm(c->outp[i], bb.g16, C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
   }
   e = epi();
   e.act = ACT_RELU;
   e.out16 = bb.u16;
   e.ld16 = C;
-  if ((st = run_gemm(c->skipproj, bb.s16, C, C, B, T, T, e, s))) return st;
+  if ((st = run_gemm(c->skipproj, bb.s16, C, C, B, T, T, e, s, "diffsvc.skipproj"))) return st;
   e = epi();
   e.out32 = eps;
   e.ld32 = c->n_mel;
   (void)rows;
-  return run_gemm(c->outproj, bb.u16, C, C, B, T, T, e, s);
+  return run_gemm(c->outproj, bb.u16, C, C, B, T, T, e, s, "diffsvc.eps_out");
 }
 
 static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
@@ -1166,7 +1192,7 @@ static int project_cond(svc_ctx* c, const float* cond, int B, int T, const Denoi
   EpiArgs e = epi();
   e.out16 = bb.cp16;
   e.ld16 = c->n_layers * 2 * C;
-  return run_gemm(c->cp_all, cond16, C, C, B, T, T, e, s);
+  return run_gemm(c->cp_all, cond16, C, C, B, T, T, e, s, "diffsvc.condproj");
 }
 
 svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B, int T, int t, float* eps,
@@ -1206,6 +1232,7 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
   if ((st = project_cond(c, cond, B, T, bb, s))) return st;
   float* x = x0;  // the sampler state lives in the output buffer
   WS_GET(f16, x16, (size_t)rows * ld16);
+  SVC_HIP_CHECK(hipMemsetAsync(x16, 0, (size_t)rows * ld16 * sizeof(f16), s));  // zero pad channels
   if (x_T) {
     SVC_HIP_CHECK(hipMemcpyAsync(x, x_T, (size_t)rows * nm * 4, hipMemcpyDeviceToDevice, s));
     if ((st = f32_to_f16(x, nm, x16, ld16, rows, nm, ld16, s))) return st;
@@ -1238,6 +1265,7 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
   }
   WS_GET(float, xp, (size_t)rows * nm);
   WS_GET(f16, xp16, (size_t)rows * ld16);
+  SVC_HIP_CHECK(hipMemsetAsync(xp16, 0, (size_t)rows * ld16 * sizeof(f16), s));
   int nh = 0, head = 0;  // hist slots: newest at hist[(head - 1) mod 5]
   const std::vector<float>& ac = c->alphas_cumprod_f32;
   for (int i = ((c->steps - 1) / interval) * interval; i >= 0; i -= interval) {
@@ -1336,7 +1364,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
   EpiArgs e = epi();
   e.out16 = pre16;
   e.ld16 = c->v_c0;
-  if ((st = run_gemm(c->vpre, mel16, ldm, nm, B, T, T, e, s))) return st;
+  if ((st = run_gemm(c->vpre, mel16, ldm, nm, B, T, T, e, s, "bigvgan.conv_pre"))) return st;
   WS_GET(float, X, big);
   WS_GET(float, Xj, big);
   WS_GET(float, tmp, big);
@@ -1359,7 +1387,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
       u.ophase = r;
       u.out32 = X;
       u.ld32 = ch;
-      if ((st = run_gemm(S.phases[r], in16, S.cin, S.cin, B, Lin, Lin, u, s))) return st;
+      if ((st = run_gemm(S.phases[r], in16, S.cin, S.cin, B, Lin, Lin, u, s, "bigvgan.ups"))) return st;
     }
     const int nk = (int)S.c1.size();
     for (int j = 0; j < nk; ++j) {
@@ -1372,7 +1400,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
         EpiArgs e1 = epi();
         e1.out32 = tmp;
         e1.ld32 = ch;
-        if ((st = run_gemm(S.c1[j][l], a16, ch, ch, B, L, L, e1, s))) return st;
+        if ((st = run_gemm(S.c1[j][l], a16, ch, ch, B, L, L, e1, s, "bigvgan.amp_c1"))) return st;
         if ((st = activation1d(tmp, a16, B, L, ch, ch, S.acts[j][2 * l + 1].alpha, S.acts[j][2 * l + 1].beta,
                                S.acts[j][2 * l + 1].filt, s)))
           return st;
@@ -1402,7 +1430,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
             e2.ld32 = ch;
           }
         }
-        if ((st = run_gemm(S.c2[j][l], a16, ch, ch, B, L, L, e2, s))) return st;
+        if ((st = run_gemm(S.c2[j][l], a16, ch, ch, B, L, L, e2, s, "bigvgan.amp_c2"))) return st;
       }
     }
     in16 = next16;  // stage output (f16) feeds the next ConvTranspose; it is rewritten only after that ran
@@ -1545,3 +1573,59 @@ svc_status svc_op_layernorm(const float* x, const float* g, const float* b, int 
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------- GEMM microbenchmark
+// Times `iters` launches of one implicit-GEMM configuration on synthetic operands (tools/gemm_bench.py):
+// M rows, N packed columns, K = taps*Cp, 1-tap or 3-tap conv, epilogue 0 = f16 store, 1 = paired gate.
+__global__ void fill_f16_kernel(f16* p, int64_t n, uint32_t seed) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+  h ^= h >> 13;
+  h *= 0x5bd1e995u;
+  h ^= h >> 15;
+  p[i] = (f16)(((h & 0xFFFF) / 65536.0f - 0.5f) * 0.5f);
+}
+
+extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_kind, int variant, int iters, double* ms_out) {
+  SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters >= 1, "gemm_bench: bad args");
+  const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)round_up(N, 256);
+  f16 *X, *W, *Y, *cp;
+  float* bias;
+  SVC_HIP_CHECK(hipMalloc(&X, (size_t)M * Cin * 2));
+  SVC_HIP_CHECK(hipMalloc(&W, (size_t)Npad * Kpad * 2));
+  SVC_HIP_CHECK(hipMalloc(&Y, (size_t)M * N * 2));
+  SVC_HIP_CHECK(hipMalloc(&cp, (size_t)M * N * 2));
+  SVC_HIP_CHECK(hipMalloc(&bias, (size_t)Npad * 4));
+  SVC_HIP_CHECK(hipMemset(bias, 0, (size_t)Npad * 4));
+  hipLaunchKernelGGL(fill_f16_kernel, dim3(cdiv((int64_t)M * Cin, 256)), dim3(256), 0, 0, X, (int64_t)M * Cin, 1u);
+  hipLaunchKernelGGL(fill_f16_kernel, dim3(cdiv((int64_t)Npad * Kpad, 256)), dim3(256), 0, 0, W, (int64_t)Npad * Kpad, 2u);
+  hipLaunchKernelGGL(fill_f16_kernel, dim3(cdiv((int64_t)M * N, 256)), dim3(256), 0, 0, cp, (int64_t)M * N, 3u);
+  ConvGemmArgs a{};
+  a.X = X; a.ldx = Cin; a.T_in = M; a.Cp = Cin; a.Cvalid = Cin; a.W = W; a.K = K; a.Kpad = Kpad;
+  a.tap_mul = 1; a.tap_add = -(taps / 2); a.istride = 1; a.B = 1; a.T_out = M; a.N = N;
+  EpiArgs e = epi();
+  e.bias = bias; e.T_ostore = M; e.ostride = 1;
+  if (epi_kind == 1) {
+    e.kind = EPI_GATE; e.cp = cp; e.ld_cp = N; e.y16 = Y; e.ldy16 = N / 2;
+  } else {
+    e.out16 = Y; e.ld16 = N;
+  }
+  hipEvent_t e0, e1;
+  SVC_HIP_CHECK(hipEventCreate(&e0));
+  SVC_HIP_CHECK(hipEventCreate(&e1));
+  int st = SVC_OK;
+  for (int w = 0; w < 2 && !st; ++w) st = variant < 0 ? conv_gemm(a, e, 0) : conv_gemm2(a, e, zero_page(), variant, 0);
+  SVC_HIP_CHECK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters && !st; ++i)
+    st = variant < 0 ? conv_gemm(a, e, 0) : conv_gemm2(a, e, zero_page(), variant, 0);
+  SVC_HIP_CHECK(hipEventRecord(e1, 0));
+  SVC_HIP_CHECK(hipEventSynchronize(e1));
+  float ms = 0;
+  SVC_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  *ms_out = ms / iters;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  for (void* p : {(void*)X, (void*)W, (void*)Y, (void*)cp, (void*)bias}) (void)hipFree(p);
+  return st;
+}

@@ -1,0 +1,35 @@
+"""GEMM kernel microbenchmark (GPU): TFLOP/s of the implicit-GEMM variants on the hot-path shapes.
+Usage: python tools/gemm_bench.py [variant ...]"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from svc_inference_pipeline_amd import _lib  # noqa: E402
+
+SHAPES = [  # name, M, N, Cin, taps, epi
+    ("diffsvc.dilated(gate)", 29984, 768, 384, 3, 1),
+    ("diffsvc.dilated(store)", 29984, 768, 384, 3, 0),
+    ("whisper.fc1", 48000, 4096, 1024, 1, 0),
+    ("whisper.fc2", 48000, 1024, 4096, 1, 0),
+    ("bigvgan.s1 k11", 32 * 14992, 384, 384, 11, 0),
+    ("square 8192", 8192, 8192, 8192, 1, 0),
+]
+
+
+def main():
+    variants = [int(v) for v in sys.argv[1:]] or [-1, 0, 1]
+    import torch
+    torch.cuda.init()
+    for name, M, N, Cin, taps, epi in SHAPES:
+        row = []
+        for v in variants:
+            ms = ctypes.c_double()
+            _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, 10, ctypes.byref(ms))
+            tf = 2.0 * M * N * Cin * taps / (ms.value * 1e-3) / 1e12
+            row.append(f"v{v}: {ms.value * 1000:8.1f} us {tf:7.1f} TF")
+        print(f"{name:24s}", " | ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
