@@ -24,7 +24,12 @@ struct G2 {
   static constexpr int A_INSTR = BM / 8;  // 1 KiB wave instructions per A tile
   static constexpr int B_INSTR = BN / 8;
   static constexpr int NW = WM * WN;
-  static constexpr int LDS_BYTES = ST * (BM + BN) * 128;
+  static constexpr int RING_BYTES = ST * (BM + BN) * 128;
+  // epilogue staging of the f32 C tile: one pass if it fits 160 KiB, else two column halves
+  static constexpr int EP = (BM * (BN + 4) * 4 <= 163840) ? 1 : 2;
+  static constexpr int C_BYTES = BM * (BN / EP + 4) * 4;
+  static constexpr int LDS_BYTES = RING_BYTES > C_BYTES ? RING_BYTES : C_BYTES;
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
   // LDS-DMA instructions each wave issues per K-tile (the vmcnt unit of the ring)
   static constexpr int I_PER_TILE = (A_INSTR + NW - 1) / NW + (B_INSTR + NW - 1) / NW;
   static_assert(A_INSTR % NW == 0 && B_INSTR % NW == 0, "uniform DMA count per wave");
@@ -159,78 +164,138 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_gemm2_kernel(ConvGemmArg
   }
 
   // ---------------------------------------------------------------- epilogue
-  // acc[i][j][r] = C[m0 + wm*TM + i*32 + (r&3) + 8(r>>2) + 4*lh][n0 + wn*TN + j*32 + lr]
-  const int mbase = m0 + wm * CF::TM + 4 * lh;
-  const int nbase = n0 + wn * CF::TN + lr;
+  // Stage the f32 tile through LDS (the ring is free once every wave left the K loop), then apply the
+  // epilogue on 4-column chunks with 16-byte vector loads/stores (coalesced rows).
+  // acc[i][j][r] = C[wm*TM + i*32 + (r&3) + 8(r>>2) + 4*lh][wn*TN + j*32 + lr]
+  __syncthreads();
+  // the staged C tile may exceed LDS: process it in EP column passes (each wave belongs to one pass)
+  constexpr int EP = CF::EP;
+  constexpr int BNP = BN / EP;
+  constexpr int LDC = BNP + 4;
+  static_assert(WN % EP == 0 && BM * LDC * 4 <= CF::LDS_BYTES, "C tile pass must fit the LDS ring");
+  float* Cs = reinterpret_cast<float*>(smem2);
+#pragma unroll
+  for (int pass = 0; pass < EP; ++pass) {
+  if (wn / (WN / EP) == pass) {
+#pragma unroll
+    for (int i = 0; i < CF::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          Cs[(wm * CF::TM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh) * LDC + wn * CF::TN - pass * BNP + j * 32 + lr] =
+              acc[i][j][r];
+  }
+  __syncthreads();
   if constexpr (!PAIR) {
-#pragma unroll
-    for (int i = 0; i < CF::FM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mbase + i * 32 + (r & 3) + 8 * (r >> 2);
-        if (m >= M) continue;
-        const int b = m / a.T_out, t = m - b * a.T_out;
-        const int64_t orow = (int64_t)b * e.T_ostore + (int64_t)t * e.ostride + e.ophase;
-#pragma unroll
-        for (int j = 0; j < CF::FN; ++j) {
-          const int n = nbase + j * 32;
-          if (n >= a.N) continue;
-          float v = acc[i][j][r];
-          if (e.kind == EPI_COND) {
-            v = v + e.bias[n];
-            v = v + e.emb_m[(int64_t)e.idx_m[m] * e.ld_emb + n];
-            v = v + e.emb_l[(int64_t)e.idx_l[m] * e.ld_emb + n];
-            v = v + e.emb_s[(int64_t)e.singer[b] * e.ld_emb + n];
-            e.out32[orow * e.ld32 + n] = v;
-            if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(v);
-            continue;
-          }
-          if (e.bias) v += e.bias[n];
-          if (e.act == ACT_GELU) v = gelu_erf(v);
-          else if (e.act == ACT_RELU) v = fmaxf(v, 0.0f);
-          if (n < e.scale_cols) v *= e.col_scale;
-          if (e.add_t) v += e.add_t[(int64_t)t * e.ld_add_t + n];
-          if (e.add_row) v += e.add_row[orow * e.ld_add_row + n];
-          if (e.acc32) {
-            v = e.acc32[orow * e.ld_acc + n] + v;
-            if (e.acc_div != 1.0f) v = v / e.acc_div;
-          }
-          if (e.out32) e.out32[orow * e.ld32 + n] = v;
-          if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(e.add16 ? v + e.add16[n] : v);
+    constexpr int CPR = BNP / 4;
+    for (int idx = tid; idx < BM * CPR; idx += CF::NT) {
+      const int row = idx / CPR, cc = idx - row * CPR;
+      const int m = m0 + row, n = n0 + pass * BNP + 4 * cc;
+      if (m >= M || n >= a.N) continue;
+      const int b = m / a.T_out, t = m - b * a.T_out;
+      const int64_t orow = (int64_t)b * e.T_ostore + (int64_t)t * e.ostride + e.ophase;
+      float4 v = *reinterpret_cast<const float4*>(Cs + row * LDC + 4 * cc);  // pass-local columns
+      const float4 bi = *reinterpret_cast<const float4*>(e.bias + n);
+      v.x += bi.x; v.y += bi.y; v.z += bi.z; v.w += bi.w;
+      if (e.kind == EPI_COND) {
+        const float4 em = *reinterpret_cast<const float4*>(e.emb_m + (int64_t)e.idx_m[m] * e.ld_emb + n);
+        const float4 el = *reinterpret_cast<const float4*>(e.emb_l + (int64_t)e.idx_l[m] * e.ld_emb + n);
+        const float4 es = *reinterpret_cast<const float4*>(e.emb_s + (int64_t)e.singer[b] * e.ld_emb + n);
+        v.x = ((v.x + em.x) + el.x) + es.x;
+        v.y = ((v.y + em.y) + el.y) + es.y;
+        v.z = ((v.z + em.z) + el.z) + es.z;
+        v.w = ((v.w + em.w) + el.w) + es.w;
+      } else {
+        if (e.act == ACT_GELU) {
+          v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+        } else if (e.act == ACT_RELU) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
+        if (n < e.scale_cols) {
+          v.x *= e.col_scale; v.y *= e.col_scale; v.z *= e.col_scale; v.w *= e.col_scale;
+        }
+        if (e.add_t) {
+          const float4 at = *reinterpret_cast<const float4*>(e.add_t + (int64_t)t * e.ld_add_t + n);
+          v.x += at.x; v.y += at.y; v.z += at.z; v.w += at.w;
+        }
+        if (e.add_row) {
+          const float4 ar = *reinterpret_cast<const float4*>(e.add_row + orow * e.ld_add_row + n);
+          v.x += ar.x; v.y += ar.y; v.z += ar.z; v.w += ar.w;
+        }
+        if (e.acc32) {
+          const float4 ac = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
+          v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
+          if (e.acc_div != 1.0f) {
+            v.x = v.x / e.acc_div; v.y = v.y / e.acc_div; v.z = v.z / e.acc_div; v.w = v.w / e.acc_div;
+          }
+        }
+      }
+      if (e.out32) *reinterpret_cast<float4*>(e.out32 + orow * e.ld32 + n) = v;
+      if (e.out16) {
+        float4 w = v;
+        if (e.add16) {
+          const float4 ad = *reinterpret_cast<const float4*>(e.add16 + n);
+          w.x += ad.x; w.y += ad.y; w.z += ad.z; w.w += ad.w;
+        }
+        union { uint2 u; f16 h[4]; } pk;
+        pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
+        *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
       }
     }
   } else {
-#pragma unroll
-    for (int i = 0; i < CF::FM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mbase + i * 32 + (r & 3) + 8 * (r >> 2);
-        if (m >= M) continue;
-#pragma unroll
-        for (int p = 0; p < CF::FN / 2; ++p) {
-          const int n = nbase + 2 * p * 32;  // packed column of the first-half element
-          if (n >= a.N) continue;
-          const int ch = (n >> 6) * 32 + (n & 31);
-          float v1 = acc[i][2 * p][r] + e.bias[n];
-          float v2 = acc[i][2 * p + 1][r] + e.bias[n + 32];
-          if (e.kind == EPI_GATE) {
-            const f16* cpr = e.cp + (int64_t)m * e.ld_cp;
-            v1 += (float)cpr[n];
-            v2 += (float)cpr[n + 32];
-            e.y16[(int64_t)m * e.ldy16 + ch] = f16_sat(sigmoidf_(v1) * tanhf(v2));
-          } else {  // EPI_RESSKIP
-            const int64_t o = (int64_t)m * e.ldx32 + ch;
-            const float xn = (e.x32[o] + v1) / 1.41421356237309515f;
-            e.x32[o] = xn;
-            const float sk = e.skip_first ? v2 : (v2 + e.skip32[o]);
-            e.skip32[o] = sk;
-            e.y16[(int64_t)m * e.ldy16 + ch] = e.last_layer ? f16_sat(sk / e.skip_scale) : f16_sat(xn + e.dnext[ch]);
-          }
+    // pairs: chunk = 4 first-half columns n..n+3 and their partners n+32..n+35 -> channels ch..ch+3
+    constexpr int CPR = BNP / 8;
+    for (int idx = tid; idx < BM * CPR; idx += CF::NT) {
+      const int row = idx / CPR, cc = idx - row * CPR;
+      const int m = m0 + row;
+      const int nl = (cc >> 3) * 64 + 4 * (cc & 7);  // pass-local packed column of the first-half element
+      const int n = n0 + pass * BNP + nl;
+      if (m >= M || n >= a.N) continue;
+      const int ch = (n >> 6) * 32 + (n & 31);
+      float4 v1 = *reinterpret_cast<const float4*>(Cs + row * LDC + nl);
+      float4 v2 = *reinterpret_cast<const float4*>(Cs + row * LDC + nl + 32);
+      const float4 b1 = *reinterpret_cast<const float4*>(e.bias + n);
+      const float4 b2 = *reinterpret_cast<const float4*>(e.bias + n + 32);
+      v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
+      v2.x += b2.x; v2.y += b2.y; v2.z += b2.z; v2.w += b2.w;
+      union { uint2 u; f16 h[4]; } pk;
+      if (e.kind == EPI_GATE) {
+        union { uint2 u; f16 h[4]; } c1, c2;
+        c1.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n);
+        c2.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n + 32);
+        pk.h[0] = f16_sat(sigmoidf_(v1.x + (float)c1.h[0]) * tanhf(v2.x + (float)c2.h[0]));
+        pk.h[1] = f16_sat(sigmoidf_(v1.y + (float)c1.h[1]) * tanhf(v2.y + (float)c2.h[1]));
+        pk.h[2] = f16_sat(sigmoidf_(v1.z + (float)c1.h[2]) * tanhf(v2.z + (float)c2.h[2]));
+        pk.h[3] = f16_sat(sigmoidf_(v1.w + (float)c1.h[3]) * tanhf(v2.w + (float)c2.h[3]));
+      } else {  // EPI_RESSKIP
+        const int64_t o = (int64_t)m * e.ldx32 + ch;
+        float4 x = *reinterpret_cast<const float4*>(e.x32 + o);
+        x.x = (x.x + v1.x) / 1.41421356237309515f;
+        x.y = (x.y + v1.y) / 1.41421356237309515f;
+        x.z = (x.z + v1.z) / 1.41421356237309515f;
+        x.w = (x.w + v1.w) / 1.41421356237309515f;
+        *reinterpret_cast<float4*>(e.x32 + o) = x;
+        float4 sk = v2;
+        if (!e.skip_first) {
+          const float4 so = *reinterpret_cast<const float4*>(e.skip32 + o);
+          sk.x = v2.x + so.x; sk.y = v2.y + so.y; sk.z = v2.z + so.z; sk.w = v2.w + so.w;
+        }
+        *reinterpret_cast<float4*>(e.skip32 + o) = sk;
+        if (e.last_layer) {
+          pk.h[0] = f16_sat(sk.x / e.skip_scale); pk.h[1] = f16_sat(sk.y / e.skip_scale);
+          pk.h[2] = f16_sat(sk.z / e.skip_scale); pk.h[3] = f16_sat(sk.w / e.skip_scale);
+        } else {
+          const float4 dn = *reinterpret_cast<const float4*>(e.dnext + ch);
+          pk.h[0] = f16_sat(x.x + dn.x); pk.h[1] = f16_sat(x.y + dn.y);
+          pk.h[2] = f16_sat(x.z + dn.z); pk.h[3] = f16_sat(x.w + dn.w);
         }
       }
+      *reinterpret_cast<uint2*>(e.y16 + (int64_t)m * e.ldy16 + ch) = pk.u;
     }
   }
+  __syncthreads();
+  }  // pass
 }
 
 template <int BM, int BN, int WM, int WN, int ST, bool PAIR>
@@ -258,15 +323,22 @@ static int launch2(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
 }
 
 int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s) {
-  SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0, "conv_gemm2: layout");
+  SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0 && a.N % 4 == 0, "conv_gemm2: layout");
+  SVC_REQUIRE(e.ld32 % 4 == 0 && e.ld16 % 4 == 0 && e.ld_add_row % 4 == 0 && e.ld_acc % 4 == 0 && e.ld_add_t % 4 == 0 &&
+                  e.ld_cp % 4 == 0 && e.ldx32 % 4 == 0 && e.ldy16 % 4 == 0 && e.ld_emb % 4 == 0,
+              "conv_gemm2: epilogue leading dimensions must be multiples of 4 (vector epilogue)");
   SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm2: 16-B alignment");
   const bool pair = (e.kind == EPI_GATE || e.kind == EPI_RESSKIP);
   if (pair) {
     SVC_REQUIRE(a.N % 64 == 0, "conv_gemm2: paired epilogue needs N %% 64 == 0");
     if (variant == 1) return launch2<256, 128, 4, 2, 3, true>(a, e, zpage, s, "conv_gemm2<256,128,pair>");
+    if (variant == 2) return launch2<256, 256, 2, 4, 2, true>(a, e, zpage, s, "conv_gemm2<256,256,pair>");
+    if (variant == 3) return launch2<192, 256, 2, 4, 2, true>(a, e, zpage, s, "conv_gemm2<192,256,pair>");
     return launch2<128, 128, 2, 2, 4, true>(a, e, zpage, s, "conv_gemm2<128,128,pair>");
   }
   if (variant == 1) return launch2<256, 128, 4, 2, 3, false>(a, e, zpage, s, "conv_gemm2<256,128>");
+  if (variant == 2) return launch2<256, 256, 2, 4, 2, false>(a, e, zpage, s, "conv_gemm2<256,256>");
+  if (variant == 3) return launch2<192, 256, 2, 4, 2, false>(a, e, zpage, s, "conv_gemm2<192,256>");
   return launch2<128, 128, 2, 2, 4, false>(a, e, zpage, s, "conv_gemm2<128,128>");
 }
 

@@ -9,12 +9,26 @@
 
 Inputs are device tensors of B equal-length utterances (24 kHz f32 and the 16 kHz int16-quantised
 copy Whisper consumes); every stage runs in libsvc_hip.so on the current stream.
+
+Long inputs (SURVEY.md §5 "Long-context", BASELINE config 4). The reference pads/trims Whisper's input
+to one 30 s window and caps the mapped content at 2812 frames (utils/whisper.py:52-56), so for clips
+longer than ~29.99 s its `torch.cat` in modules/encoder.py:197 raises. Here, when T > 2812, Whisper runs
+on consecutive windows of 478 720 samples (29.92 s = 1496 encoder frames = exactly 2805 mel frames, so
+the 15:8 map stays integral and every window starts on a mel frame). Each window is encoded in its own
+zero-padded 30 s context and mapped with the reference's own 15:8 rule. Parity for such clips is per
+window (tests/test_gpu_long.py). Mel, F0, the sampler and BigVGAN run over the whole length in one pass:
+a 180 s song needs ~0.4 GB per vocoder stage buffer, far below 288 GB of HBM, so the vocoder needs no
+overlap-add seams.
 """
 from dataclasses import dataclass
 
 import torch
 
 from .runtime import SVCEngine
+
+WHISPER_WINDOW = 478720       # 16 kHz samples per long-input window (29.92 s)
+WINDOW_MEL_FRAMES = 2805      # = 1496 encoder frames * 15 / 8
+MAX_MAPPED = 2812             # utils/whisper.py:56 (1500 * 15 // 8)
 
 
 @dataclass
@@ -29,6 +43,25 @@ class SVCPipeline:
     def __init__(self, engine: SVCEngine):
         self.engine = engine
 
+    def content(self, wav16, T):
+        """Whisper content features mapped to T mel frames -> f16 [B, T, D]."""
+        e = self.engine
+        B = wav16.shape[0]
+        if T <= MAX_MAPPED:
+            return e.map_content(e.whisper_encode(wav16), T)
+        n_win = -(-T // WINDOW_MEL_FRAMES)
+        need = n_win * WHISPER_WINDOW
+        w = wav16
+        if w.shape[1] < need:
+            w = torch.nn.functional.pad(w, (0, need - w.shape[1]))
+        wins = w[:, :need].reshape(B * n_win, WHISPER_WINDOW).contiguous()
+        feats = e.whisper_encode(wins)                      # [B*n_win, 1500, D]
+        D = feats.shape[-1]
+        out = torch.empty(B, n_win * WINDOW_MEL_FRAMES, D, device=wav16.device, dtype=torch.float16)
+        full = e.map_content(feats, WINDOW_MEL_FRAMES)     # every window mapped to 2805 frames
+        out.copy_(full.view(B, n_win * WINDOW_MEL_FRAMES, D))
+        return out[:, :T].contiguous()
+
     def convert(self, wav24, wav16, singer, fast_inference=True, speedup=10, seed=0, utt_ids=None, x_T=None,
                 noise=None, f0=None):
         e = self.engine
@@ -37,8 +70,7 @@ class SVCPipeline:
         if f0 is None:
             f0 = e.f0(wav24, T)
         e.pitch_shift(f0)
-        feats = e.whisper_encode(wav16)
-        content = e.map_content(feats, T)
+        content = self.content(wav16, T)
         cond = e.condition(content, f0, energy, singer)
         if utt_ids is None and x_T is None:
             utt_ids = torch.arange(wav24.shape[0], device=wav24.device, dtype=torch.int32)

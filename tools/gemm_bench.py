@@ -21,7 +21,10 @@ def main():
     variants = [int(v) for v in sys.argv[1:]] or [-1, 0, 1]
     import torch
     torch.cuda.init()
+    only = os.environ.get("GEMM_BENCH_SHAPES")
     for name, M, N, Cin, taps, epi in SHAPES:
+        if only and not any(o in name for o in only.split(",")):
+            continue
         row = []
         for v in variants:
             ms = ctypes.c_double()
