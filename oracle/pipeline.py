@@ -16,6 +16,30 @@ from . import noise as ON
 from . import praat_ac as PA
 
 
+WHISPER_WINDOW = 478720      # svc_inference_pipeline_amd/pipeline.py: 29.92 s windows for T > 2812
+WINDOW_MEL_FRAMES = 2805
+
+
+def whisper_content(ws, wav16, T):
+    """utils/whisper.py:22-81 for one utterance -> f32 [T, D]. Up to 2812 frames this is exactly the
+    reference's path; longer clips (where the reference raises) are encoded per 29.92 s window, each
+    padded to Whisper's 30 s context and mapped 15:8 onto its 2805 mel frames."""
+    dims = W.whisper_dims_from_state(ws)
+    wav16 = np.asarray(wav16, np.float32)
+
+    def enc(w):
+        lm = OF.whisper_log_mel(torch.from_numpy(OF.pad_or_trim(w))[None])
+        return OM.whisper_encoder(ws, lm, dims["n_audio_head"])[0].numpy()
+
+    if T <= 2812:
+        return OF.map_whisper_features(enc(wav16), T)
+    parts = []
+    for c in range(-(-T // WINDOW_MEL_FRAMES)):
+        tl = min(WINDOW_MEL_FRAMES, T - c * WINDOW_MEL_FRAMES)
+        parts.append(OF.map_whisper_features(enc(wav16[c * WHISPER_WINDOW:(c + 1) * WHISPER_WINDOW]), tl))
+    return np.concatenate(parts, 0)
+
+
 def convert(cfg, ws, ms, vs, wav24, wav16, singer, speedup=10, seed=0, fast_inference=True, x_T=None, f0=None):
     """Returns dict(wav f32[T*hop], mel, f0, x0)."""
     mel = OF.mel_spectrogram(torch.from_numpy(np.asarray(wav24, np.float32))[None], cfg)  # [1,100,T]
@@ -24,10 +48,7 @@ def convert(cfg, ws, ms, vs, wav24, wav16, singer, speedup=10, seed=0, fast_infe
     if f0 is None:
         f0 = PA.f0_features(wav24, T, fs=cfg.fs, hop=cfg.hop_length, floor=cfg.f0_min, ceiling=cfg.f0_max)
     f0 = OF.pitch_shift(f0, C.load_stats(cfg)["target_f0_median"])
-    dims = W.whisper_dims_from_state(ws)
-    lm = OF.whisper_log_mel(torch.from_numpy(OF.pad_or_trim(np.asarray(wav16, np.float32)))[None])
-    feats = OM.whisper_encoder(ws, lm, dims["n_audio_head"])[0].numpy()
-    content = OF.map_whisper_features(feats, T)
+    content = whisper_content(ws, wav16, T)
     cond = OM.conditioner(ms, torch.from_numpy(content)[None], torch.from_numpy(f0)[None], energy,
                           torch.tensor([[int(singer)]]))
     table = W.step_embedding_table(len(C.noise_schedule(cfg.mapper)))

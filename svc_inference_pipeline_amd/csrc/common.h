@@ -77,7 +77,6 @@ struct ConvGemmArgs {
 enum EpiKind : int {
   EPI_GENERIC = 0,  // v = act(acc + bias[n]) (*col_scale) (+add_t) (+add_row) ((acc32+v)/acc_div)
   EPI_GATE = 1,     // DiffSVC: sigmoid(gate+cp) * tanh(filter+cp)          (paired columns)
-  EPI_RESSKIP = 2,  // DiffSVC: x=(x+res)/sqrt2 ; skip(+)=sk ; next-layer f16 input (paired columns)
   EPI_COND = 3,     // conditioner: acc + bias + emb_m[idx_m] + emb_l[idx_l] + emb_s[singer]
 };
 
@@ -95,12 +94,9 @@ struct EpiArgs {
   const float* add_t; int ld_add_t;         // added after act, indexed by t (positional embedding)
   const float* add_row; int ld_add_row;     // added after act, indexed by orow (residual input)
   int scale_cols; float col_scale;          // columns < scale_cols multiplied by col_scale (q/k scaling)
-  // DiffSVC gate / residual-skip
+  // DiffSVC gate
   const f16* cp; int ld_cp;                 // conditioner projection (packed order, bias folded)
-  float* x32; float* skip32; int ldx32;     // residual stream and skip accumulator [rows][C]
-  const float* dnext;                       // next layer diffusion projection [C] (shared by batch) or null
-  f16* y16; int ldy16;                      // next layer input f16
-  int skip_first, last_layer; float skip_scale;
+  f16* y16; int ldy16;                      // gate output sigmoid(gate) * tanh(filter), f16
   // conditioner
   const int* idx_m; const int* idx_l; const int* singer;
   const float* emb_m; const float* emb_l; const float* emb_s; int ld_emb;

@@ -237,7 +237,8 @@ struct svc_ctx {
   bool has_mapper = false;
   int C = 384, n_mel = 100, n_layers = 20, dil_cycle = 4, steps = 1000, content_dim = 1024, n_bins = 256;
   PackedGemm content_lin, cp_all, melpre, skipproj, outproj;
-  std::vector<PackedGemm> dil, outp;
+  std::vector<PackedGemm> dil, outres;  // per layer: dilated conv (paired), residual half of output_projection
+  PackedGemm skip_all;                  // skip halves of all layers' output_projection, K = layers * C
   float *emb_m = nullptr, *emb_l = nullptr, *emb_s = nullptr, *mbins = nullptr, *ebins = nullptr;
   float* dproj = nullptr;  // [steps][layers][C]
   std::vector<float> alphas_cumprod_f32, sra, srm1, pc1, pc2, plogvar;
@@ -432,7 +433,7 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
     e.ophase = 0;
   }
   if (!e.bias) e.bias = g.bias;
-  const bool pair = (e.kind == EPI_GATE || e.kind == EPI_RESSKIP);
+  const bool pair = e.kind == EPI_GATE;
   if (pair || g.N > 64) {
     static int variant = -1;
     if (variant < 0) {
@@ -563,7 +564,8 @@ int build_mapper(svc_ctx* c) {
   c->steps = steps;
   std::vector<int> perm = pair_perm(C);
   c->dil.resize(NL);
-  c->outp.resize(NL);
+  c->outres.resize(NL);
+  std::vector<const Param*> opw_l(NL), opb_l(NL);
   std::vector<const Param*> cpw(NL), cpb(NL), dpw(NL), dpb(NL);
   for (int i = 0; i < NL; ++i) {
     std::string r = q + "residual_layers." + std::to_string(i) + ".";
@@ -581,8 +583,25 @@ int build_mapper(svc_ctx* c) {
     dpb[i] = pb;
     const int d = 1 << (i % c->dil_cycle);
     if ((st = pack_conv1d(c, c->dil[i], dw->host, db->host, 2 * C, C, 3, C, d, d, 1, &perm))) return st;
-    if ((st = pack_conv1d(c, c->outp[i], ow->host, ob->host, 2 * C, C, 1, C, 1, 0, 1, &perm))) return st;
+    // rows 0..C-1 of output_projection are the residual, C..2C-1 the skip (modules/diffsvc.py:229-231)
+    if ((st = pack_conv1d(c, c->outres[i], ow->host, ob->host, C, C, 1, C, 1, 0, 1))) return st;
+    opw_l[i] = ow;
+    opb_l[i] = ob;
   }
+  // sum over layers of skip_i = g_i @ Wskip_i + bskip_i is ONE GEMM over the concatenated gate outputs
+  // [g_0 .. g_{L-1}] (K = L*C): no per-layer f32 skip read-modify-write
+  st = pack_gemm(
+      c, c->skip_all, C, NL * C, NL * C, 1,
+      [&](int n, int ci, int) {
+        const int l = ci / C, k = ci % C;
+        return opw_l[l]->host[(int64_t)(C + n) * C + k];
+      },
+      [&](int n) {
+        double b = 0;
+        for (int l = 0; l < NL; ++l) b += opb_l[l]->host[C + n];
+        return (float)b;
+      });
+  if (st) return st;
   const int cond_sz = (int)cpw[0]->shape[1];
   // all 20 conditioner projections as one GEMM (loop-invariant over diffusion steps: hoisted)
   st = pack_gemm(
@@ -1111,13 +1130,12 @@ svc_status svc_condition(svc_ctx* c, const void* content16, const double* f0, co
 
 // ---------------------------------------------------------------------------- DiffSVC denoiser
 struct DenoiseBufs {
-  f16* cp16;     // [rows][NL*2C]
-  float* h32;    // [rows][C]
-  float* skip32; // [rows][C]
-  f16* y16;      // [rows][C]
-  f16* g16;      // [rows][C]
-  f16* s16;      // [rows][C] (skip / sqrt(NL), then skip_projection output)
-  f16* u16;
+  f16* cp16;     // [rows][NL*2C] conditioner projections of every layer (hoisted out of the sampler loop)
+  float* h32;    // [rows][C] residual stream
+  f16* y16;      // [rows][C] next layer input x + diffusion_projection
+  f16* g16;      // [rows][NL*C] gate outputs of every layer (A operand of the skip GEMM)
+  f16* s16;      // [rows][C] sum(skip) / sqrt(NL)
+  f16* u16;      // [rows][C] relu(skip_projection)
 };
 
 static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s) {
@@ -1138,22 +1156,29 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     g.kind = EPI_GATE;
     g.cp = bb.cp16 + (size_t)i * 2 * C;
     g.ld_cp = NL * 2 * C;
-    g.y16 = bb.g16;
-    g.ldy16 = C;
+    g.y16 = bb.g16 + (size_t)i * C;
+    g.ldy16 = NL * C;
     if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s, "diffsvc.dilated"))) return st;
+    if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
+    // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step)
     EpiArgs r = epi();
-    r.kind = EPI_RESSKIP;
-    r.x32 = bb.h32;
-    r.skip32 = bb.skip32;
-    r.ldx32 = C;
-    r.skip_first = i == 0;
-    r.last_layer = i == NL - 1;
-    r.skip_scale = sqrtf((float)NL);
-    r.dnext = (i + 1 < NL) ? dp + (size_t)(i + 1) * C : nullptr;
-    r.y16 = (i + 1 < NL) ? bb.y16 : bb.s16;
-    r.ldy16 = C;
-    if ((st = run_gemm(c->outp[i], bb.g16, C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
+    r.acc32 = bb.h32;
+    r.ld_acc = C;
+    r.acc_div = 1.41421356237309515f;
+    r.out32 = bb.h32;
+    r.ld32 = C;
+    r.out16 = bb.y16;
+    r.ld16 = C;
+    r.add16 = dp + (size_t)(i + 1) * C;
+    if ((st = run_gemm(c->outres[i], bb.g16 + (size_t)i * C, NL * C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
   }
+  // skip = sum_i skip_i (modules/diffsvc.py:311); x = skip / sqrt(len(layers)) (:315)
+  e = epi();
+  e.scale_cols = C;
+  e.col_scale = 1.0f / sqrtf((float)NL);
+  e.out16 = bb.s16;
+  e.ld16 = C;
+  if ((st = run_gemm(c->skip_all, bb.g16, NL * C, NL * C, B, T, T, e, s, "diffsvc.skipsum"))) return st;
   e = epi();
   e.act = ACT_RELU;
   e.out16 = bb.u16;
@@ -1170,18 +1195,17 @@ static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   const size_t rows = (size_t)B * T, C = c->C;
   WS_GET(f16, cp16, rows * c->n_layers * 2 * C);
   WS_GET(float, h32, rows * C);
-  WS_GET(float, sk, rows * C);
   WS_GET(f16, y16, rows * C);
-  WS_GET(f16, g16, rows * C);
+  WS_GET(f16, g16, rows * c->n_layers * C);
   WS_GET(f16, s16, rows * C);
   WS_GET(f16, u16, rows * C);
-  bb = DenoiseBufs{cp16, h32, sk, y16, g16, s16, u16};
+  bb = DenoiseBufs{cp16, h32, y16, g16, s16, u16};
   return SVC_OK;
 }
 
 static size_t denoise_bytes(svc_ctx* c, int B, int T) {
   const size_t rows = (size_t)B * T, C = c->C;
-  return rows * c->n_layers * 2 * C * 2 + rows * C * (4 + 4 + 2 * 4) + 16 * 4096;
+  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 3) + 16 * 4096;
 }
 
 static int project_cond(svc_ctx* c, const float* cond, int B, int T, const DenoiseBufs& bb, hipStream_t s) {

@@ -4,7 +4,7 @@
 // K19,K20,K22): the A operand is the time-major f16 activation tensor read through a per-tap row
 // shift (zero padding per utterance), the B operand is the weight packed [N][taps*Cp] f16, the
 // accumulator is f32, and a runtime-selected epilogue fuses bias / GELU / ReLU / positional add /
-// residual add / DiffSVC gated activation / DiffSVC residual+skip update / conditioner embedding sum.
+// residual add / conditioner embedding sum (the paired DiffSVC gate runs in gemm2.hip).
 //
 // Tiling: 256 threads = 4 waves (2x2), tile BM x BN x 64, register-staged global->LDS prefetch of
 // tile k+1 overlapping the MFMAs of tile k, LDS double buffer, one barrier per K-tile. LDS rows are
@@ -33,7 +33,7 @@ __device__ __forceinline__ float act_apply(int act, float v) {
   return v;
 }
 
-template <int BM, int BN, bool PAIR>
+template <int BM, int BN>
 __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiArgs e) {
   using CF = TileCfg<BM, BN>;
   extern __shared__ __align__(16) f16 smem[];
@@ -160,84 +160,46 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
   // acc[i][j][r] = C[m0 + wm*BM/2 + i*16 + (lane>>4)*4 + r][n0 + wn*BN/2 + j*16 + (lane&15)]
   const int mrow0 = m0 + wm * (BM / 2) + (lane >> 4) * 4;
   const int ncol0 = n0 + wn * (BN / 2) + (lane & 15);
-  if constexpr (!PAIR) {
 #pragma unroll
-    for (int i = 0; i < CF::FM; ++i) {
+  for (int i = 0; i < CF::FM; ++i) {
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int m = mrow0 + i * 16 + rr;
-        if (m >= M) continue;
-        const int b = m / a.T_out;
-        const int t = m - b * a.T_out;
-        const int64_t orow = (int64_t)b * e.T_ostore + (int64_t)t * e.ostride + e.ophase;
+    for (int rr = 0; rr < 4; ++rr) {
+      const int m = mrow0 + i * 16 + rr;
+      if (m >= M) continue;
+      const int b = m / a.T_out;
+      const int t = m - b * a.T_out;
+      const int64_t orow = (int64_t)b * e.T_ostore + (int64_t)t * e.ostride + e.ophase;
 #pragma unroll
-        for (int j = 0; j < CF::FN; ++j) {
-          const int n = ncol0 + j * 16;
-          if (n >= a.N) continue;
-          float v = acc[i][j][rr];
-          if (e.kind == EPI_COND) {
-            v = v + e.bias[n];
-            v = v + e.emb_m[(int64_t)e.idx_m[m] * e.ld_emb + n];
-            v = v + e.emb_l[(int64_t)e.idx_l[m] * e.ld_emb + n];
-            v = v + e.emb_s[(int64_t)e.singer[b] * e.ld_emb + n];
-            e.out32[orow * e.ld32 + n] = v;
-            if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(v);
-            continue;
-          }
-          if (e.bias) v += e.bias[n];
-          v = act_apply(e.act, v);
-          if (n < e.scale_cols) v *= e.col_scale;
-          if (e.add_t) v += e.add_t[(int64_t)t * e.ld_add_t + n];
-          if (e.add_row) v += e.add_row[orow * e.ld_add_row + n];
-          if (e.acc32) {
-            v = e.acc32[orow * e.ld_acc + n] + v;
-            if (e.acc_div != 1.0f) v = v / e.acc_div;
-          }
-          if (e.out32) e.out32[orow * e.ld32 + n] = v;
-          if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(e.add16 ? v + e.add16[n] : v);
+      for (int j = 0; j < CF::FN; ++j) {
+        const int n = ncol0 + j * 16;
+        if (n >= a.N) continue;
+        float v = acc[i][j][rr];
+        if (e.kind == EPI_COND) {
+          v = v + e.bias[n];
+          v = v + e.emb_m[(int64_t)e.idx_m[m] * e.ld_emb + n];
+          v = v + e.emb_l[(int64_t)e.idx_l[m] * e.ld_emb + n];
+          v = v + e.emb_s[(int64_t)e.singer[b] * e.ld_emb + n];
+          e.out32[orow * e.ld32 + n] = v;
+          if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(v);
+          continue;
         }
-      }
-    }
-  } else {
-    // paired columns: fragment 2p holds the first-half channel, 2p+1 the second-half channel
-#pragma unroll
-    for (int i = 0; i < CF::FM; ++i) {
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int m = mrow0 + i * 16 + rr;
-        if (m >= M) continue;
-#pragma unroll
-        for (int p = 0; p < CF::FN / 2; ++p) {
-          const int n = ncol0 + 2 * p * 16;  // packed column of the first-half element
-          if (n >= a.N) continue;
-          const int ch = (n >> 5) * 16 + (n & 15);
-          float v1 = acc[i][2 * p][rr] + e.bias[n];
-          float v2 = acc[i][2 * p + 1][rr] + e.bias[n + 16];
-          if (e.kind == EPI_GATE) {
-            const f16* cpr = e.cp + (int64_t)m * e.ld_cp;
-            v1 += (float)cpr[n];
-            v2 += (float)cpr[n + 16];
-            float g = sigmoidf_(v1) * tanhf(v2);
-            e.y16[(int64_t)m * e.ldy16 + ch] = f16_sat(g);
-          } else {  // EPI_RESSKIP
-            const int64_t o = (int64_t)m * e.ldx32 + ch;
-            float xn = (e.x32[o] + v1) / 1.41421356237309515f;
-            e.x32[o] = xn;
-            float sk = e.skip_first ? v2 : (v2 + e.skip32[o]);
-            e.skip32[o] = sk;
-            if (e.last_layer) {
-              e.y16[(int64_t)m * e.ldy16 + ch] = f16_sat(sk / e.skip_scale);
-            } else {
-              e.y16[(int64_t)m * e.ldy16 + ch] = f16_sat(xn + e.dnext[ch]);
-            }
-          }
+        if (e.bias) v += e.bias[n];
+        v = act_apply(e.act, v);
+        if (n < e.scale_cols) v *= e.col_scale;
+        if (e.add_t) v += e.add_t[(int64_t)t * e.ld_add_t + n];
+        if (e.add_row) v += e.add_row[orow * e.ld_add_row + n];
+        if (e.acc32) {
+          v = e.acc32[orow * e.ld_acc + n] + v;
+          if (e.acc_div != 1.0f) v = v / e.acc_div;
         }
+        if (e.out32) e.out32[orow * e.ld32 + n] = v;
+        if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(e.add16 ? v + e.add16[n] : v);
       }
     }
   }
 }
 
-template <int BM, int BN, bool PAIR>
+template <int BM, int BN>
 static int launch(const ConvGemmArgs& a0, const EpiArgs& e, hipStream_t s) {
   using CF = TileCfg<BM, BN>;
   ConvGemmArgs a = a0;
@@ -249,14 +211,14 @@ static int launch(const ConvGemmArgs& a0, const EpiArgs& e, hipStream_t s) {
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm: bad grid %lld", (long long)grid);
   static bool attr_set = false;  // > 64 KiB of dynamic LDS must be opted into once per instantiation
   if (!attr_set) {
-    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)conv_gemm_kernel<BM, BN, PAIR>,
+    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)conv_gemm_kernel<BM, BN>,
                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     attr_set = true;
   }
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
-  const int tok = prof_begin(PAIR ? "conv_gemm<128,128,pair>" : (BN == 32 ? "conv_gemm<256,32>" : (BN == 64 ? "conv_gemm<256,64>" : "conv_gemm<128,128>")),
+  const int tok = prof_begin((BN == 32 ? "conv_gemm<256,32>" : (BN == 64 ? "conv_gemm<256,64>" : "conv_gemm<128,128>")),
                              2.0 * M * (double)a.N * kreal, 0.0, s);
-  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN, PAIR>), dim3((unsigned)grid), dim3(256), lds, s, a, e);
+  hipLaunchKernelGGL((conv_gemm_kernel<BM, BN>), dim3((unsigned)grid), dim3(256), lds, s, a, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
@@ -267,14 +229,10 @@ int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0 && a.K <= a.Kpad && a.Cvalid <= a.Cp,
               "conv_gemm: layout (Cp=%d ldx=%d K=%d Kpad=%d)", a.Cp, a.ldx, a.K, a.Kpad);
   SVC_REQUIRE(a.Cp <= a.ldx || a.Cvalid <= a.ldx, "conv_gemm: Cp > ldx");
-  const bool pair = (e.kind == EPI_GATE || e.kind == EPI_RESSKIP);
-  if (pair) {
-    SVC_REQUIRE(a.N % 32 == 0, "conv_gemm: paired epilogue needs N %% 32 == 0");
-    return launch<128, 128, true>(a, e, s);
-  }
-  if (a.N <= 32) return launch<256, 32, false>(a, e, s);
-  if (a.N <= 64) return launch<256, 64, false>(a, e, s);
-  return launch<128, 128, false>(a, e, s);
+  SVC_REQUIRE(e.kind == EPI_GENERIC || e.kind == EPI_COND, "conv_gemm: paired epilogues run in conv_gemm2");
+  if (a.N <= 32) return launch<256, 32>(a, e, s);
+  if (a.N <= 64) return launch<256, 64>(a, e, s);
+  return launch<128, 128>(a, e, s);
 }
 
 }  // namespace svc

@@ -259,38 +259,13 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void conv_gemm2_kernel(ConvGemmArg
       const float4 b2 = *reinterpret_cast<const float4*>(e.bias + n + 32);
       v1.x += b1.x; v1.y += b1.y; v1.z += b1.z; v1.w += b1.w;
       v2.x += b2.x; v2.y += b2.y; v2.z += b2.z; v2.w += b2.w;
-      union { uint2 u; f16 h[4]; } pk;
-      if (e.kind == EPI_GATE) {
-        union { uint2 u; f16 h[4]; } c1, c2;
-        c1.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n);
-        c2.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n + 32);
-        pk.h[0] = f16_sat(sigmoidf_(v1.x + (float)c1.h[0]) * tanhf(v2.x + (float)c2.h[0]));
-        pk.h[1] = f16_sat(sigmoidf_(v1.y + (float)c1.h[1]) * tanhf(v2.y + (float)c2.h[1]));
-        pk.h[2] = f16_sat(sigmoidf_(v1.z + (float)c1.h[2]) * tanhf(v2.z + (float)c2.h[2]));
-        pk.h[3] = f16_sat(sigmoidf_(v1.w + (float)c1.h[3]) * tanhf(v2.w + (float)c2.h[3]));
-      } else {  // EPI_RESSKIP
-        const int64_t o = (int64_t)m * e.ldx32 + ch;
-        float4 x = *reinterpret_cast<const float4*>(e.x32 + o);
-        x.x = (x.x + v1.x) / 1.41421356237309515f;
-        x.y = (x.y + v1.y) / 1.41421356237309515f;
-        x.z = (x.z + v1.z) / 1.41421356237309515f;
-        x.w = (x.w + v1.w) / 1.41421356237309515f;
-        *reinterpret_cast<float4*>(e.x32 + o) = x;
-        float4 sk = v2;
-        if (!e.skip_first) {
-          const float4 so = *reinterpret_cast<const float4*>(e.skip32 + o);
-          sk.x = v2.x + so.x; sk.y = v2.y + so.y; sk.z = v2.z + so.z; sk.w = v2.w + so.w;
-        }
-        *reinterpret_cast<float4*>(e.skip32 + o) = sk;
-        if (e.last_layer) {
-          pk.h[0] = f16_sat(sk.x / e.skip_scale); pk.h[1] = f16_sat(sk.y / e.skip_scale);
-          pk.h[2] = f16_sat(sk.z / e.skip_scale); pk.h[3] = f16_sat(sk.w / e.skip_scale);
-        } else {
-          const float4 dn = *reinterpret_cast<const float4*>(e.dnext + ch);
-          pk.h[0] = f16_sat(x.x + dn.x); pk.h[1] = f16_sat(x.y + dn.y);
-          pk.h[2] = f16_sat(x.z + dn.z); pk.h[3] = f16_sat(x.w + dn.w);
-        }
-      }
+      union { uint2 u; f16 h[4]; } pk, c1, c2;  // EPI_GATE
+      c1.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n);
+      c2.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n + 32);
+      pk.h[0] = f16_sat(sigmoidf_(v1.x + (float)c1.h[0]) * tanhf(v2.x + (float)c2.h[0]));
+      pk.h[1] = f16_sat(sigmoidf_(v1.y + (float)c1.h[1]) * tanhf(v2.y + (float)c2.h[1]));
+      pk.h[2] = f16_sat(sigmoidf_(v1.z + (float)c1.h[2]) * tanhf(v2.z + (float)c2.h[2]));
+      pk.h[3] = f16_sat(sigmoidf_(v1.w + (float)c1.h[3]) * tanhf(v2.w + (float)c2.h[3]));
       *reinterpret_cast<uint2*>(e.y16 + (int64_t)m * e.ldy16 + ch) = pk.u;
     }
   }
@@ -325,10 +300,10 @@ static int launch2(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
 int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s) {
   SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0 && a.N % 4 == 0, "conv_gemm2: layout");
   SVC_REQUIRE(e.ld32 % 4 == 0 && e.ld16 % 4 == 0 && e.ld_add_row % 4 == 0 && e.ld_acc % 4 == 0 && e.ld_add_t % 4 == 0 &&
-                  e.ld_cp % 4 == 0 && e.ldx32 % 4 == 0 && e.ldy16 % 4 == 0 && e.ld_emb % 4 == 0,
+                  e.ld_cp % 4 == 0 && e.ldy16 % 4 == 0 && e.ld_emb % 4 == 0,
               "conv_gemm2: epilogue leading dimensions must be multiples of 4 (vector epilogue)");
   SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm2: 16-B alignment");
-  const bool pair = (e.kind == EPI_GATE || e.kind == EPI_RESSKIP);
+  const bool pair = e.kind == EPI_GATE;
   if (pair) {
     SVC_REQUIRE(a.N % 64 == 0, "conv_gemm2: paired epilogue needs N %% 64 == 0");
     if (variant == 1) return launch2<256, 128, 4, 2, 3, true>(a, e, zpage, s, "conv_gemm2<256,128,pair>");

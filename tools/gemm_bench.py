@@ -10,9 +10,12 @@ from svc_inference_pipeline_amd import _lib  # noqa: E402
 SHAPES = [  # name, M, N, Cin, taps, epi
     ("diffsvc.dilated(gate)", 29984, 768, 384, 3, 1),
     ("diffsvc.dilated(store)", 29984, 768, 384, 3, 0),
+    ("diffsvc.outproj(res)", 29984, 384, 384, 1, 0),
+    ("diffsvc.skipsum", 29984, 384, 7680, 1, 0),
+    ("bigvgan.s2 k11", 32 * 14992, 384, 384, 11, 0),
     ("whisper.fc1", 48000, 4096, 1024, 1, 0),
     ("whisper.fc2", 48000, 1024, 4096, 1, 0),
-    ("bigvgan.s1 k11", 32 * 14992, 384, 384, 11, 0),
+    ("bigvgan.s1 k11", 32 * 3748, 768, 768, 11, 0),
     ("square 8192", 8192, 8192, 8192, 1, 0),
 ]
 
@@ -27,6 +30,8 @@ def main():
             continue
         row = []
         for v in variants:
+            if v < 0 and epi == 1:  # the paired gate epilogue exists only in conv_gemm2
+                continue
             ms = ctypes.c_double()
             _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, 10, ctypes.byref(ms))
             tf = 2.0 * M * N * Cin * taps / (ms.value * 1e-3) / 1e12

@@ -1,0 +1,15 @@
+#!/bin/bash
+# One gpurun call: GPU parity tests, GEMM variant table, short bench. Each GPU step has its own limit;
+# the script stops at the first failure.
+set -o pipefail
+mkdir -p gpurun_out
+TESTS=${TESTS:-"tests/test_gpu_ops.py tests/test_gpu_stages.py tests/test_gpu_long.py"}
+timeout -k 10 700 python -m pytest $TESTS -m gpu -q --timeout 500 > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest exit $rc"; tail -15 gpurun_out/gpu_tests.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python3 tools/gemm_bench.py ${VARIANTS:--1 0 1 2 3} > gpurun_out/gemm_bench.log 2>&1 || exit $?
+grep -v amdgpu.ids gpurun_out/gemm_bench.log
+if [ -n "$BENCH" ]; then
+  timeout -k 10 400 python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/bench_quick.log 2>&1 || exit $?
+  tail -1 gpurun_out/bench_quick.log | cut -c1-600
+fi
