@@ -100,12 +100,182 @@ __global__ __launch_bounds__(256) void activation1d_v2_kernel(const float* __res
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Register-streaming form (default). A thread owns VEC adjacent channels of one utterance and walks a run
+// of R outputs in blocks of P. It keeps sliding windows in registers: xw = x[t-5 .. t+P+4] (10 carried +
+// P loaded per block) and sw = s[2t-5 .. 2t+2P+4] (10 carried + 2P computed per block). No LDS, no
+// barriers; loads are coalesced across lanes (adjacent lanes = adjacent channel groups). Window values
+// are computed from replicate-clamped x loads, which is exact for every upsampled index inside [0, 2L-1];
+// indices outside take their neighbour's value (the low-pass filter's replicate padding).
+template <int VEC>
+struct ActVec;
+template <>
+struct ActVec<1> {
+  __device__ static void load(const float* p, float* o) { o[0] = *p; }
+  __device__ static void store(f16* p, const float* v) { *p = f16_sat(v[0]); }
+};
+template <>
+struct ActVec<4> {
+  typedef float4 T;
+  __device__ static void load(const float* p, float* o) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+  }
+  __device__ static void store(f16* p, const float* v) {
+    union { uint2 u; f16 h[4]; } pk;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pk.h[i] = f16_sat(v[i]);
+    *reinterpret_cast<uint2*>(p) = pk.u;
+  }
+};
+template <>
+struct ActVec<2> {
+  __device__ static void load(const float* p, float* o) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    o[0] = v.x; o[1] = v.y;
+  }
+  __device__ static void store(f16* p, const float* v) {
+    union { unsigned u; f16 h[2]; } pk;
+    pk.h[0] = f16_sat(v[0]);
+    pk.h[1] = f16_sat(v[1]);
+    *reinterpret_cast<unsigned*>(p) = pk.u;
+  }
+};
+
+template <int VEC, int P, int R>
+__global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __restrict__ x, f16* __restrict__ y,
+                                                              int B, int L, int C, int ldy,
+                                                              const float* __restrict__ alpha_log,
+                                                              const float* __restrict__ beta_log,
+                                                              const float* __restrict__ filt) {
+  static_assert(R % P == 0, "run = whole blocks");
+  using V = ActVec<VEC>;
+  const int ngroups = C / VEC;
+  const int nruns = (L + R - 1) / R;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= (int64_t)B * nruns * ngroups) return;
+  const int g = (int)(gid % ngroups);
+  const int64_t rest = gid / ngroups;
+  const int run = (int)(rest % nruns), b = (int)(rest / nruns);
+  const int c = g * VEC;
+  const float* xb = x + (int64_t)b * L * C + c;
+  f16* yb = y + (int64_t)b * L * ldy + c;
+  float f[12];
+#pragma unroll
+  for (int k = 0; k < 12; ++k) f[k] = filt[k];
+  float as[VEC], ib[VEC];
+#pragma unroll
+  for (int v = 0; v < VEC; ++v) {
+    as[v] = expf(alpha_log[c + v]);
+    ib[v] = 1.0f / (expf(beta_log[c + v]) + 0.000000001f);
+  }
+  auto xload = [&](int t, float* o) {
+    t = t < 0 ? 0 : (t >= L ? L - 1 : t);
+    V::load(xb + (int64_t)t * C, o);
+  };
+  auto snake = [&](float* u) {
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) {
+      const float sn = sin_rev(u[v] * as[v]);
+      u[v] = u[v] + ib[v] * (sn * sn);
+    }
+  };
+  // s[2tb-5+i] from the window xw[k] = x[tb-5+k] (valid when that index lies inside [0, 2L-1])
+  auto s_win = [&](const float (*xw)[VEC], int i, float* o) {
+    const int odd = (i + 1) & 1;           // parity of j = 2tb-5+i
+    const int base = ((i - 5) >> 1) + 2 + odd;
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) o[v] = 0.f;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const float w = f[11 - odd - 2 * a];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) o[v] += xw[base + a][v] * w;
+    }
+#pragma unroll
+    for (int v = 0; v < VEC; ++v) o[v] *= 2.0f;
+    snake(o);
+  };
+
+  const int t0 = run * R;
+  const int t_end = t0 + R < L ? t0 + R : L;
+  float xw[P + 10][VEC], sw[2 * P + 10][VEC];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) xload(t0 - 5 + k, xw[k]);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) s_win(xw, i, sw[i]);
+  // replicate padding of the upsampled signal: s[j] = s[2L-1] past the end, s[0] before the start
+#pragma unroll
+  for (int i = 1; i < 10; ++i)
+    if (2 * t0 - 5 + i > 2 * L - 1)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) sw[i][v] = sw[i - 1][v];
+#pragma unroll
+  for (int i = 8; i >= 0; --i)
+    if (2 * t0 - 5 + i < 0)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) sw[i][v] = sw[i + 1][v];
+  for (int t = t0; t < t_end; t += P) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) xload(t + 5 + k, xw[10 + k]);
+#pragma unroll
+    for (int i = 10; i < 2 * P + 10; ++i) s_win(xw, i, sw[i]);
+    if (2 * t + 2 * P + 4 > 2 * L - 1) {
+#pragma unroll
+      for (int i = 10; i < 2 * P + 10; ++i)
+        if (2 * t - 5 + i > 2 * L - 1)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) sw[i][v] = sw[i - 1][v];
+    }
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      if (t + p < t_end) {
+        float acc[VEC];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v] = 0.f;
+#pragma unroll
+        for (int k = 0; k < 12; ++k)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[v] += f[k] * sw[2 * p + k][v];
+        V::store(yb + (int64_t)(t + p) * ldy, acc);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) xw[k][v] = xw[P + k][v];
+#pragma unroll
+    for (int i = 0; i < 10; ++i)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) sw[i][v] = sw[2 * P + i][v];
+  }
+}
+
+template <int VEC, int P, int R>
+static void launch_rs(const float* x, f16* y, int B, int L, int C, int ldy, const float* al, const float* bl,
+                      const float* filt, hipStream_t s) {
+  const int64_t n = (int64_t)B * cdiv(L, R) * (C / VEC);
+  hipLaunchKernelGGL((activation1d_rs_kernel<VEC, P, R>), dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, y, B, L,
+                     C, ldy, al, bl, filt);
+}
+
 int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const float* alpha_log, const float* beta_log,
                  const float* filt, hipStream_t s) {
   SVC_REQUIRE(L >= 1 && C >= 4 && C % 4 == 0 && ldy % 4 == 0, "activation1d: L=%d C=%d ldy=%d", L, C, ldy);
   SVC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "activation1d: alignment");
   const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * (4 + 2), s);
-  if (C % 64 == 0) {
+  // SVC_ACT_VARIANT (read per call, for A/B runs): 0 = LDS-tiled kernel, 1..4 = register streaming
+  const char* venv = getenv("SVC_ACT_VARIANT");
+  const int variant = venv ? atoi(venv) : 0;
+  if (variant == 1) {
+    launch_rs<4, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
+  } else if (variant == 2) {
+    launch_rs<2, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
+  } else if (variant == 3) {
+    launch_rs<4, 4, 64>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
+  } else if (variant == 4) {
+    launch_rs<1, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
+  } else if (C % 64 == 0) {
     hipLaunchKernelGGL(activation1d_v2_kernel<16>, dim3(cdiv(L, A2_TT), C / 64, B), dim3(256), 0, s, x, y, L, C, ldy,
                        alpha_log, beta_log, filt);
   } else if (C % 48 == 0) {

@@ -309,11 +309,14 @@ int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
     if (variant == 1) return launch2<256, 128, 4, 2, 3, true>(a, e, zpage, s, "conv_gemm2<256,128,pair>");
     if (variant == 2) return launch2<256, 256, 2, 4, 2, true>(a, e, zpage, s, "conv_gemm2<256,256,pair>");
     if (variant == 3) return launch2<192, 256, 2, 4, 2, true>(a, e, zpage, s, "conv_gemm2<192,256,pair>");
+    if (variant == 4) return launch2<128, 128, 2, 2, 2, true>(a, e, zpage, s, "conv_gemm2<128,128,st2,pair>");
     return launch2<128, 128, 2, 2, 4, true>(a, e, zpage, s, "conv_gemm2<128,128,pair>");
   }
   if (variant == 1) return launch2<256, 128, 4, 2, 3, false>(a, e, zpage, s, "conv_gemm2<256,128>");
   if (variant == 2) return launch2<256, 256, 2, 4, 2, false>(a, e, zpage, s, "conv_gemm2<256,256>");
   if (variant == 3) return launch2<192, 256, 2, 4, 2, false>(a, e, zpage, s, "conv_gemm2<192,256>");
+  // 2-deep ring: 68 KiB of LDS, two workgroups per CU overlap one's epilogue with the other's K loop
+  if (variant == 4) return launch2<128, 128, 2, 2, 2, false>(a, e, zpage, s, "conv_gemm2<128,128,st2>");
   return launch2<128, 128, 2, 2, 4, false>(a, e, zpage, s, "conv_gemm2<128,128>");
 }
 

@@ -65,8 +65,11 @@ def test_conv_transpose1d(B, T, Cin, Cout, k, s):
     assert rel_l2(out, ref.numpy()) < 2e-3
 
 
-@pytest.mark.parametrize("B,L,C", [(2, 37, 24), (1, 1, 24), (1, 2, 48), (3, 129, 96), (1, 300, 768), (2, 64, 40)])
-def test_activation1d(B, L, C):
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("B,L,C", [(2, 37, 24), (1, 1, 24), (1, 2, 48), (1, 3, 8), (2, 11, 12), (3, 129, 96),
+                                   (1, 300, 768), (2, 64, 40), (2, 257, 48)])
+def test_activation1d(B, L, C, variant, monkeypatch):
+    monkeypatch.setenv("SVC_ACT_VARIANT", variant)
     from svc_inference_pipeline_amd import weights as W
     g = torch.Generator().manual_seed(2)
     x = torch.randn(B, C, L, generator=g) * 2

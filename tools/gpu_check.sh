@@ -7,7 +7,11 @@ TESTS=${TESTS:-"tests/test_gpu_ops.py tests/test_gpu_stages.py tests/test_gpu_lo
 timeout -k 10 700 python -m pytest $TESTS -m gpu -q --timeout 500 > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "pytest exit $rc"; tail -15 gpurun_out/gpu_tests.log
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python3 tools/gemm_bench.py ${VARIANTS:--1 0 1 2 3} > gpurun_out/gemm_bench.log 2>&1 || exit $?
+if [ -n "$ACT" ]; then
+  timeout -k 10 300 python3 tools/act_bench.py > gpurun_out/act_bench.log 2>&1 || exit $?
+  grep -v amdgpu.ids gpurun_out/act_bench.log
+fi
+timeout -k 10 300 python3 tools/gemm_bench.py ${VARIANTS:--1 0 1 2 3 4} > gpurun_out/gemm_bench.log 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/gemm_bench.log
 if [ -n "$BENCH" ]; then
   timeout -k 10 400 python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/bench_quick.log 2>&1 || exit $?
