@@ -10,7 +10,7 @@ CXXFLAGS := -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-functi
 
 all: $(LIB)
 
-build/%.o: $(SRC_DIR)/%.hip $(SRC_DIR)/common.h include/svc_hip.h
+build/%.o: $(SRC_DIR)/%.hip $(wildcard $(SRC_DIR)/*.h) include/svc_hip.h
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@
 

@@ -105,6 +105,7 @@ int energy_from_mel(const float* mel, int n_mels, float* en, int rows, hipStream
 int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s);
 int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
+int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int pack_qkv(const float* q, const float* k, const float* v, f16* qkv, int64_t rows, int D, float scale, hipStream_t s);
 int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double time_step, double floor_hz,
@@ -434,13 +435,12 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   }
   if (!e.bias) e.bias = g.bias;
   const bool pair = e.kind == EPI_GATE;
+  // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..13 = conv_gemm3 tile, 14 = gemm3 auto
+  const char* venv = getenv("SVC_GEMM_VARIANT");  // read per call (A/B runs and tests switch it)
+  const int variant = venv ? atoi(venv) : 0;
   if (pair || g.N > 64) {
-    static int variant = -1;
-    if (variant < 0) {
-      const char* v = getenv("SVC_GEMM_VARIANT");
-      variant = v ? atoi(v) : 0;
-    }
-    if (pair || variant >= 0) return conv_gemm2(a, e, zero_page(), variant, s);
+    if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
+    if (pair || variant >= 0) return conv_gemm2(a, e, zero_page(), variant < 0 ? 0 : variant, s);
   }
   return conv_gemm(a, e, s);
 }
@@ -1639,10 +1639,14 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_HIP_CHECK(hipEventCreate(&e0));
   SVC_HIP_CHECK(hipEventCreate(&e1));
   int st = SVC_OK;
-  for (int w = 0; w < 2 && !st; ++w) st = variant < 0 ? conv_gemm(a, e, 0) : conv_gemm2(a, e, zero_page(), variant, 0);
+  auto run = [&]() {
+    if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, 0);
+    return variant < 0 ? conv_gemm(a, e, 0) : conv_gemm2(a, e, zero_page(), variant, 0);
+  };
+  for (int w = 0; w < 2 && !st; ++w) st = run();
   SVC_HIP_CHECK(hipEventRecord(e0, 0));
   for (int i = 0; i < iters && !st; ++i)
-    st = variant < 0 ? conv_gemm(a, e, 0) : conv_gemm2(a, e, zero_page(), variant, 0);
+    st = run();
   SVC_HIP_CHECK(hipEventRecord(e1, 0));
   SVC_HIP_CHECK(hipEventSynchronize(e1));
   float ms = 0;

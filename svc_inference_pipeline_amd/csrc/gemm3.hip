@@ -1,0 +1,345 @@
+// Third-generation implicit-GEMM Conv1d / Linear for gfx950: 8-wave ping-pong, v_mfma_f32_16x16x32_f16.
+//
+// Same operands and epilogues as conv_gemm2 (A = time-major f16 activations read through per-tap row
+// shifts, B = weights packed [Npad][Kpad], LDS images of 128-B rows with the 16-B chunk XOR swizzle
+// kv ^ ((row >> 1) & 7) applied on the DMA source address), different schedule:
+//
+//   * 8 waves = 2 (M) x 4 (N); wave tile (BM/2) x (BN/4), split into 4 quadrants (m half, n half).
+//     A K-tile (BK = 64) is 4 phases, one quadrant each: phase p reads its quadrant's fragments
+//     (L section), then barrier, then 16 MFMAs (M section, s_setprio 1), then barrier.
+//   * The two wave groups run one barrier apart (group 1 takes an extra barrier first), so on every
+//     SIMD one wave's M section overlaps the other wave's L section: LDS-read latency and DMA issue
+//     hide behind the partner's MFMAs instead of stalling the matrix pipe.
+//   * Global -> LDS by LDS-DMA into 2 K-tile buffers, one half-tile (A-lo, A-hi, B-lo or B-hi: the rows
+//     one quadrant half needs) per phase with a counted vmcnt:
+//         phase 0: B-lo(k+1)  1: B-hi(k+1)  2: A-hi(k+1)  3: A-lo(k+2)
+//     Each half-tile is restaged >= 2 phases after its last read of the previous use of that buffer
+//     (write-after-read across the staggered groups) and retired (vmcnt + barrier) >= 1 phase before
+//     its first read; vmcnt(N) keeps the 3 youngest half-tiles in flight. Tiles past the end are
+//     dummy DMAs from the zero page so the counts stay uniform.
+//   * When Cp % 64 == 0 a K-tile lies inside one conv tap: the tap shift is wave-uniform and the
+//     A-operand address is a per-lane base plus a scalar offset (one compare + select per DMA).
+#include "common.h"
+#include "epilogue.h"
+
+namespace svc {
+
+template <int BM, int BN>
+struct G3 {
+  static constexpr int NT = 512;
+  static constexpr int WTM = BM / 2, WTN = BN / 4;   // wave tile
+  static constexpr int QM = WTM / 2, QN = WTN / 2;   // quadrant (one phase)
+  static constexpr int FQM = QM / 16, FQN = QN / 16; // 16x16 fragments per quadrant
+  static constexpr int TILE = (BM + BN) * 128;       // bytes of one K-tile image (A rows, then B rows)
+  static constexpr int RING = 2 * TILE;
+  static constexpr int AH = BM / 128;                // DMA instructions per wave per A half-tile
+  static constexpr int BH = BN / 128;
+  static constexpr int EP = (BM * (BN + 4) * 4 <= 163840) ? 1 : 2;
+  static constexpr int LDC = BN / EP + 4;
+  static constexpr int C_BYTES = BM * LDC * 4;
+  static constexpr int LDS = RING > C_BYTES ? RING : C_BYTES;
+  static_assert(LDS <= 163840, "LDS budget");
+  static_assert(QM % 16 == 0 && QN % 16 == 0 && QM % 8 == 0 && QN % 8 == 0 && AH >= 1 && BH >= 1, "tile shape");
+};
+
+__device__ __forceinline__ int sw3(int row, int kv) { return kv ^ ((row >> 1) & 7); }
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void g3_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ void g3_dma(const void* src, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// row (within the A or B image) of element i of half-tile h, for a half made of blocks of Q rows
+// every W rows: rows w*W + h*Q + [0, Q)
+__device__ __forceinline__ int half_row(int i, int h, int Q, int W) { return (i / Q) * W + h * Q + (i % Q); }
+
+template <int BM, int BN, bool CP64, bool PAIR>
+__global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage,
+                                                           float inv_cp) {
+  using CF = G3<BM, BN>;
+  extern __shared__ __align__(16) unsigned char sm3[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tile_n = wgid % a.ntiles_n, tile_m = wgid / a.ntiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int M = a.B * a.T_out;
+  const int nk = a.Kpad / 64;
+  const f16* zsrc = zpage + lane * 8;
+
+  // ---- DMA slots. A half h, instruction v: image rows rb .. rb+7, lane -> row rb + (lane >> 3),
+  // LDS chunk lane & 7 holding logical k-chunk kv = (lane & 7) ^ ((row >> 1) & 7).
+  int a_rb[2][CF::AH], a_kv[2][CF::AH], a_t[2][CF::AH];
+  const f16* a_p[2][CF::AH];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int v = 0; v < CF::AH; ++v) {
+      const int u = wave + 8 * v;
+      const int rb = half_row(8 * u, h, CF::QM, CF::WTM);
+      const int row = rb + (lane >> 3);
+      const int kv = sw3(row, lane & 7);
+      a_rb[h][v] = rb;
+      a_kv[h][v] = kv;
+      const int m = m0 + row;
+      if (m < M) {
+        const int b = m / a.T_out, t = m - b * a.T_out;
+        a_t[h][v] = t * a.istride;
+        a_p[h][v] = a.X + (int64_t)b * a.T_in * a.ldx + kv * 8;
+      } else {
+        a_t[h][v] = -(1 << 29);
+        a_p[h][v] = a.X;
+      }
+    }
+  int b_rb[2][CF::BH];
+  const f16* b_p[2][CF::BH];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int v = 0; v < CF::BH; ++v) {
+      const int u = wave + 8 * v;
+      const int rb = half_row(8 * u, h, CF::QN, CF::WTN);
+      const int row = rb + (lane >> 3);
+      b_rb[h][v] = rb;
+      b_p[h][v] = a.W + (int64_t)(n0 + row) * a.Kpad + sw3(row, lane & 7) * 8;
+    }
+
+  auto a_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE; };
+  auto b_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE + BM * 128; };
+
+  auto issue_a = [&](int h, int kt) {
+    unsigned char* dst = a_img(kt);
+    if constexpr (CP64) {
+      // the whole K-tile lies in tap `tap`; columns c0 .. c0+63 of it
+      const int kg = kt * 64;
+      const int tap = kg / a.Cp;  // wave-uniform
+      const int c0 = kg - tap * a.Cp;
+      const int shift = tap * a.tap_mul + a.tap_add;
+      const int64_t off = (int64_t)shift * a.ldx + c0;
+#pragma unroll
+      for (int v = 0; v < CF::AH; ++v) {
+        const int st = a_t[h][v] + shift;
+        const bool ok = kt < nk && st >= 0 && st < a.T_in;
+        const f16* src = ok ? a_p[h][v] + (int64_t)a_t[h][v] * a.ldx + off : zsrc;
+        g3_dma(src, dst + a_rb[h][v] * 128);
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < CF::AH; ++v) {
+        const int kg = kt * 64 + a_kv[h][v] * 8;
+        int tap = (int)((float)kg * inv_cp);
+        if ((tap + 1) * a.Cp <= kg) ++tap;
+        if (tap * a.Cp > kg) --tap;
+        const int c = kg - tap * a.Cp;
+        const int st = a_t[h][v] + tap * a.tap_mul + a.tap_add;
+        const bool ok = kt < nk && kg < a.K && st >= 0 && st < a.T_in;
+        // a_p already carries the lane's kv * 8 column offset: add the tap-local column base only
+        const f16* src = ok ? a_p[h][v] + (int64_t)st * a.ldx + (c - a_kv[h][v] * 8) : zsrc;
+        g3_dma(src, dst + a_rb[h][v] * 128);
+      }
+    }
+  };
+  auto issue_b = [&](int h, int kt) {
+    unsigned char* dst = b_img(kt);
+#pragma unroll
+    for (int v = 0; v < CF::BH; ++v) g3_dma(kt < nk ? (const void*)(b_p[h][v] + kt * 64) : (const void*)zsrc, dst + b_rb[h][v] * 128);
+  };
+
+  floatx4 acc[2][2][CF::FQM][CF::FQN];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < CF::FQM; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FQN; ++j) acc[x][y][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  half8 af[CF::FQM][2], bf[CF::FQN][2];
+  const int fr = lane & 15, fk = lane >> 4;
+
+  // one phase: quadrant (QMI, QNI) of K-tile kt
+  auto phase = [&](auto QMI_, auto QNI_, int kt) {
+    constexpr int QMI = decltype(QMI_)::value, QNI = decltype(QNI_)::value;
+    constexpr int P = QMI * 2 + QNI;
+    const unsigned char* Ab = a_img(kt);
+    const unsigned char* Bb = b_img(kt);
+    // ---- L section: this quadrant's fragments (A reused between phases 0/1 and 2/3)
+    if constexpr (QNI == 0) {
+#pragma unroll
+      for (int i = 0; i < CF::FQM; ++i) {
+        const int row = wm * CF::WTM + QMI * CF::QM + i * 16 + fr;
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+          af[i][s] = *reinterpret_cast<const half8*>(Ab + row * 128 + (sw3(row, s * 4 + fk) << 4));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < CF::FQN; ++j) {
+      const int row = wn * CF::WTN + QNI * CF::QN + j * 16 + fr;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        bf[j][s] = *reinterpret_cast<const half8*>(Bb + row * 128 + (sw3(row, s * 4 + fk) << 4));
+    }
+    // restage one half-tile; keep the 3 youngest half-tiles in flight
+    if constexpr (P == 0) {
+      issue_b(0, kt + 1);
+      vm_wait<CF::BH + 2 * CF::AH>();
+    } else if constexpr (P == 1) {
+      issue_b(1, kt + 1);
+      vm_wait<2 * CF::BH + CF::AH>();
+    } else if constexpr (P == 2) {
+      issue_a(1, kt + 1);
+      vm_wait<CF::AH + 2 * CF::BH>();
+    } else {
+      issue_a(0, kt + 2);
+      vm_wait<2 * CF::AH + CF::BH>();
+    }
+    g3_barrier();
+    // ---- M section
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < CF::FQM; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FQN; ++j)
+          acc[QMI][QNI][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][s], bf[j][s], acc[QMI][QNI][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    g3_barrier();
+  };
+
+  // ---- prologue: A-lo(0), B-lo(0), B-hi(0), A-hi(0), A-lo(1) in flight; retire the first two
+  issue_a(0, 0);
+  issue_b(0, 0);
+  issue_b(1, 0);
+  issue_a(1, 0);
+  issue_a(0, 1);
+  vm_wait<2 * CF::AH + CF::BH>();
+  g3_barrier();
+  if (wm == 1) g3_barrier();  // stagger: group 1 runs one barrier behind group 0
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (int kt = 0; kt < nk; ++kt) {
+    phase(I0{}, I0{}, kt);
+    phase(I0{}, I1{}, kt);
+    phase(I1{}, I0{}, kt);
+    phase(I1{}, I1{}, kt);
+  }
+  if (wm == 0) g3_barrier();
+  vm_wait<0>();  // trailing dummy DMAs land before the ring is reused for C staging
+  __syncthreads();
+
+  // ---- epilogue: stage C through LDS in EP column passes, then the shared vector epilogue
+  // acc[x][y][i][j][r] = C[wm*WTM + x*QM + i*16 + fk*4 + r][wn*WTN + y*QN + j*16 + fr]
+  constexpr int EP = CF::EP, BNP = BN / EP, LDC = CF::LDC;
+  float* Cs = reinterpret_cast<float*>(sm3);
+#pragma unroll
+  for (int pass = 0; pass < EP; ++pass) {
+    if (wn / (4 / EP) == pass) {
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int i = 0; i < CF::FQM; ++i)
+#pragma unroll
+            for (int j = 0; j < CF::FQN; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                Cs[(wm * CF::WTM + x * CF::QM + i * 16 + fk * 4 + r) * LDC + wn * CF::WTN - pass * BNP + y * CF::QN +
+                   j * 16 + fr] = acc[x][y][i][j][r];
+    }
+    __syncthreads();
+    epilogue_pass<BM, BNP, LDC, CF::NT, PAIR>(Cs, m0, n0 + pass * BNP, M, a, e, tid);
+    __syncthreads();
+  }
+}
+
+template <int BM, int BN, bool PAIR>
+static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipStream_t s, const char* tag) {
+  using CF = G3<BM, BN>;
+  ConvGemmArgs a = a0;
+  const int M = a.B * a.T_out;
+  a.ntiles_n = cdiv(a.N, BN);
+  const int64_t grid = (int64_t)cdiv(M, BM) * a.ntiles_n;
+  SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm3: bad grid");
+  SVC_REQUIRE((int64_t)a.ntiles_n * BN <= round_up(a.N, 256), "conv_gemm3: weights not padded for BN=%d", BN);
+  const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
+  static bool attr[2] = {false, false};
+  if (!attr[cp64]) {
+    const void* fn = cp64 ? (const void*)conv_gemm3_kernel<BM, BN, true, PAIR>
+                          : (const void*)conv_gemm3_kernel<BM, BN, false, PAIR>;
+    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS));
+    attr[cp64] = true;
+  }
+  const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
+  const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);
+  if (cp64)
+    hipLaunchKernelGGL((conv_gemm3_kernel<BM, BN, true, PAIR>), dim3((unsigned)grid), dim3(CF::NT), CF::LDS, s, a, e,
+                       zpage, 1.0f / (float)a.Cp);
+  else
+    hipLaunchKernelGGL((conv_gemm3_kernel<BM, BN, false, PAIR>), dim3((unsigned)grid), dim3(CF::NT), CF::LDS, s, a, e,
+                       zpage, 1.0f / (float)a.Cp);
+  prof_end(tok, s);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+// tile choice: fewest waves of workgroups over 256 CUs, weighted by the per-FLOP efficiency of the tile
+static int pick3(int M, int N) {
+  const int bms[4] = {256, 128, 256, 128}, bns[4] = {256, 256, 128, 128};
+  const double eff[4] = {1.0, 0.85, 0.85, 0.6};
+  int best = 0;
+  double best_t = 1e300;
+  for (int v = 0; v < 4; ++v) {
+    const int64_t tiles = (int64_t)cdiv(M, bms[v]) * cdiv(N, bns[v]);
+    const double t = (double)cdiv64(tiles, 256) * bms[v] * bns[v] / eff[v];
+    if (t < best_t - 1e-9) {
+      best_t = t;
+      best = v;
+    }
+  }
+  return best;
+}
+
+int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s) {
+  SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0 && a.N % 4 == 0, "conv_gemm3: layout");
+  SVC_REQUIRE(e.ld32 % 4 == 0 && e.ld16 % 4 == 0 && e.ld_add_row % 4 == 0 && e.ld_acc % 4 == 0 && e.ld_add_t % 4 == 0 &&
+                  e.ld_cp % 4 == 0 && e.ldy16 % 4 == 0 && e.ld_emb % 4 == 0,
+              "conv_gemm3: epilogue leading dimensions must be multiples of 4 (vector epilogue)");
+  SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm3: 16-B alignment");
+  const int M = a.B * a.T_out;
+  const int v = (variant >= 0 && variant < 4) ? variant : pick3(M, a.N);
+  if (e.kind == EPI_GATE) {
+    SVC_REQUIRE(a.N % 64 == 0, "conv_gemm3: paired epilogue needs N %% 64 == 0");
+    switch (v) {
+      case 0: return launch3<256, 256, true>(a, e, zpage, s, "conv_gemm3<256,256,pair>");
+      case 1: return launch3<128, 256, true>(a, e, zpage, s, "conv_gemm3<128,256,pair>");
+      case 2: return launch3<256, 128, true>(a, e, zpage, s, "conv_gemm3<256,128,pair>");
+      default: return launch3<128, 128, true>(a, e, zpage, s, "conv_gemm3<128,128,pair>");
+    }
+  }
+  switch (v) {
+    case 0: return launch3<256, 256, false>(a, e, zpage, s, "conv_gemm3<256,256>");
+    case 1: return launch3<128, 256, false>(a, e, zpage, s, "conv_gemm3<128,256>");
+    case 2: return launch3<256, 128, false>(a, e, zpage, s, "conv_gemm3<256,128>");
+    default: return launch3<128, 128, false>(a, e, zpage, s, "conv_gemm3<128,128>");
+  }
+}
+
+}  // namespace svc

@@ -36,6 +36,20 @@ def main():
             _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, 10, ctypes.byref(ms))
             tf = 2.0 * M * N * Cin * taps / (ms.value * 1e-3) / 1e12
             row.append(f"v{v}: {ms.value * 1000:8.1f} us {tf:7.1f} TF")
+        if os.environ.get("GEMM_BENCH_TORCH", "1") == "1":
+            # hipBLASLt yardstick (plain GEMM, K = taps * Cin, no epilogue), same shape
+            a = torch.randn(M, Cin * taps, device="cuda", dtype=torch.float16)
+            b = torch.randn(Cin * taps, N, device="cuda", dtype=torch.float16)
+            torch.mm(a, b)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(10):
+                torch.mm(a, b)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 10
+            row.append(f"torch.mm: {ms * 1000:8.1f} us {2.0 * M * N * Cin * taps / (ms * 1e-3) / 1e12:7.1f} TF")
+            del a, b
         print(f"{name:24s}", " | ".join(row), flush=True)
 
 
