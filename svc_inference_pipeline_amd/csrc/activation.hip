@@ -266,7 +266,7 @@ int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const flo
   const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * (4 + 2), s);
   // SVC_ACT_VARIANT (read per call, for A/B runs): 0 = LDS-tiled kernel, 1..4 = register streaming
   const char* venv = getenv("SVC_ACT_VARIANT");
-  const int variant = venv ? atoi(venv) : 0;
+  const int variant = venv ? atoi(venv) : 2;
   if (variant == 1) {
     launch_rs<4, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
   } else if (variant == 2) {

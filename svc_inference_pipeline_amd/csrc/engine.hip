@@ -435,9 +435,10 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   }
   if (!e.bias) e.bias = g.bias;
   const bool pair = e.kind == EPI_GATE;
-  // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..13 = conv_gemm3 tile, 14 = gemm3 auto
+  // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..13 = conv_gemm3 tile,
+  // 14 (default) = conv_gemm3 with the fitted tile choice
   const char* venv = getenv("SVC_GEMM_VARIANT");  // read per call (A/B runs and tests switch it)
-  const int variant = venv ? atoi(venv) : 0;
+  const int variant = venv ? atoi(venv) : 14;
   if (pair || g.N > 64) {
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
     if (pair || variant >= 0) return conv_gemm2(a, e, zero_page(), variant < 0 ? 0 : variant, s);

@@ -300,15 +300,19 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
   return SVC_OK;
 }
 
-// tile choice: fewest waves of workgroups over 256 CUs, weighted by the per-FLOP efficiency of the tile
-static int pick3(int M, int N) {
+// Tile choice: estimated time = rounds of workgroups over the CUs x cost of one round, in units of a
+// 256x256 round. 128x128 needs 68 KiB of LDS, so two workgroups share a CU (512 slots); the per-round
+// costs are fitted to tools/gemm_bench.py on MI355X (profiles/r01_gemm_bench.txt): 256x128 / 128x256
+// 0.62, 128x128 0.6 (0.4 when K <= 512, where the fixed prologue/epilogue share dominates).
+static int pick3(int M, int N, int Kpad) {
   const int bms[4] = {256, 128, 256, 128}, bns[4] = {256, 256, 128, 128};
-  const double eff[4] = {1.0, 0.85, 0.85, 0.6};
+  const double cost[4] = {1.0, 0.62, 0.62, Kpad <= 512 ? 0.4 : 0.6};
+  const int slots[4] = {256, 256, 256, 512};
   int best = 0;
   double best_t = 1e300;
   for (int v = 0; v < 4; ++v) {
     const int64_t tiles = (int64_t)cdiv(M, bms[v]) * cdiv(N, bns[v]);
-    const double t = (double)cdiv64(tiles, 256) * bms[v] * bns[v] / eff[v];
+    const double t = (double)cdiv64(tiles, slots[v]) * cost[v];
     if (t < best_t - 1e-9) {
       best_t = t;
       best = v;
@@ -324,7 +328,7 @@ int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
               "conv_gemm3: epilogue leading dimensions must be multiples of 4 (vector epilogue)");
   SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm3: 16-B alignment");
   const int M = a.B * a.T_out;
-  const int v = (variant >= 0 && variant < 4) ? variant : pick3(M, a.N);
+  const int v = (variant >= 0 && variant < 4) ? variant : pick3(M, a.N, a.Kpad);
   if (e.kind == EPI_GATE) {
     SVC_REQUIRE(a.N % 64 == 0, "conv_gemm3: paired epilogue needs N %% 64 == 0");
     switch (v) {

@@ -11,9 +11,16 @@ if [ -n "$ACT" ]; then
   timeout -k 10 300 python3 tools/act_bench.py > gpurun_out/act_bench.log 2>&1 || exit $?
   grep -v amdgpu.ids gpurun_out/act_bench.log
 fi
-timeout -k 10 300 python3 tools/gemm_bench.py ${VARIANTS:--1 0 1 2 3 4} > gpurun_out/gemm_bench.log 2>&1 || exit $?
+timeout -k 10 300 python3 tools/gemm_bench.py ${VARIANTS:--1 0 1 10 11 12 13 14} > gpurun_out/gemm_bench.log 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/gemm_bench.log
 if [ -n "$BENCH" ]; then
-  timeout -k 10 400 python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/bench_quick.log 2>&1 || exit $?
-  tail -1 gpurun_out/bench_quick.log | cut -c1-600
+  # BENCH_ENVS: space-separated "VAR=val,VAR=val" settings, one quick bench each ("-" = defaults)
+  i=0
+  for cfg in ${BENCH_ENVS:--}; do
+    i=$((i+1))
+    envs=""; [ "$cfg" != "-" ] && envs=$(echo "$cfg" | tr ',' ' ')
+    echo "bench[$i] $cfg"
+    env $envs timeout -k 10 400 python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/bench_quick_$i.log 2>&1 || exit $?
+    tail -1 gpurun_out/bench_quick_$i.log | cut -c1-300
+  done
 fi
