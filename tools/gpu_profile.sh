@@ -11,11 +11,14 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 STEPS=${STEPS:-3}
+if [ -z "${PMC_ONLY:-}" ]; then
 timeout -k 10 900 python3 bench.py --steps $STEPS --warmup 1 > $OUT/bench.json 2> $OUT/bench.err
 echo "bench done"; tail -c 600 $OUT/bench.json
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/trace_bench.json 2> $OUT/trace_bench.err
 echo "trace done"
-KRE=${KRE:-conv_gemm_kernel<128, 128, true>}
+fi
+# rocprofv3 matches the kernel symbol as recorded (templates with bool parameters stay mangled)
+KRE=${KRE:-conv_gemm3_kernelILi128ELi128ELb1ELb1E}
 timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_fetch.err
 echo "pmc fetch done"
 timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/pmc_write -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_write.err

@@ -10,6 +10,7 @@ import csv
 import glob
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -24,6 +25,19 @@ NAME_MAP = {
 
 
 def short(name):
+    """Demangled kernel name -> the tag bench.py's live profile uses (libsvc_hip prof_begin names)."""
+    m = re.search(r"conv_gemm3_kernel<(\d+), (\d+), (true|false), (true|false)>", name)
+    if m:
+        return f"conv_gemm3<{m.group(1)},{m.group(2)}{',pair' if m.group(4) == 'true' else ''}>"
+    m = re.search(r"conv_gemm3_kernelILi(\d+)ELi(\d+)ELb([01])ELb([01])E", name)  # rocprof keeps these mangled
+    if m:
+        return f"conv_gemm3<{m.group(1)},{m.group(2)}{',pair' if m.group(4) == '1' else ''}>"
+    m = re.search(r"conv_gemm2_kernel<(\d+), (\d+), \d+, \d+, (\d+), (true|false)>", name)
+    if m:
+        return f"conv_gemm2<{m.group(1)},{m.group(2)}{',pair' if m.group(4) == 'true' else ''}>"
+    m = re.search(r"activation1d_rs_kernel", name)
+    if m:
+        return "activation1d"
     for k, v in NAME_MAP.items():
         if k in name:
             return v
