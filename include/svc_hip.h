@@ -99,6 +99,12 @@ svc_status svc_op_conv1d(const float* x, int B, int T_in, int Cin, const float* 
 svc_status svc_op_conv_transpose1d(const float* x, int B, int T_in, int Cin, const float* w, const float* bias,
                                    int Cout, int k, int stride, int pad, float* y, void* stream);
 /* Activation1d(SnakeBeta, logscale): x f32 [B*L][C] -> y f32 [B*L][C] */
+/* BigVGAN AMP step for small channel counts: y = conv_k,d(Activation1d(x)) + bias (+ add_row), fused.
+ * x, add_row, y f32 [B*L][C] time-major; w f32 [C][C][k] (effective weight); C in {24, 48, 96}.
+ * Replaces modules/bigvgan.py:427-431 (a1/c1, a2/c2 pairs) for the late generator stages. */
+svc_status svc_op_amp_conv(const float* x, int B, int L, int C, const float* alpha_log, const float* beta_log,
+                           const float* filt, const float* w, const float* bias, int k, int d, const float* add_row,
+                           float* y, void* stream);
 svc_status svc_op_activation1d(const float* x, int B, int L, int C, const float* alpha_log, const float* beta_log,
                                const float* filt12, float* y, void* stream);
 /* attention on f32 q,k,v [B*L][D] (already projected; scaled inside by dh^-1/4 each) -> out f32 [B*L][D] */

@@ -33,6 +33,8 @@ PROTOTYPES = {
                               c_int, c_void_p, c_void_p]),
     "svc_op_conv_transpose1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                         c_void_p, c_void_p]),
+    "svc_op_amp_conv": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                c_int, c_void_p, c_void_p, c_void_p]),
     "svc_op_activation1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "svc_op_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "svc_op_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),

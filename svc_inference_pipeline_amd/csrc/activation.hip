@@ -10,16 +10,11 @@
 // sin uses v_sin_f32 after an explicit reduction to [-0.5, 0.5] revolutions: its error (~|u|*6e-8) is the
 // size of the f32 rounding of the argument u*alpha that the reference itself incurs.
 #include "common.h"
+#include "snake.h"
 
 namespace svc {
 
 constexpr int A2_TT = 64;
-
-__device__ __forceinline__ float sin_rev(float x) {
-  float r = x * 0.15915494309189535f;
-  r = r - rintf(r);
-  return __builtin_amdgcn_sinf(r);
-}
 
 template <int CG>
 __global__ __launch_bounds__(256) void activation1d_v2_kernel(const float* __restrict__ x, f16* __restrict__ y, int L,
@@ -107,41 +102,6 @@ __global__ __launch_bounds__(256) void activation1d_v2_kernel(const float* __res
 // barriers; loads are coalesced across lanes (adjacent lanes = adjacent channel groups). Window values
 // are computed from replicate-clamped x loads, which is exact for every upsampled index inside [0, 2L-1];
 // indices outside take their neighbour's value (the low-pass filter's replicate padding).
-template <int VEC>
-struct ActVec;
-template <>
-struct ActVec<1> {
-  __device__ static void load(const float* p, float* o) { o[0] = *p; }
-  __device__ static void store(f16* p, const float* v) { *p = f16_sat(v[0]); }
-};
-template <>
-struct ActVec<4> {
-  typedef float4 T;
-  __device__ static void load(const float* p, float* o) {
-    const float4 v = *reinterpret_cast<const float4*>(p);
-    o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-  }
-  __device__ static void store(f16* p, const float* v) {
-    union { uint2 u; f16 h[4]; } pk;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) pk.h[i] = f16_sat(v[i]);
-    *reinterpret_cast<uint2*>(p) = pk.u;
-  }
-};
-template <>
-struct ActVec<2> {
-  __device__ static void load(const float* p, float* o) {
-    const float2 v = *reinterpret_cast<const float2*>(p);
-    o[0] = v.x; o[1] = v.y;
-  }
-  __device__ static void store(f16* p, const float* v) {
-    union { unsigned u; f16 h[2]; } pk;
-    pk.h[0] = f16_sat(v[0]);
-    pk.h[1] = f16_sat(v[1]);
-    *reinterpret_cast<unsigned*>(p) = pk.u;
-  }
-};
-
 template <int VEC, int P, int R>
 __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __restrict__ x, f16* __restrict__ y,
                                                               int B, int L, int C, int ldy,

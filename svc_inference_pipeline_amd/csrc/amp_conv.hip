@@ -1,0 +1,263 @@
+// BigVGAN AMP-block convolution for small channel counts (C = 24 / 48 / 96, the late generator stages),
+// with the Activation1d that precedes it fused in (modules/bigvgan.py:424-431 AMPBlock1.forward:
+// xt = a1(x); xt = c1(xt); xt = a2(xt); xt = c2(xt); x = xt + x — Activation1d :234-307, SnakeBeta :146-159).
+//
+// At these widths a conv is HBM-bound: per output element it does 2*k*C MACs (<= 2.1 kFLOP) against 8+ B of
+// traffic. So the kernel is built for memory, not the matrix pipe. A workgroup owns BT consecutive output
+// rows of one utterance, i.e. one contiguous [BT][C] block of every time-major tensor:
+//   1. act -> LDS: SnakeBeta (x2 up-sample, snake, x2 down-sample) of rows [t0-P, t0+BT+P), P = (k-1)/2*d,
+//      streamed from x (f32) with per-thread sliding register windows (as activation1d_rs_kernel), stored
+//      f16 into an LDS image. Rows outside [0, L) are zeros: the conv's own zero padding.
+//   2. conv: v_mfma_f32_16x16x32_f16 with A fragments read from the LDS image at row r + tap*d (row stride
+//      padded so 16-row fragment reads are conflict-free) and B = the packed weights [Npad][Kpad] (L1/L2).
+//   3. epilogue: C staged through LDS, then streamed as float4 over the contiguous block: bias, residual add
+//      (add_row), resblock mean accumulation (acc32 / acc_div), f32 and/or f16 stores.
+// The activation never round-trips through HBM, and every HBM access is a coalesced 16-byte stream.
+#include "common.h"
+#include "snake.h"
+#include "amp_conv.h"
+
+namespace svc {
+
+template <int C>
+struct AmpCfg {
+  static constexpr int BT = 128;                    // output rows per workgroup
+  static constexpr int MAXP = 32;                   // max conv padding (k-1)/2*d supported
+  static constexpr int LDA = C == 24 ? 24 : C + 8;  // f16 row stride: 48/112/208 B, conflict-free fragment reads
+  static constexpr int ROWS = BT + 2 * MAXP;
+  static constexpr int FN = (C + 15) / 16;          // 16-column fragments
+  static constexpr int A_BYTES = ROWS * LDA * 2;
+  static constexpr int C_BYTES = BT * C * 4;
+  static constexpr int LDS = A_BYTES > C_BYTES ? A_BYTES : C_BYTES;
+  static_assert(C % 8 == 0 && LDA % 8 == 0, "16-B fragment rows");
+};
+
+constexpr int AMP_NT = 256;
+
+template <int C>
+__global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
+  using CF = AmpCfg<C>;
+  extern __shared__ __align__(16) unsigned char amp_sm[];
+  f16* As = reinterpret_cast<f16*>(amp_sm);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int L = p.L;
+  const int ntiles = (L + CF::BT - 1) / CF::BT;
+  const int b = blockIdx.x / ntiles, t0 = (blockIdx.x - b * ntiles) * CF::BT;
+  const int P = (p.k - 1) / 2 * p.d;
+  const int rows = CF::BT + 2 * P;
+
+  // ------------------------------------------------------------------ 1. SnakeBeta -> LDS (f16)
+  {
+    constexpr int VEC = 2, BLK = 8, RUN = 16;
+    using V = ActVec<VEC>;
+    float f[12];
+#pragma unroll
+    for (int q = 0; q < 12; ++q) f[q] = p.filt[q];
+    const int ngrp = C / VEC;
+    const int nruns = (rows + RUN - 1) / RUN;
+    const float* xb = p.x + (int64_t)b * L * C;
+    for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
+      const int cg = task % ngrp, ru = task / ngrp;
+      const int c = cg * VEC;
+      const int rs = t0 - P + ru * RUN;                       // first global row of this run
+      const int re = min(rs + RUN, t0 + CF::BT + P);
+      float as[VEC], ib[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) {
+        as[v] = expf(p.alpha_log[c + v]);
+        ib[v] = 1.0f / (expf(p.beta_log[c + v]) + 0.000000001f);
+      }
+      auto xload = [&](int t, float* o) {
+        t = t < 0 ? 0 : (t >= L ? L - 1 : t);
+        V::load(xb + (int64_t)t * C + c, o);
+      };
+      auto snake = [&](float* u) {
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          u[v] *= 2.0f;
+          const float sn = sin_rev(u[v] * as[v]);
+          u[v] = u[v] + ib[v] * (sn * sn);
+        }
+      };
+      // s at the two ends of the up-sampled signal (the low-pass filter's replicate padding uses them)
+      float s0[VEC], sE[VEC];
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) s0[v] = sE[v] = 0.f;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        float x0[VEC], x1[VEC];
+        xload(-3 + a, x0);         // j = 0: even, q = 0
+        xload(L - 3 + a, x1);      // j = 2L-1: odd, q = L-1
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          s0[v] += x0[v] * f[11 - 2 * a];
+          sE[v] += x1[v] * f[10 - 2 * a];
+        }
+      }
+      snake(s0);
+      snake(sE);
+      // s[2tb-5+i] from the window xw[q] = x[tb-5+q] (exact inside [0, 2L-1]), else the end value
+      auto s_at = [&](const float (*xw)[VEC], int i, int j, float* o) {
+        const int odd = (i + 1) & 1;
+        const int base = ((i - 5) >> 1) + 2 + odd;
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) o[v] = 0.f;
+#pragma unroll
+        for (int a = 0; a < 6; ++a) {
+          const float w = f[11 - odd - 2 * a];
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) o[v] += xw[base + a][v] * w;
+        }
+        snake(o);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) o[v] = j < 0 ? s0[v] : (j > 2 * L - 1 ? sE[v] : o[v]);
+      };
+      float xw[BLK + 10][VEC], sw[2 * BLK + 10][VEC];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) xload(rs - 5 + q, xw[q]);
+#pragma unroll
+      for (int i = 0; i < 10; ++i) s_at(xw, i, 2 * rs - 5 + i, sw[i]);
+      for (int t = rs; t < re; t += BLK) {
+#pragma unroll
+        for (int q = 0; q < BLK; ++q) xload(t + 5 + q, xw[10 + q]);
+#pragma unroll
+        for (int i = 10; i < 2 * BLK + 10; ++i) s_at(xw, i, 2 * t - 5 + i, sw[i]);
+#pragma unroll
+        for (int q = 0; q < BLK; ++q) {
+          const int row = t + q;
+          if (row < re) {
+            float y[VEC];
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) y[v] = 0.f;
+            if (row >= 0 && row < L) {
+#pragma unroll
+              for (int kk = 0; kk < 12; ++kk)
+#pragma unroll
+                for (int v = 0; v < VEC; ++v) y[v] += f[kk] * sw[2 * q + kk][v];
+            }
+            V::store(As + (row - (t0 - P)) * CF::LDA + c, y);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 10; ++q)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) xw[q][v] = xw[BLK + q][v];
+#pragma unroll
+        for (int i = 0; i < 10; ++i)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) sw[i][v] = sw[2 * BLK + i][v];
+      }
+    }
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------------ 2. conv on the matrix pipe
+  constexpr int MW = CF::BT / 16 / 4;  // 16-row fragments per wave
+  constexpr int CPT = C / 8;           // 8-wide k chunks per tap
+  floatx4 acc[MW][CF::FN];
+#pragma unroll
+  for (int i = 0; i < MW; ++i)
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int ks = (p.k * C + 31) / 32;
+  const int fr = lane & 15, fk = lane >> 4;
+  for (int s = 0; s < ks; ++s) {
+    const int q = 4 * s + fk;
+    int tap = q / CPT, cc = q - tap * CPT;
+    if (tap >= p.k) tap = cc = 0;  // K tail: zero weights, any finite A
+    half8 af[MW], bf[CF::FN];
+#pragma unroll
+    for (int i = 0; i < MW; ++i) {
+      const int r = (wave * MW + i) * 16 + fr + tap * p.d;
+      af[i] = *reinterpret_cast<const half8*>(As + r * CF::LDA + cc * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j)
+      bf[j] = *reinterpret_cast<const half8*>(p.W + (int64_t)(j * 16 + fr) * p.Kpad + s * 32 + fk * 8);
+#pragma unroll
+    for (int i = 0; i < MW; ++i)
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+  }
+  __syncthreads();  // the activation image is dead: reuse LDS for the C tile
+
+  // ------------------------------------------------------------------ 3. epilogue over the [BT][C] block
+  float* Cs = reinterpret_cast<float*>(amp_sm);
+#pragma unroll
+  for (int i = 0; i < MW; ++i)
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) {
+      const int col = j * 16 + fr;
+      if (col < C)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Cs[((wave * MW + i) * 16 + fk * 4 + r) * C + col] = acc[i][j][r];
+    }
+  __syncthreads();
+  const int nvalid = min(CF::BT, L - t0);
+  const int64_t base = ((int64_t)b * L + t0) * C;
+  for (int i4 = tid; i4 < nvalid * C / 4; i4 += AMP_NT) {
+    const int col = (i4 * 4) % C;
+    const int64_t g = base + (int64_t)i4 * 4;
+    float4 v = reinterpret_cast<const float4*>(Cs)[i4];
+    const float4 bi = *reinterpret_cast<const float4*>(p.bias + col);
+    v.x += bi.x; v.y += bi.y; v.z += bi.z; v.w += bi.w;
+    if (e.add_row) {
+      const float4 ar = *reinterpret_cast<const float4*>(e.add_row + g);
+      v.x += ar.x; v.y += ar.y; v.z += ar.z; v.w += ar.w;
+    }
+    if (e.acc32) {
+      const float4 ac = *reinterpret_cast<const float4*>(e.acc32 + g);
+      v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
+      if (e.acc_div != 1.0f) {
+        v.x = v.x / e.acc_div; v.y = v.y / e.acc_div; v.z = v.z / e.acc_div; v.w = v.w / e.acc_div;
+      }
+    }
+    if (e.out32) *reinterpret_cast<float4*>(e.out32 + g) = v;
+    if (e.out16) {
+      union { uint2 u; f16 h[4]; } pk;
+      pk.h[0] = f16_sat(v.x); pk.h[1] = f16_sat(v.y); pk.h[2] = f16_sat(v.z); pk.h[3] = f16_sat(v.w);
+      *reinterpret_cast<uint2*>(e.out16 + g) = pk.u;
+    }
+  }
+}
+
+template <int C>
+static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
+  using CF = AmpCfg<C>;
+  static bool attr = false;
+  if (!attr) {
+    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)amp_conv_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      CF::LDS));
+    attr = true;
+  }
+  const int64_t grid = (int64_t)p.B * cdiv(p.L, CF::BT);
+  SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "amp_conv: bad grid");
+  const double elems = (double)p.B * p.L * C;
+  // algorithmic bytes: x in (f32), output out (f32 and/or f16), epilogue operands in (f32)
+  const double bytes = elems * (4.0 + (e.out32 ? 4 : 0) + (e.out16 ? 2 : 0) + (e.add_row ? 4 : 0) + (e.acc32 ? 4 : 0));
+  const char* tag = C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>");
+  const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
+  hipLaunchKernelGGL(amp_conv_kernel<C>, dim3((unsigned)grid), dim3(AMP_NT), CF::LDS, s, p, e);
+  prof_end(tok, s);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+bool amp_conv_supported(int C, int k, int d) {
+  return (C == 24 || C == 48 || C == 96) && k >= 1 && k % 2 == 1 && (k - 1) / 2 * d <= AmpCfg<24>::MAXP;
+}
+
+// act + conv + epilogue; e uses out32 / out16 / add_row / acc32 with leading dimension C (contiguous rows)
+int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
+  SVC_REQUIRE(amp_conv_supported(C, p.k, p.d), "amp_conv: C=%d k=%d d=%d unsupported", C, p.k, p.d);
+  SVC_REQUIRE(p.L >= 1 && p.Kpad >= p.k * C && p.Kpad % 32 == 0, "amp_conv: L=%d Kpad=%d", p.L, p.Kpad);
+  SVC_REQUIRE((!e.out32 || e.ld32 == C) && (!e.out16 || e.ld16 == C) && (!e.add_row || e.ld_add_row == C) &&
+                  (!e.acc32 || e.ld_acc == C) && !e.add16 && e.act == ACT_NONE && e.kind == EPI_GENERIC,
+              "amp_conv: epilogue must be contiguous rows of C channels (bias / add_row / acc32 / out32 / out16)");
+  SVC_REQUIRE(((uintptr_t)p.x & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "amp_conv: alignment");
+  if (C == 24) return launch_amp<24>(p, e, s);
+  if (C == 48) return launch_amp<48>(p, e, s);
+  return launch_amp<96>(p, e, s);
+}
+
+}  // namespace svc

@@ -14,6 +14,7 @@
 
 #include "../../include/svc_hip.h"
 #include "common.h"
+#include "amp_conv.h"
 
 namespace svc {
 
@@ -1397,6 +1398,8 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
   WS_GET(f16, a16, big);
   WS_GET(f16, next16, big);
   const f16* in16 = pre16;
+  const char* amp_env = getenv("SVC_AMP_FUSED");  // "0" = unfused activation1d + GEMM everywhere (A/B runs)
+  const bool use_amp = !(amp_env && amp_env[0] == '0');
   int L = T;
   const int ns = (int)c->vstages.size();
   for (int i = 0; i < ns; ++i) {
@@ -1419,16 +1422,23 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
       const int nd = (int)S.c1[j].size();
       for (int l = 0; l < nd; ++l) {
         const float* src = (l == 0) ? X : Xj;
-        if ((st = activation1d(src, a16, B, L, ch, ch, S.acts[j][2 * l].alpha, S.acts[j][2 * l].beta,
-                               S.acts[j][2 * l].filt, s)))
-          return st;
+        const ActP& a1 = S.acts[j][2 * l];
+        const ActP& a2 = S.acts[j][2 * l + 1];
+        // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
+        const bool fuse = use_amp && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
         EpiArgs e1 = epi();
         e1.out32 = tmp;
         e1.ld32 = ch;
-        if ((st = run_gemm(S.c1[j][l], a16, ch, ch, B, L, L, e1, s, "bigvgan.amp_c1"))) return st;
-        if ((st = activation1d(tmp, a16, B, L, ch, ch, S.acts[j][2 * l + 1].alpha, S.acts[j][2 * l + 1].beta,
-                               S.acts[j][2 * l + 1].filt, s)))
-          return st;
+        if (fuse) {
+          const PackedGemm& g1 = S.c1[j][l];
+          const AmpConvArgs p1{src, B, L, S.rk[j], S.rd[j][l], a1.alpha, a1.beta, a1.filt, g1.W, g1.Kpad, g1.bias};
+          prof_site("bigvgan.amp_c1");
+          if ((st = amp_conv(p1, ch, e1, s))) return st;
+        } else {
+          if ((st = activation1d(src, a16, B, L, ch, ch, a1.alpha, a1.beta, a1.filt, s))) return st;
+          if ((st = run_gemm(S.c1[j][l], a16, ch, ch, B, L, L, e1, s, "bigvgan.amp_c1"))) return st;
+          if ((st = activation1d(tmp, a16, B, L, ch, ch, a2.alpha, a2.beta, a2.filt, s))) return st;
+        }
         EpiArgs e2 = epi();
         e2.add_row = src;
         e2.ld_add_row = ch;
@@ -1455,7 +1465,14 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
             e2.ld32 = ch;
           }
         }
-        if ((st = run_gemm(S.c2[j][l], a16, ch, ch, B, L, L, e2, s, "bigvgan.amp_c2"))) return st;
+        if (fuse) {
+          const PackedGemm& g2 = S.c2[j][l];
+          const AmpConvArgs p2{tmp, B, L, S.rk[j], 1, a2.alpha, a2.beta, a2.filt, g2.W, g2.Kpad, g2.bias};
+          prof_site("bigvgan.amp_c2");
+          if ((st = amp_conv(p2, ch, e2, s))) return st;
+        } else if ((st = run_gemm(S.c2[j][l], a16, ch, ch, B, L, L, e2, s, "bigvgan.amp_c2"))) {
+          return st;
+        }
       }
     }
     in16 = next16;  // stage output (f16) feeds the next ConvTranspose; it is rewritten only after that ran
@@ -1526,6 +1543,30 @@ svc_status svc_op_conv1d(const float* x, int B, int T_in, int Cin, const float* 
   e.out32 = y;
   e.ld32 = Cout;
   st = run_gemm(g, x16, Cp, Cin, B, T_in, T_out, e, s);
+  (void)hipStreamSynchronize(s);
+  free_packed(c, g);
+  return st;
+}
+
+svc_status svc_op_amp_conv(const float* x, int B, int L, int C, const float* alpha_log, const float* beta_log,
+                           const float* filt, const float* w, const float* bias, int k, int d, const float* add_row,
+                           float* y, void* stream) {
+  svc_ctx* c;
+  op_ws(&c);
+  hipStream_t s = (hipStream_t)stream;
+  SVC_REQUIRE(amp_conv_supported(C, k, d), "op_amp_conv: C=%d k=%d d=%d unsupported", C, k, d);
+  std::vector<float> wh, bh;
+  PackedGemm g;
+  int st;
+  if ((st = pack_from_device(c, g, w, (size_t)C * C * k, bias, C, wh, bh))) return st;
+  if ((st = pack_conv1d(c, g, wh.data(), bh.data(), C, C, k, C, d, (k - 1) / 2 * d, 1))) return st;
+  EpiArgs e = epi();
+  e.out32 = y;
+  e.ld32 = C;
+  e.add_row = add_row;
+  e.ld_add_row = C;
+  const AmpConvArgs p{x, B, L, k, d, alpha_log, beta_log, filt, g.W, g.Kpad, g.bias};
+  st = amp_conv(p, C, e, s);
   (void)hipStreamSynchronize(s);
   free_packed(c, g);
   return st;

@@ -92,6 +92,29 @@ def test_activation1d(B, L, C, variant, monkeypatch):
     assert np.max(np.abs(out - ref.numpy()) / (np.abs(ref.numpy()) + 1e-2)) < 5e-3
 
 
+@pytest.mark.parametrize("C", [24, 48, 96])
+@pytest.mark.parametrize("B,L,k,d", [(2, 37, 3, 1), (1, 1, 11, 5), (1, 5, 7, 3), (2, 130, 11, 5), (1, 300, 7, 3),
+                                     (3, 257, 11, 1)])
+def test_amp_conv(B, L, k, d, C):
+    """Fused SnakeBeta Activation1d -> dilated conv -> bias + residual (BigVGAN C <= 96 stages)."""
+    from svc_inference_pipeline_amd import weights as W
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(B, C, L, generator=g) * 2
+    al = torch.randn(C, generator=g) * 0.3
+    be = torch.randn(C, generator=g) * 0.3
+    f = W.kaiser_sinc_filter1d(0.25, 0.3, 12).view(-1)
+    w = torch.randn(C, C, k, generator=g) / np.sqrt(C * k)
+    b = torch.randn(C, generator=g) * 0.1
+    res = torch.randn(B, C, L, generator=g)
+    ref = F.conv1d(OM.activation1d(x, al, be, f), w, b, padding=(k - 1) // 2 * d, dilation=d) + res
+    y = torch.empty(B * L, C, device="cuda")
+    xd, ad, bd, fd, wd, bbd, rd = dev(_tm(x)), dev(al), dev(be), dev(f), dev(w), dev(b), dev(_tm(res))
+    call("svc_op_amp_conv", ptr(xd), B, L, C, ptr(ad), ptr(bd), ptr(fd), ptr(wd), ptr(bbd), k, d, ptr(rd), ptr(y),
+         stream())
+    out = y.cpu().view(B, L, C).permute(0, 2, 1).numpy()
+    assert rel_l2(out, ref.numpy()) < 2e-3
+
+
 @pytest.mark.parametrize("B,L,D", [(1, 1500, 1024), (2, 100, 128), (1, 64, 64), (2, 1, 64), (1, 129, 256)])
 def test_attention(B, L, D):
     g = torch.Generator().manual_seed(3)
