@@ -115,6 +115,9 @@ svc_status svc_op_layernorm(const float* x, const float* g, const float* b, int 
    read(idx, ...) synchronises and returns kernel idx's name, total ms, launches, algorithmic FLOPs/bytes;
    n_kernels receives the number of distinct kernels. */
 svc_status svc_profile_enable(int enable);
+/* Restrict live profiling to kernels whose name starts with kernel_prefix ("" or NULL = all): bench.py times
+ * only the dominant kernel in its timed region, so the other ~4 000 launches per step carry no events. */
+svc_status svc_profile_filter(const char* kernel_prefix);
 svc_status svc_profile_read(int idx, char* name, int name_len, double* total_ms, int64_t* launches, double* flops,
                             double* bytes, int* n_kernels);
 /* GEMM microbenchmark on synthetic operands: average ms per launch of one implicit-GEMM configuration

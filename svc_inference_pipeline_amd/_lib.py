@@ -39,6 +39,7 @@ PROTOTYPES = {
     "svc_op_attention": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
     "svc_op_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "svc_profile_enable": (c_int, [c_int]),
+    "svc_profile_filter": (c_int, [ctypes.c_char_p]),
     "svc_profile_read": (c_int, [c_int, ctypes.c_char_p, c_int, ctypes.POINTER(c_double), ctypes.POINTER(c_int64),
                                  ctypes.POINTER(c_double), ctypes.POINTER(c_double), ctypes.POINTER(c_int)]),
     "svc_gemm_bench": (c_int, [c_int, c_int, c_int, c_int, c_int, c_int, c_int, ctypes.POINTER(c_double)]),
@@ -81,6 +82,10 @@ def call(name, *args):
 
 def profile_enable(on=True):
     call("svc_profile_enable", 1 if on else 0)
+
+
+def profile_filter(prefix=""):
+    call("svc_profile_filter", prefix.encode() if prefix else None)
 
 
 def profile_read():

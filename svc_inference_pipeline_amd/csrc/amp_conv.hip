@@ -195,28 +195,44 @@ __global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs
   __syncthreads();
   const int nvalid = min(CF::BT, L - t0);
   const int64_t base = ((int64_t)b * L + t0) * C;
-  for (int i4 = tid; i4 < nvalid * C / 4; i4 += AMP_NT) {
-    const int col = (i4 * 4) % C;
-    const int64_t g = base + (int64_t)i4 * 4;
-    float4 v = reinterpret_cast<const float4*>(Cs)[i4];
-    const float4 bi = *reinterpret_cast<const float4*>(p.bias + col);
-    v.x += bi.x; v.y += bi.y; v.z += bi.z; v.w += bi.w;
-    if (e.add_row) {
-      const float4 ar = *reinterpret_cast<const float4*>(e.add_row + g);
-      v.x += ar.x; v.y += ar.y; v.z += ar.z; v.w += ar.w;
+  const int n4 = nvalid * C / 4;
+  constexpr int U = 4;  // loads of a group are issued before its stores (out32 may alias add_row / acc32)
+  for (int g0 = 0; g0 < n4; g0 += AMP_NT * U) {
+    float4 v[U], ar[U], ac[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i4 = g0 + u * AMP_NT + tid;
+      v[u] = ar[u] = ac[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i4 >= n4) continue;
+      const int64_t g = base + (int64_t)i4 * 4;
+      v[u] = reinterpret_cast<const float4*>(Cs)[i4];
+      if (e.add_row) ar[u] = *reinterpret_cast<const float4*>(e.add_row + g);
+      if (e.acc32) ac[u] = *reinterpret_cast<const float4*>(e.acc32 + g);
     }
-    if (e.acc32) {
-      const float4 ac = *reinterpret_cast<const float4*>(e.acc32 + g);
-      v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
-      if (e.acc_div != 1.0f) {
-        v.x = v.x / e.acc_div; v.y = v.y / e.acc_div; v.z = v.z / e.acc_div; v.w = v.w / e.acc_div;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i4 = g0 + u * AMP_NT + tid;
+      if (i4 >= n4) continue;
+      const int col = (i4 * 4) % C;
+      const int64_t g = base + (int64_t)i4 * 4;
+      float4 w = v[u];
+      const float4 bi = *reinterpret_cast<const float4*>(p.bias + col);
+      w.x += bi.x; w.y += bi.y; w.z += bi.z; w.w += bi.w;
+      if (e.add_row) {
+        w.x += ar[u].x; w.y += ar[u].y; w.z += ar[u].z; w.w += ar[u].w;
       }
-    }
-    if (e.out32) *reinterpret_cast<float4*>(e.out32 + g) = v;
-    if (e.out16) {
-      union { uint2 u; f16 h[4]; } pk;
-      pk.h[0] = f16_sat(v.x); pk.h[1] = f16_sat(v.y); pk.h[2] = f16_sat(v.z); pk.h[3] = f16_sat(v.w);
-      *reinterpret_cast<uint2*>(e.out16 + g) = pk.u;
+      if (e.acc32) {
+        w.x = ac[u].x + w.x; w.y = ac[u].y + w.y; w.z = ac[u].z + w.z; w.w = ac[u].w + w.w;
+        if (e.acc_div != 1.0f) {
+          w.x = w.x / e.acc_div; w.y = w.y / e.acc_div; w.z = w.z / e.acc_div; w.w = w.w / e.acc_div;
+        }
+      }
+      if (e.out32) *reinterpret_cast<float4*>(e.out32 + g) = w;
+      if (e.out16) {
+        union { uint2 u2; f16 h[4]; } pk;
+        pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
+        *reinterpret_cast<uint2*>(e.out16 + g) = pk.u2;
+      }
     }
   }
 }

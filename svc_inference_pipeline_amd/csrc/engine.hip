@@ -13,6 +13,8 @@
 #include <vector>
 
 #include "../../include/svc_hip.h"
+#include <cstring>
+
 #include "common.h"
 #include "amp_conv.h"
 
@@ -35,6 +37,7 @@ struct ProfRec {
   double flops, bytes;
 };
 static bool g_prof = false;
+static std::string g_prof_filter;  // when non-empty, only kernels whose name starts with it are recorded
 static std::vector<ProfRec> g_prof_recs;
 static std::vector<hipEvent_t> g_ev_pool;
 
@@ -54,6 +57,7 @@ void prof_site(const char* site) { g_site = site ? site : ""; }
 
 int prof_begin(const char* name, double flops, double bytes, hipStream_t s) {
   if (!g_prof) return -1;
+  if (!g_prof_filter.empty() && strncmp(name, g_prof_filter.c_str(), g_prof_filter.size()) != 0) return -1;
   std::string full = std::string(name) + (g_site[0] ? std::string("@") + g_site : std::string());
   ProfRec r{full, ev_get(), ev_get(), flops, bytes};
   if (!r.a || !r.b) return -1;
@@ -899,6 +903,11 @@ svc_status svc_profile_enable(int enable) {
     g_prof_recs.clear();
   }
   g_prof = enable != 0;
+  return SVC_OK;
+}
+
+svc_status svc_profile_filter(const char* kernel_prefix) {
+  g_prof_filter = kernel_prefix ? kernel_prefix : "";
   return SVC_OK;
 }
 
