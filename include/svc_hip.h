@@ -99,6 +99,15 @@ svc_status svc_op_conv1d(const float* x, int B, int T_in, int Cin, const float* 
 svc_status svc_op_conv_transpose1d(const float* x, int B, int T_in, int Cin, const float* w, const float* bias,
                                    int Cout, int k, int stride, int pad, float* y, void* stream);
 /* Activation1d(SnakeBeta, logscale): x f32 [B*L][C] -> y f32 [B*L][C] */
+/* Rational-ratio resampler (F1; replaces librosa.resample in utils/audio.py:49-53 and ffmpeg's 16 kHz decode in
+ * utils/whisper_extractor/audio.py:41-49). x f32 [B][n_in] -> y f32 [B][svc_resample_len(n_in, sr_in, sr_out)],
+ * scipy.signal.resample_poly's Kaiser(5) polyphase FIR; quantize16 = 1 rounds to int16 / 32768 (s16le decode). */
+int64_t svc_resample_len(int64_t n_in, int sr_in, int sr_out);
+svc_status svc_resample(const float* x, int B, int64_t n_in, int sr_in, int sr_out, int quantize16, float* y,
+                        void* stream);
+/* host-only: the designed taps (cap >= *n, or h = NULL to query *n) and the plan's up/down/pre_remove */
+svc_status svc_resample_filter(int sr_in, int sr_out, double* h, int cap, int* n, int* up, int* down,
+                               int* pre_remove);
 /* BigVGAN AMP step for small channel counts: y = conv_k,d(Activation1d(x)) + bias (+ add_row), fused.
  * x, add_row, y f32 [B*L][C] time-major; w f32 [C][C][k] (effective weight); C in {24, 48, 96}.
  * Replaces modules/bigvgan.py:427-431 (a1/c1, a2/c2 pairs) for the late generator stages. */

@@ -33,6 +33,9 @@ PROTOTYPES = {
                               c_int, c_void_p, c_void_p]),
     "svc_op_conv_transpose1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                         c_void_p, c_void_p]),
+    "svc_resample_len": (ctypes.c_int64, [ctypes.c_int64, c_int, c_int]),
+    "svc_resample": (c_int, [c_void_p, c_int, ctypes.c_int64, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "svc_resample_filter": (c_int, [c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "svc_op_amp_conv": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
                                 c_int, c_void_p, c_void_p, c_void_p]),
     "svc_op_activation1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

@@ -245,3 +245,65 @@ def load_state_dict_checkpoint(path, key, expected):
     if missing or bad:
         raise ValueError(f"checkpoint {path}: missing {missing[:5]}..., shape-mismatch {bad[:5]}...")
     return {k: sd[k].float().numpy() for k in expected}
+
+
+def _tensor_dict(sd, strip_module=True, prefix=None):
+    out = {}
+    for k, v in sd.items():
+        if strip_module:
+            k = k.split("module.")[-1]
+        if prefix is not None and not k.startswith(prefix):
+            continue
+        if torch.is_tensor(v):
+            out[k] = v.detach().float().cpu().numpy()
+    return out
+
+
+def load_checkpoints(mapper_path=None, vocoder_path=None, whisper_path=None):
+    """The reference's three checkpoint formats -> {"mapper"|"vocoder"|"whisper": state dict of f32 arrays}.
+
+    mapper  utils/load_models.py:23-49   ckpt["state_dict"], keys of ModuleList([EncoderFramework, DiffSVC])
+    vocoder utils/load_models.py:52-79   ckpt["generator_state_dict"], keys of Generator
+    whisper utils/whisper_extractor/__init__.py:72-120  {"dims", "model_state_dict"}; the encoder half is kept
+    "module." prefixes are stripped as the reference does. Loading is weights_only (no unpickling of code).
+    Unlike the reference, which keeps random init for missing or mis-shaped keys, SVCEngine's native
+    finalize rejects them (svc_ctx_finalize)."""
+    out = {}
+    if mapper_path:
+        ckpt = torch.load(mapper_path, map_location="cpu", weights_only=True)
+        out["mapper"] = _tensor_dict(ckpt["state_dict"])
+    if vocoder_path:
+        ckpt = torch.load(vocoder_path, map_location="cpu", weights_only=True)
+        out["vocoder"] = _tensor_dict(ckpt["generator_state_dict"])
+    if whisper_path:
+        ckpt = torch.load(whisper_path, map_location="cpu", weights_only=True)
+        out["whisper"] = _tensor_dict(ckpt["model_state_dict"], strip_module=False, prefix="encoder.")
+        dims = ckpt.get("dims", {})
+        got = whisper_dims_from_state(out["whisper"])
+        for k in ("n_mels", "n_audio_ctx", "n_audio_state", "n_audio_head", "n_audio_layer"):
+            if k in dims and int(dims[k]) != int(got[k]):
+                raise ValueError(f"whisper checkpoint {whisper_path}: dims[{k}]={dims[k]} but weights give {got[k]}")
+    return out
+
+
+def save_checkpoints(dirname, mapper_state=None, vocoder_state=None, whisper_state=None, module_prefix=False):
+    """Write states in the reference's checkpoint formats (tests and tools; the inverse of load_checkpoints)."""
+    import os
+    os.makedirs(dirname, exist_ok=True)
+    pre = "module." if module_prefix else ""
+    paths = {}
+    if mapper_state is not None:
+        paths["mapper"] = os.path.join(dirname, "mapper.pt")
+        torch.save({"state_dict": {pre + k: torch.from_numpy(np.asarray(v)) for k, v in mapper_state.items()}},
+                   paths["mapper"])
+    if vocoder_state is not None:
+        paths["vocoder"] = os.path.join(dirname, "vocoder.pt")
+        torch.save({"generator_state_dict": {pre + k: torch.from_numpy(np.asarray(v)) for k, v in vocoder_state.items()}},
+                   paths["vocoder"])
+    if whisper_state is not None:
+        paths["whisper"] = os.path.join(dirname, "whisper.pt")
+        torch.save({"dims": whisper_dims_from_state(whisper_state),
+                    "model_state_dict": {k: torch.from_numpy(np.asarray(v)) for k, v in whisper_state.items()}},
+                   paths["whisper"])
+    return paths
+
