@@ -13,7 +13,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def header_symbols():
     txt = open(os.path.join(REPO, "include", "svc_hip.h")).read()
-    return sorted(set(re.findall(r"^(?:svc_status|const char\*|int)\s+(svc_[a-z0-9_]+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:svc_status|const char\*|int|int64_t)\s+(svc_[a-z0-9_]+)\s*\(", txt, re.M)))
 
 
 def test_header_matches_binding():
