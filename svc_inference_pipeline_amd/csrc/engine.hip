@@ -316,7 +316,7 @@ int pack_gemm(svc_ctx* c, PackedGemm& g, int N, int Cin, int Cp, int taps, WG wg
   g.taps = taps;
   g.K = taps * Cp;
   g.Kpad = (int)round_up(g.K, 64);
-  g.Npad = (int)round_up(N, 256);
+  g.Npad = (int)std::max(round_up(N, 256), round_up(N, 384));  // every conv_gemm2/3 tile width fits
   std::vector<f16> w((size_t)g.Npad * g.Kpad, (f16)0.0f);
   std::vector<float> b((size_t)g.Npad, 0.0f);
   for (int n = 0; n < N; ++n) {
@@ -440,10 +440,10 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   }
   if (!e.bias) e.bias = g.bias;
   const bool pair = e.kind == EPI_GATE;
-  // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..13 = conv_gemm3 tile,
-  // 14 (default) = conv_gemm3 with the fitted tile choice
+  // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..14 = conv_gemm3 tile,
+  // 15 (default) = conv_gemm3 with the fitted tile choice
   const char* venv = getenv("SVC_GEMM_VARIANT");  // read per call (A/B runs and tests switch it)
-  const int variant = venv ? atoi(venv) : 14;
+  const int variant = venv ? atoi(venv) : 15;
   if (pair || g.N > 64) {
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
     if (pair || variant >= 0) return conv_gemm2(a, e, zero_page(), variant < 0 ? 0 : variant, s);
@@ -1664,7 +1664,7 @@ __global__ void fill_f16_kernel(f16* p, int64_t n, uint32_t seed) {
 
 extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_kind, int variant, int iters, double* ms_out) {
   SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters >= 1, "gemm_bench: bad args");
-  const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)round_up(N, 256);
+  const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float* bias;
   SVC_HIP_CHECK(hipMalloc(&X, (size_t)M * Cin * 2));

@@ -278,7 +278,8 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
   a.ntiles_n = cdiv(a.N, BN);
   const int64_t grid = (int64_t)cdiv(M, BM) * a.ntiles_n;
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm3: bad grid");
-  SVC_REQUIRE((int64_t)a.ntiles_n * BN <= round_up(a.N, 256), "conv_gemm3: weights not padded for BN=%d", BN);
+  SVC_REQUIRE((int64_t)a.ntiles_n * BN <= std::max(round_up(a.N, 256), round_up(a.N, 384)),
+              "conv_gemm3: weights not padded for BN=%d", BN);
   const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
   static bool attr[2] = {false, false};
   if (!attr[cp64]) {
@@ -328,13 +329,14 @@ int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
               "conv_gemm3: epilogue leading dimensions must be multiples of 4 (vector epilogue)");
   SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm3: 16-B alignment");
   const int M = a.B * a.T_out;
-  const int v = (variant >= 0 && variant < 4) ? variant : pick3(M, a.N, a.Kpad);
+  const int v = (variant >= 0 && variant < 5) ? variant : pick3(M, a.N, a.Kpad);
   if (e.kind == EPI_GATE) {
     SVC_REQUIRE(a.N % 64 == 0, "conv_gemm3: paired epilogue needs N %% 64 == 0");
     switch (v) {
       case 0: return launch3<256, 256, true>(a, e, zpage, s, "conv_gemm3<256,256,pair>");
       case 1: return launch3<128, 256, true>(a, e, zpage, s, "conv_gemm3<128,256,pair>");
       case 2: return launch3<256, 128, true>(a, e, zpage, s, "conv_gemm3<256,128,pair>");
+      case 4: return launch3<128, 384, true>(a, e, zpage, s, "conv_gemm3<128,384,pair>");
       default: return launch3<128, 128, true>(a, e, zpage, s, "conv_gemm3<128,128,pair>");
     }
   }
@@ -342,6 +344,7 @@ int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
     case 0: return launch3<256, 256, false>(a, e, zpage, s, "conv_gemm3<256,256>");
     case 1: return launch3<128, 256, false>(a, e, zpage, s, "conv_gemm3<128,256>");
     case 2: return launch3<256, 128, false>(a, e, zpage, s, "conv_gemm3<256,128>");
+    case 4: return launch3<128, 384, false>(a, e, zpage, s, "conv_gemm3<128,384>");
     default: return launch3<128, 128, false>(a, e, zpage, s, "conv_gemm3<128,128>");
   }
 }

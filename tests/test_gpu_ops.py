@@ -34,9 +34,9 @@ def _tm(x):  # [B, C, T] -> time-major [B*T, C]
     (3, 700, 384, 768, 3, 1, 2, 2, 0),       # several M tiles + M tail (gemm3 tile shapes)
     (2, 333, 256, 512, 3, 1, 4, 4, 2),
 ])
-@pytest.mark.parametrize("variant", ["0", "1", "-1", "10", "11", "12", "13", "14"])
+@pytest.mark.parametrize("variant", ["0", "1", "-1", "10", "11", "12", "13", "14", "15"])
 def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, monkeypatch):
-    monkeypatch.setenv("SVC_GEMM_VARIANT", variant)  # -1: v1, 0..4: conv_gemm2 tiles, 10..14: conv_gemm3
+    monkeypatch.setenv("SVC_GEMM_VARIANT", variant)  # -1: v1, 0..4: conv_gemm2 tiles, 10..14: conv_gemm3 tiles, 15: auto
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, Cin, T, generator=g)
     w = torch.randn(Cout, Cin, k, generator=g) / np.sqrt(Cin * k)
@@ -53,7 +53,7 @@ def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, monkeypatch)
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k,s", [(2, 25, 768, 384, 8, 4), (1, 40, 96, 48, 4, 2), (2, 33, 48, 24, 4, 2),
                                               (1, 9, 1536, 768, 8, 4)])
-@pytest.mark.parametrize("variant", ["0", "-1", "10", "14"])
+@pytest.mark.parametrize("variant", ["0", "-1", "10", "14", "15"])
 def test_conv_transpose1d(B, T, Cin, Cout, k, s, variant, monkeypatch):
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
     g = torch.Generator().manual_seed(1)

@@ -92,7 +92,7 @@ def test_eps_single_step(engine, cfg, states, golden):
         assert rel_l2(eps.cpu().numpy(), g[f"eps_t{t}"]) < 5e-3, t
 
 
-@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14"])
+@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15"])
 def test_eps_gemm_variants(engine, golden, variant, monkeypatch):
     """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant."""
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
