@@ -302,16 +302,17 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
 }
 
 // Tile choice: estimated time = rounds of workgroups over the CUs x cost of one round, in units of a
-// 256x256 round. 128x128 needs 68 KiB of LDS, so two workgroups share a CU (512 slots); the per-round
-// costs are fitted to tools/gemm_bench.py on MI355X (profiles/r01_gemm_bench.txt): 256x128 / 128x256
-// 0.62, 128x128 0.6 (0.4 when K <= 512, where the fixed prologue/epilogue share dominates).
+// 256x256 round, fitted to tools/gemm_bench.py on MI355X (profiles/r01_gemm_bench.txt):
+//   256x128 / 128x256 0.62; 128x384 0.87 (N = 384 without the 256-wide tile's idle half);
+//   128x128 0.6, or 0.4 when K <= 512 where the fixed prologue/epilogue share dominates. 128x128 needs
+//   68 KiB of LDS, so two workgroups share a CU (512 slots).
 static int pick3(int M, int N, int Kpad) {
-  const int bms[4] = {256, 128, 256, 128}, bns[4] = {256, 256, 128, 128};
-  const double cost[4] = {1.0, 0.62, 0.62, Kpad <= 512 ? 0.4 : 0.6};
-  const int slots[4] = {256, 256, 256, 512};
+  const int bms[5] = {256, 128, 256, 128, 128}, bns[5] = {256, 256, 128, 128, 384};
+  const double cost[5] = {1.0, 0.62, 0.62, Kpad <= 512 ? 0.4 : 0.6, 0.87};
+  const int slots[5] = {256, 256, 256, 512, 256};
   int best = 0;
   double best_t = 1e300;
-  for (int v = 0; v < 4; ++v) {
+  for (int v = 0; v < 5; ++v) {
     const int64_t tiles = (int64_t)cdiv(M, bms[v]) * cdiv(N, bns[v]);
     const double t = (double)cdiv64(tiles, slots[v]) * cost[v];
     if (t < best_t - 1e-9) {
