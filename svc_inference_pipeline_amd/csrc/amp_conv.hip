@@ -21,7 +21,7 @@ namespace svc {
 
 template <int C>
 struct AmpCfg {
-  static constexpr int BT = 128;                    // output rows per workgroup
+  static constexpr int BT = C <= 48 ? 256 : 128;    // output rows per workgroup (halo share of the act work)
   static constexpr int MAXP = 32;                   // max conv padding (k-1)/2*d supported
   static constexpr int LDA = C == 24 ? 24 : C + 8;  // f16 row stride: 48/112/208 B, conflict-free fragment reads
   static constexpr int ROWS = BT + 2 * MAXP;
@@ -48,7 +48,7 @@ __global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs
 
   // ------------------------------------------------------------------ 1. SnakeBeta -> LDS (f16)
   {
-    constexpr int VEC = 2, BLK = 8, RUN = 16;
+    constexpr int VEC = 1, BLK = 8, RUN = 16;
     using V = ActVec<VEC>;
     float f[12];
 #pragma unroll
@@ -112,14 +112,22 @@ __global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs
 #pragma unroll
         for (int v = 0; v < VEC; ++v) o[v] = j < 0 ? s0[v] : (j > 2 * L - 1 ? sE[v] : o[v]);
       };
-      float xw[BLK + 10][VEC], sw[2 * BLK + 10][VEC];
+      float xw[BLK + 10][VEC], sw[2 * BLK + 10][VEC], xn[BLK][VEC];
 #pragma unroll
       for (int q = 0; q < 10; ++q) xload(rs - 5 + q, xw[q]);
+#pragma unroll
+      for (int q = 0; q < BLK; ++q) xload(rs + 5 + q, xn[q]);  // first block, in flight during the warm-up
 #pragma unroll
       for (int i = 0; i < 10; ++i) s_at(xw, i, 2 * rs - 5 + i, sw[i]);
       for (int t = rs; t < re; t += BLK) {
 #pragma unroll
-        for (int q = 0; q < BLK; ++q) xload(t + 5 + q, xw[10 + q]);
+        for (int q = 0; q < BLK; ++q)
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) xw[10 + q][v] = xn[q][v];
+        if (t + BLK < re) {  // next block's loads overlap this block's arithmetic
+#pragma unroll
+          for (int q = 0; q < BLK; ++q) xload(t + BLK + 5 + q, xn[q]);
+        }
 #pragma unroll
         for (int i = 10; i < 2 * BLK + 10; ++i) s_at(xw, i, 2 * t - 5 + i, sw[i]);
 #pragma unroll
@@ -161,19 +169,27 @@ __global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs
     for (int j = 0; j < CF::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int ks = (p.k * C + 31) / 32;
   const int fr = lane & 15, fk = lane >> 4;
+  const f16* wrow = p.W + (int64_t)fr * p.Kpad + fk * 8;
+  half8 bn[CF::FN];  // weight fragments of the next k-step, loaded one step ahead (L2 latency off the MFMA path)
+#pragma unroll
+  for (int j = 0; j < CF::FN; ++j) bn[j] = *reinterpret_cast<const half8*>(wrow + (int64_t)j * 16 * p.Kpad);
   for (int s = 0; s < ks; ++s) {
     const int q = 4 * s + fk;
     int tap = q / CPT, cc = q - tap * CPT;
     if (tap >= p.k) tap = cc = 0;  // K tail: zero weights, any finite A
     half8 af[MW], bf[CF::FN];
 #pragma unroll
+    for (int j = 0; j < CF::FN; ++j) bf[j] = bn[j];
+    if (s + 1 < ks) {
+#pragma unroll
+      for (int j = 0; j < CF::FN; ++j)
+        bn[j] = *reinterpret_cast<const half8*>(wrow + (int64_t)j * 16 * p.Kpad + (s + 1) * 32);
+    }
+#pragma unroll
     for (int i = 0; i < MW; ++i) {
       const int r = (wave * MW + i) * 16 + fr + tap * p.d;
       af[i] = *reinterpret_cast<const half8*>(As + r * CF::LDA + cc * 8);
     }
-#pragma unroll
-    for (int j = 0; j < CF::FN; ++j)
-      bf[j] = *reinterpret_cast<const half8*>(p.W + (int64_t)(j * 16 + fr) * p.Kpad + s * 32 + fk * 8);
 #pragma unroll
     for (int i = 0; i < MW; ++i)
 #pragma unroll
