@@ -184,6 +184,8 @@ struct Arena {
   }
 };
 
+constexpr int kMaxSubStreams = 4;
+
 struct PackedGemm {
   f16* W = nullptr;
   float* bias = nullptr;
@@ -259,6 +261,18 @@ struct svc_ctx {
   float vpost_b = 0;
   float* fade = nullptr;
   int nfade = 5120;
+  // sampler sub-batch streams (svc_diffsvc_sample), created on first use
+  hipStream_t sub_streams[kMaxSubStreams] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[kMaxSubStreams] = {};
+  int n_sub_streams = 0;
+  int ensure_sub_streams(int n) {
+    if (!ev_fork && hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming) != hipSuccess) return SVC_ERR_HIP;
+    for (; n_sub_streams < n; ++n_sub_streams) {
+      if (hipStreamCreateWithFlags(&sub_streams[n_sub_streams], hipStreamNonBlocking) != hipSuccess) return SVC_ERR_HIP;
+      if (hipEventCreateWithFlags(&ev_join[n_sub_streams], hipEventDisableTiming) != hipSuccess) return SVC_ERR_HIP;
+    }
+    return SVC_OK;
+  }
   int hop_out = 256;
 };
 
@@ -837,6 +851,11 @@ svc_status svc_ctx_destroy(svc_ctx* c) {
   (void)hipDeviceSynchronize();
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->ws.base) (void)hipFree(c->ws.base);
+  for (int i = 0; i < c->n_sub_streams; ++i) {
+    (void)hipStreamDestroy(c->sub_streams[i]);
+    (void)hipEventDestroy(c->ev_join[i]);
+  }
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   delete c;
   return SVC_OK;
 }
@@ -1275,24 +1294,6 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
     if ((st = init_noise(x, x16, ld16, B, T, nm, seed, utt_ids, 1.0f / 1.2f, s))) return st;
   }
   WS_GET(float, eps, (size_t)rows * nm);
-  if (mode == SVC_MODE_DDPM) {
-    for (int i = c->steps - 1; i >= 0; --i) {
-      if ((st = denoise(c, bb, x16, B, T, i, eps, s))) return st;
-      DdpmArgs a{};
-      a.sra = c->sra[i];
-      a.srm1 = c->srm1[i];
-      a.c1 = c->pc1[i];
-      a.c2 = c->pc2[i];
-      a.sigma = i > 0 ? expf(0.5f * c->plogvar[i]) : 0.0f;
-      a.z = noise ? noise + (size_t)(c->steps - 1 - i) * rows * nm : nullptr;
-      a.seed = seed;
-      a.utt_ids = utt_ids;
-      a.step = i;
-      if ((st = ddpm_update(x, eps, x16, ld16, B, T, nm, a, s))) return st;
-    }
-    return SVC_OK;
-  }
-  // PLMS: history ring of 4 epsilons + the first step's predictor buffers
   float* hist[5];
   for (int k = 0; k < 5; ++k) {
     WS_GET(float, hb, (size_t)rows * nm);
@@ -1301,6 +1302,64 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
   WS_GET(float, xp, (size_t)rows * nm);
   WS_GET(f16, xp16, (size_t)rows * ld16);
   SVC_HIP_CHECK(hipMemsetAsync(xp16, 0, (size_t)rows * ld16 * sizeof(f16), s));
+
+  // Utterance-aligned sub-batches on their own streams, issued kernel by kernel in alternation: their
+  // launches overlap on the GPU, so one sub-batch's epilogue / prologue phases (HBM-bound, ~40 % of a
+  // denoiser GEMM launch at this size) run beside the other's MFMA phases. Utterances are independent,
+  // so results are identical to a single stream. SVC_SAMPLER_STREAMS=1 disables the split.
+  const char* ns_env = getenv("SVC_SAMPLER_STREAMS");
+  const int S = std::max(1, std::min(std::min(ns_env ? atoi(ns_env) : 2, B), (int)kMaxSubStreams));
+  struct Sub {
+    int B, b0;
+    size_t r0;
+    hipStream_t s;
+  } sub[kMaxSubStreams];
+  if ((st = c->ensure_sub_streams(S))) return st;
+  SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
+  for (int h = 0; h < S; ++h) {
+    sub[h].b0 = h * B / S;
+    sub[h].B = (h + 1) * B / S - sub[h].b0;
+    sub[h].r0 = (size_t)sub[h].b0 * T;
+    sub[h].s = S == 1 ? s : c->sub_streams[h];
+    if (S > 1) SVC_HIP_CHECK(hipStreamWaitEvent(sub[h].s, c->ev_fork, 0));
+  }
+  auto sub_bufs = [&](const Sub& u) {
+    const size_t r = u.r0;
+    const int C = c->C, NL = c->n_layers;
+    return DenoiseBufs{bb.cp16 + r * NL * 2 * C, bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * NL * C, bb.s16 + r * C,
+                       bb.u16 + r * C};
+  };
+  auto join = [&]() -> int {
+    if (S == 1) return SVC_OK;
+    for (int h = 0; h < S; ++h) {
+      SVC_HIP_CHECK(hipEventRecord(c->ev_join[h], sub[h].s));
+      SVC_HIP_CHECK(hipStreamWaitEvent(s, c->ev_join[h], 0));
+    }
+    return SVC_OK;
+  };
+
+  if (mode == SVC_MODE_DDPM) {
+    for (int i = c->steps - 1; i >= 0; --i) {
+      for (int h = 0; h < S; ++h) {
+        const Sub& u = sub[h];
+        const size_t r = u.r0;
+        if ((st = denoise(c, sub_bufs(u), x16 + r * ld16, u.B, T, i, eps + r * nm, u.s))) return st;
+        DdpmArgs a{};
+        a.sra = c->sra[i];
+        a.srm1 = c->srm1[i];
+        a.c1 = c->pc1[i];
+        a.c2 = c->pc2[i];
+        a.sigma = i > 0 ? expf(0.5f * c->plogvar[i]) : 0.0f;
+        a.z = noise ? noise + (size_t)(c->steps - 1 - i) * rows * nm + r * nm : nullptr;
+        a.seed = seed;
+        a.utt_ids = utt_ids ? utt_ids + u.b0 : nullptr;
+        a.step = i;
+        if ((st = ddpm_update(x + r * nm, eps + r * nm, x16 + r * ld16, ld16, u.B, T, nm, a, u.s))) return st;
+      }
+    }
+    return join();
+  }
+  // PLMS: history ring of 4 epsilons + the first step's predictor buffers (the ring position is shared)
   int nh = 0, head = 0;  // hist slots: newest at hist[(head - 1) mod 5]
   const std::vector<float>& ac = c->alphas_cumprod_f32;
   for (int i = ((c->steps - 1) / interval) * interval; i >= 0; i -= interval) {
@@ -1311,67 +1370,73 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
     const float A = 1.0f / (a_t_sq * (a_t_sq + a_prev_sq));
     const float Bc = 1.0f / (a_t_sq * (sqrtf((1.0f - a_prev) * a_t) + sqrtf((1.0f - a_t) * a_prev)));
     const float d = a_prev - a_t;
-    float* ecur = hist[head];
-    if ((st = denoise(c, bb, x16, B, T, i, ecur, s))) return st;
-    PlmsArgs p{};
-    p.d = d;
-    p.A = A;
-    p.Bc = Bc;
-    p.xin = x;
-    p.xout = x;
-    p.x16 = x16;
-    p.ld16 = ld16;
-    auto H = [&](int back) { return hist[((head - back) % 5 + 5) % 5]; };
-    if (nh == 0) {
-      PlmsArgs q = p;
-      q.e[0] = ecur;
-      q.c[0] = 1.0f;
-      q.ne = 1;
-      q.div = 1.0f;
-      q.xout = xp;
-      q.x16 = xp16;
-      if ((st = plms_update(q, rows, nm, s))) return st;
-      float* eprev = hist[(head + 1) % 5];
-      if ((st = denoise(c, bb, xp16, B, T, tp, eprev, s))) return st;
-      p.e[0] = ecur;
-      p.e[1] = eprev;
-      p.c[0] = 1.0f;
-      p.c[1] = 1.0f;
-      p.ne = 2;
-      p.div = 2.0f;
-    } else if (nh == 1) {
-      p.e[0] = ecur;
-      p.e[1] = H(1);
-      p.c[0] = 3.0f;
-      p.c[1] = -1.0f;
-      p.ne = 2;
-      p.div = 2.0f;
-    } else if (nh == 2) {
-      p.e[0] = ecur;
-      p.e[1] = H(1);
-      p.e[2] = H(2);
-      p.c[0] = 23.0f;
-      p.c[1] = -16.0f;
-      p.c[2] = 5.0f;
-      p.ne = 3;
-      p.div = 12.0f;
-    } else {
-      p.e[0] = ecur;
-      p.e[1] = H(1);
-      p.e[2] = H(2);
-      p.e[3] = H(3);
-      p.c[0] = 55.0f;
-      p.c[1] = -59.0f;
-      p.c[2] = 37.0f;
-      p.c[3] = -9.0f;
-      p.ne = 4;
-      p.div = 24.0f;
+    for (int h = 0; h < S; ++h) {
+      const Sub& u = sub[h];
+      const size_t r = u.r0;
+      const int urows = u.B * T;
+      const DenoiseBufs ub = sub_bufs(u);
+      float* ecur = hist[head] + r * nm;
+      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s))) return st;
+      PlmsArgs p{};
+      p.d = d;
+      p.A = A;
+      p.Bc = Bc;
+      p.xin = x + r * nm;
+      p.xout = x + r * nm;
+      p.x16 = x16 + r * ld16;
+      p.ld16 = ld16;
+      auto H = [&](int back) { return hist[((head - back) % 5 + 5) % 5] + r * nm; };
+      if (nh == 0) {
+        PlmsArgs q = p;
+        q.e[0] = ecur;
+        q.c[0] = 1.0f;
+        q.ne = 1;
+        q.div = 1.0f;
+        q.xout = xp + r * nm;
+        q.x16 = xp16 + r * ld16;
+        if ((st = plms_update(q, urows, nm, u.s))) return st;
+        float* eprev = hist[(head + 1) % 5] + r * nm;
+        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s))) return st;
+        p.e[0] = ecur;
+        p.e[1] = eprev;
+        p.c[0] = 1.0f;
+        p.c[1] = 1.0f;
+        p.ne = 2;
+        p.div = 2.0f;
+      } else if (nh == 1) {
+        p.e[0] = ecur;
+        p.e[1] = H(1);
+        p.c[0] = 3.0f;
+        p.c[1] = -1.0f;
+        p.ne = 2;
+        p.div = 2.0f;
+      } else if (nh == 2) {
+        p.e[0] = ecur;
+        p.e[1] = H(1);
+        p.e[2] = H(2);
+        p.c[0] = 23.0f;
+        p.c[1] = -16.0f;
+        p.c[2] = 5.0f;
+        p.ne = 3;
+        p.div = 12.0f;
+      } else {
+        p.e[0] = ecur;
+        p.e[1] = H(1);
+        p.e[2] = H(2);
+        p.e[3] = H(3);
+        p.c[0] = 55.0f;
+        p.c[1] = -59.0f;
+        p.c[2] = 37.0f;
+        p.c[3] = -9.0f;
+        p.ne = 4;
+        p.div = 24.0f;
+      }
+      if ((st = plms_update(p, urows, nm, u.s))) return st;
     }
-    if ((st = plms_update(p, rows, nm, s))) return st;
     head = (head + 1) % 5;
     nh = nh < 4 ? nh + 1 : 4;
   }
-  return SVC_OK;
+  return join();
 }
 
 // ---------------------------------------------------------------------------- BigVGAN

@@ -25,7 +25,10 @@ def main():
     import torch
     torch.cuda.init()
     only = os.environ.get("GEMM_BENCH_SHAPES")
-    for name, M, N, Cin, taps, epi in SHAPES:
+    shapes = SHAPES
+    if os.environ.get("GEMM_BENCH_CUSTOM"):  # "M,N,Cin,taps,epi;..." (e.g. a K sweep)
+        shapes = [(f"custom {c}",) + tuple(int(v) for v in c.split(",")) for c in os.environ["GEMM_BENCH_CUSTOM"].split(";")]
+    for name, M, N, Cin, taps, epi in shapes:
         if only and not any(o in name for o in only.split(",")):
             continue
         row = []
