@@ -59,6 +59,16 @@ def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads):
             "sample": f"1 x {seconds:g} s clip, full oracle path (PLMS speedup {speedup}), torch-CPU fp32, {threads} threads, {dt:.1f} s"}
 
 
+def family(prof):
+    """{"kernel@site": rec} -> {kernel: summed rec}"""
+    out = {}
+    for name, v in prof.items():
+        agg = out.setdefault(name.split("@")[0], dict(ms=0.0, launches=0, flops=0.0, bytes=0.0))
+        for f in agg:
+            agg[f] += v[f]
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,14 +120,36 @@ def main():
             _lib.profile_enable(False)
         log(f"warmup {i + 1}/{args.warmup}")
 
-    by_kernel = {}
-    for name, v in prof_all.items():
-        k = name.split("@")[0]
-        agg = by_kernel.setdefault(k, dict(ms=0.0, launches=0, flops=0.0, bytes=0.0))
-        for f in agg:
-            agg[f] += v[f]
+    by_kernel = family(prof_all)
     dom_name = max(by_kernel.items(), key=lambda kv: kv[1]["ms"])[0]
     share = by_kernel[dom_name]["ms"] / sum(v["ms"] for v in by_kernel.values())
+    dom_site = max((n for n in prof_all if n.split("@")[0] == dom_name), key=lambda n: prof_all[n]["ms"])
+    dom_site = dom_site.split("@")[1] if "@" in dom_site else ""
+
+    # The sampler runs utterance-aligned sub-batches on concurrent streams (SVC_SAMPLER_STREAMS, default 3),
+    # so a launch's HIP-event duration includes time shared with the other streams' kernels. One extra untimed
+    # step with the sampler on a single stream gives the dominant call site's isolated per-launch rate.
+    streams = int(os.environ.get("SVC_SAMPLER_STREAMS", "3"))
+    isolated = None
+    if streams > 1 and dom_site.startswith("diffsvc."):
+        saved = os.environ.get("SVC_SAMPLER_STREAMS")
+        os.environ["SVC_SAMPLER_STREAMS"] = "1"
+        _lib.profile_enable(True)
+        step()
+        torch.cuda.synchronize()
+        iso = _lib.profile_read()
+        _lib.profile_enable(False)
+        if saved is None:
+            os.environ.pop("SVC_SAMPLER_STREAMS")
+        else:
+            os.environ["SVC_SAMPLER_STREAMS"] = saved
+        at_site = {n.split("@")[0]: v for n, v in iso.items() if n.endswith("@" + dom_site)}
+        if at_site:
+            k, v = max(at_site.items(), key=lambda kv: kv[1]["ms"])
+            us = v["ms"] * 1000.0 / v["launches"]
+            tf = v["flops"] / v["launches"] / (us * 1e-6) / 1e12
+            isolated = {"kernel": k, "site": dom_site, "avg_launch_us": round(us, 2), "achieved": round(tf, 2),
+                        "frac": round(tf / PEAK_F16_TFLOPS, 4), "sampler_streams": 1}
 
     dist.barrier()
     torch.cuda.synchronize()
@@ -158,6 +190,10 @@ def main():
     roof["avg_launch_us"] = round(per_launch_s * 1e6, 2)
     roof["launches_timed"] = dom["launches"]
     roof["share_of_kernel_time"] = round(share, 3)
+    roof["site"] = dom_site
+    roof["sampler_streams"] = streams
+    if isolated:
+        roof["isolated"] = isolated
     roof["traffic"] = None
     if os.path.exists(args.pmc_json):
         pmc = json.load(open(args.pmc_json))
@@ -188,7 +224,8 @@ def main():
             "roofline": roof, "cpu_baseline": cpu,
             "algorithmic_tflops_per_step": round(total_flops / 1e12, 2),
             "sustained_tflops": round(total_flops / 1e12 / (ms_per_step / 1000.0), 1),
-            "kernels_profiled_step": "last warmup step, every launch bracketed by HIP events",
+            "kernels_profiled_step": "last warmup step, every launch bracketed by HIP events (sampler sub-batches on "
+                                     f"{streams} concurrent streams: their per-launch times overlap)",
             "kernels": kernels,
         }
         print(json.dumps(line), flush=True)

@@ -17,8 +17,18 @@ echo "bench done"; tail -c 600 $OUT/bench.json
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/trace_bench.json 2> $OUT/trace_bench.err
 echo "trace done"
 fi
-# rocprofv3 matches the kernel symbol as recorded (templates with bool parameters stay mangled)
-KRE=${KRE:-conv_gemm3_kernelILi128ELi128ELb1ELb1E}
+# rocprofv3 matches the kernel symbol as recorded (templates with bool parameters stay mangled): derive the
+# regex of bench.py's dominant kernel tag, e.g. conv_gemm3<128,128,pair> -> conv_gemm3_kernelILi128ELi128ELb.ELb1E
+if [ -z "${KRE:-}" ]; then
+  KRE=$(python3 - "$OUT/bench.json" <<'PY'
+import json, re, sys
+tag = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])["roofline"]["kernel"]
+m = re.match(r"conv_gemm3<(\d+),(\d+)(,pair)?>", tag)
+print(f"conv_gemm3_kernelILi{m[1]}ELi{m[2]}ELb.ELb{1 if m[3] else 0}E" if m else tag.split("<")[0])
+PY
+)
+fi
+echo "PMC kernel regex: $KRE"
 timeout -k 10 900 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/pmc_fetch -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_fetch.err
 echo "pmc fetch done"
 timeout -k 10 900 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/pmc_write -o run -- python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $OUT/pmc_write.err
