@@ -1446,13 +1446,11 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
   SVC_REQUIRE(c->has_vocoder && c->has_mapper, "vocoder (and mapper stats) not loaded");
   hipStream_t s = (hipStream_t)stream;
   const int nm = c->v_in, ldm = (int)round_up(nm, 8);
-  const int Lmax_c = c->v_c0 * 2;  // max over stages of L_i*C_i / T  (6144 for the reference config)
-  int maxLC = 0, Lr = T;
+  int maxLC = 0, Lr = T;  // max over stages of L_i*C_i / T  (6144 for the reference config)
   for (auto& S : c->vstages) {
     Lr *= S.rate;
     maxLC = std::max(maxLC, (Lr / T) * S.cout);
   }
-  (void)Lmax_c;
   const size_t big = (size_t)B * T * maxLC;
   const size_t need = (size_t)B * T * ldm * 2 + (size_t)B * T * c->v_c0 * 2 + big * (4 * 4 + 2 * 2) + 32 * 4096;
   int st;
@@ -1460,102 +1458,144 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
   c->ws.reset();
   SVC_REQUIRE(T * c->hop_out >= c->nfade, "bigvgan: T=%d shorter than the fade-out", T);
   WS_GET(f16, mel16, (size_t)B * T * ldm);
-  if ((st = denorm_mel(x0, mel16, mel_out, ldm, B * T, nm, c->mel_min, c->mel_max, s))) return st;
   WS_GET(f16, pre16, (size_t)B * T * c->v_c0);
-  EpiArgs e = epi();
-  e.out16 = pre16;
-  e.ld16 = c->v_c0;
-  if ((st = run_gemm(c->vpre, mel16, ldm, nm, B, T, T, e, s, "bigvgan.conv_pre"))) return st;
   WS_GET(float, X, big);
   WS_GET(float, Xj, big);
   WS_GET(float, tmp, big);
   WS_GET(float, XS, big);
   WS_GET(f16, a16, big);
   WS_GET(f16, next16, big);
-  const f16* in16 = pre16;
   const char* amp_env = getenv("SVC_AMP_FUSED");  // "0" = unfused activation1d + GEMM everywhere (A/B runs)
   const bool use_amp = !(amp_env && amp_env[0] == '0');
-  int L = T;
   const int ns = (int)c->vstages.size();
+
+  // Utterance-aligned sub-batches on their own streams (as in svc_diffsvc_sample): every buffer is
+  // time-major per utterance, so a sub-batch is a row offset into each; launches alternate between streams.
+  const char* vs_env = getenv("SVC_VOCODER_STREAMS");
+  const int NS = std::max(1, std::min(std::min(vs_env ? atoi(vs_env) : 2, B), (int)kMaxSubStreams));
+  if ((st = c->ensure_sub_streams(NS))) return st;
+  SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
+  int b0[kMaxSubStreams + 1];
+  hipStream_t ss[kMaxSubStreams];
+  for (int h = 0; h <= NS; ++h) b0[h] = h * B / NS;
+  for (int h = 0; h < NS; ++h) {
+    ss[h] = NS == 1 ? s : c->sub_streams[h];
+    if (NS > 1) SVC_HIP_CHECK(hipStreamWaitEvent(ss[h], c->ev_fork, 0));
+  }
+  for (int h = 0; h < NS; ++h) {  // de-normalise + conv_pre
+    const int Bh = b0[h + 1] - b0[h];
+    const size_t r = (size_t)b0[h] * T;
+    if ((st = denorm_mel(x0 + r * nm, mel16 + r * ldm, mel_out ? mel_out + r * nm : nullptr, ldm, Bh * T, nm,
+                         c->mel_min, c->mel_max, ss[h])))
+      return st;
+    EpiArgs e = epi();
+    e.out16 = pre16 + r * c->v_c0;
+    e.ld16 = c->v_c0;
+    if ((st = run_gemm(c->vpre, mel16 + r * ldm, ldm, nm, Bh, T, T, e, ss[h], "bigvgan.conv_pre"))) return st;
+  }
+  int L = T;
   for (int i = 0; i < ns; ++i) {
     VStage& S = c->vstages[i];
     const int Lin = L;
     L = Lin * S.rate;
     const int ch = S.cout;
-    // ConvTranspose1d as `rate` phase GEMMs writing rows t*rate + r
-    for (int r = 0; r < S.rate; ++r) {
-      EpiArgs u = epi();
-      u.T_ostore = L;
-      u.ostride = S.rate;
-      u.ophase = r;
-      u.out32 = X;
-      u.ld32 = ch;
-      if ((st = run_gemm(S.phases[r], in16, S.cin, S.cin, B, Lin, Lin, u, s, "bigvgan.ups"))) return st;
-    }
-    const int nk = (int)S.c1.size();
-    for (int j = 0; j < nk; ++j) {
-      const int nd = (int)S.c1[j].size();
-      for (int l = 0; l < nd; ++l) {
-        const float* src = (l == 0) ? X : Xj;
-        const ActP& a1 = S.acts[j][2 * l];
-        const ActP& a2 = S.acts[j][2 * l + 1];
-        // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
-        const bool fuse = use_amp && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
-        EpiArgs e1 = epi();
-        e1.out32 = tmp;
-        e1.ld32 = ch;
-        if (fuse) {
-          const PackedGemm& g1 = S.c1[j][l];
-          const AmpConvArgs p1{src, B, L, S.rk[j], S.rd[j][l], a1.alpha, a1.beta, a1.filt, g1.W, g1.Kpad, g1.bias};
-          prof_site("bigvgan.amp_c1");
-          if ((st = amp_conv(p1, ch, e1, s))) return st;
-        } else {
-          if ((st = activation1d(src, a16, B, L, ch, ch, a1.alpha, a1.beta, a1.filt, s))) return st;
-          if ((st = run_gemm(S.c1[j][l], a16, ch, ch, B, L, L, e1, s, "bigvgan.amp_c1"))) return st;
-          if ((st = activation1d(tmp, a16, B, L, ch, ch, a2.alpha, a2.beta, a2.filt, s))) return st;
-        }
-        EpiArgs e2 = epi();
-        e2.add_row = src;
-        e2.ld_add_row = ch;
-        if (l + 1 < nd) {
-          e2.out32 = Xj;
-          e2.ld32 = ch;
-        } else if (j == 0) {
-          e2.out32 = XS;
-          e2.ld32 = ch;
-        } else {
-          e2.acc32 = XS;
-          e2.ld_acc = ch;
-          if (j + 1 == nk) {
-            e2.acc_div = (float)nk;
-            if (i + 1 < ns) {
-              e2.out16 = next16;
-              e2.ld16 = ch;
+    for (int h = 0; h < NS; ++h) {
+      const int Bh = b0[h + 1] - b0[h];
+      const hipStream_t sh = ss[h];
+      // each sub-batch owns the fixed region [b0 * T * maxLC, b1 * T * maxLC) of every stage buffer for all
+      // stages (offsets that moved with L * C would let a lagging stream's reads overlap another's writes)
+      const size_t ro = (size_t)b0[h] * T * maxLC;
+      float *Xh = X + ro, *Xjh = Xj + ro, *tmph = tmp + ro, *XSh = XS + ro;
+      f16* a16h = a16 + ro;
+      const f16* in16 = i == 0 ? pre16 + (size_t)b0[h] * T * c->v_c0 : next16 + ro;
+      f16* next16h = next16 + ro;
+      // ConvTranspose1d as `rate` phase GEMMs writing rows t*rate + r
+      for (int r = 0; r < S.rate; ++r) {
+        EpiArgs u = epi();
+        u.T_ostore = L;
+        u.ostride = S.rate;
+        u.ophase = r;
+        u.out32 = Xh;
+        u.ld32 = ch;
+        if ((st = run_gemm(S.phases[r], in16, S.cin, S.cin, Bh, Lin, Lin, u, sh, "bigvgan.ups"))) return st;
+      }
+      const int nk = (int)S.c1.size();
+      for (int j = 0; j < nk; ++j) {
+        const int nd = (int)S.c1[j].size();
+        for (int l = 0; l < nd; ++l) {
+          const float* src = (l == 0) ? Xh : Xjh;
+          const ActP& a1 = S.acts[j][2 * l];
+          const ActP& a2 = S.acts[j][2 * l + 1];
+          // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
+          const bool fuse = use_amp && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
+          EpiArgs e1 = epi();
+          e1.out32 = tmph;
+          e1.ld32 = ch;
+          if (fuse) {
+            const PackedGemm& g1 = S.c1[j][l];
+            const AmpConvArgs p1{src, Bh, L, S.rk[j], S.rd[j][l], a1.alpha, a1.beta, a1.filt, g1.W, g1.Kpad, g1.bias};
+            prof_site("bigvgan.amp_c1");
+            if ((st = amp_conv(p1, ch, e1, sh))) return st;
+          } else {
+            if ((st = activation1d(src, a16h, Bh, L, ch, ch, a1.alpha, a1.beta, a1.filt, sh))) return st;
+            if ((st = run_gemm(S.c1[j][l], a16h, ch, ch, Bh, L, L, e1, sh, "bigvgan.amp_c1"))) return st;
+            if ((st = activation1d(tmph, a16h, Bh, L, ch, ch, a2.alpha, a2.beta, a2.filt, sh))) return st;
+          }
+          EpiArgs e2 = epi();
+          e2.add_row = src;
+          e2.ld_add_row = ch;
+          if (l + 1 < nd) {
+            e2.out32 = Xjh;
+            e2.ld32 = ch;
+          } else if (j == 0) {
+            e2.out32 = XSh;
+            e2.ld32 = ch;
+          } else {
+            e2.acc32 = XSh;
+            e2.ld_acc = ch;
+            if (j + 1 == nk) {
+              e2.acc_div = (float)nk;
+              if (i + 1 < ns) {
+                e2.out16 = next16h;
+                e2.ld16 = ch;
+              } else {
+                e2.out32 = XSh;
+                e2.ld32 = ch;
+              }
             } else {
-              e2.out32 = XS;
+              e2.out32 = XSh;
               e2.ld32 = ch;
             }
-          } else {
-            e2.out32 = XS;
-            e2.ld32 = ch;
+          }
+          if (fuse) {
+            const PackedGemm& g2 = S.c2[j][l];
+            const AmpConvArgs p2{tmph, Bh, L, S.rk[j], 1, a2.alpha, a2.beta, a2.filt, g2.W, g2.Kpad, g2.bias};
+            prof_site("bigvgan.amp_c2");
+            if ((st = amp_conv(p2, ch, e2, sh))) return st;
+          } else if ((st = run_gemm(S.c2[j][l], a16h, ch, ch, Bh, L, L, e2, sh, "bigvgan.amp_c2"))) {
+            return st;
           }
         }
-        if (fuse) {
-          const PackedGemm& g2 = S.c2[j][l];
-          const AmpConvArgs p2{tmp, B, L, S.rk[j], 1, a2.alpha, a2.beta, a2.filt, g2.W, g2.Kpad, g2.bias};
-          prof_site("bigvgan.amp_c2");
-          if ((st = amp_conv(p2, ch, e2, s))) return st;
-        } else if ((st = run_gemm(S.c2[j][l], a16, ch, ch, B, L, L, e2, s, "bigvgan.amp_c2"))) {
-          return st;
-        }
       }
+      // the stage output next16 feeds the next ConvTranspose; it is rewritten only after that ran (same stream)
     }
-    in16 = next16;  // stage output (f16) feeds the next ConvTranspose; it is rewritten only after that ran
   }
   const int chl = c->vstages.back().cout;
-  if ((st = activation1d(XS, a16, B, L, chl, chl, c->vact_post.alpha, c->vact_post.beta, c->vact_post.filt, s)))
-    return st;
-  return conv_post(a16, chl, B, L, chl, c->vpost_w, c->vpost_b, c->fade, c->nfade, wav, s);
+  for (int h = 0; h < NS; ++h) {
+    const int Bh = b0[h + 1] - b0[h];
+    const size_t ro = (size_t)b0[h] * T * maxLC;
+    if ((st = activation1d(XS + ro, a16 + ro, Bh, L, chl, chl, c->vact_post.alpha, c->vact_post.beta,
+                           c->vact_post.filt, ss[h])))
+      return st;
+    if ((st = conv_post(a16 + ro, chl, Bh, L, chl, c->vpost_w, c->vpost_b, c->fade, c->nfade,
+                        wav + (size_t)b0[h] * L, ss[h])))
+      return st;
+    if (NS > 1) {
+      SVC_HIP_CHECK(hipEventRecord(c->ev_join[h], ss[h]));
+      SVC_HIP_CHECK(hipStreamWaitEvent(s, c->ev_join[h], 0));
+    }
+  }
+  return SVC_OK;
 }
 
 // ---------------------------------------------------------------------------- op-level (tests)

@@ -147,6 +147,17 @@ def test_bigvgan(engine, cfg, states, golden):
     assert rel_l2(wav[0].cpu().numpy(), g["synth"]) < budget
 
 
+def test_vocoder_sub_streams_bit_identical(engine, monkeypatch):
+    """BigVGAN with utterance-aligned sub-batches on 1, 2 or 3 streams: identical waveforms."""
+    rng = np.random.default_rng(1)
+    x = dev(rng.uniform(-1, 1, (3, 40, 100)).astype(np.float32))
+    outs = {}
+    for ns in ("1", "2", "3"):
+        monkeypatch.setenv("SVC_VOCODER_STREAMS", ns)
+        outs[ns] = engine.bigvgan(x).cpu().numpy()
+    assert np.array_equal(outs["2"], outs["1"]) and np.array_equal(outs["3"], outs["1"])
+
+
 def test_bigvgan_batch_independence(engine, cfg):
     """Utterances in a batch never leak into each other through conv/activation halos."""
     rng = np.random.default_rng(0)
