@@ -1471,8 +1471,9 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
 
   // Utterance-aligned sub-batches on their own streams (as in svc_diffsvc_sample): every buffer is
   // time-major per utterance, so a sub-batch is a row offset into each; launches alternate between streams.
+  // Default 1: its launches are long (0.3-2 ms) and measured no faster split (SVC_VOCODER_STREAMS=2/3).
   const char* vs_env = getenv("SVC_VOCODER_STREAMS");
-  const int NS = std::max(1, std::min(std::min(vs_env ? atoi(vs_env) : 2, B), (int)kMaxSubStreams));
+  const int NS = std::max(1, std::min(std::min(vs_env ? atoi(vs_env) : 1, B), (int)kMaxSubStreams));
   if ((st = c->ensure_sub_streams(NS))) return st;
   SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
   int b0[kMaxSubStreams + 1];
