@@ -146,6 +146,30 @@ def map_whisper_features(raw_feats, target_len_in, fast_mapping=True):
     return down[:target_len]
 
 
+class MappingError(RuntimeError):
+    """utils/hubert.py:114-120: the reference calls exit() when the mapped length is off by more than 3."""
+
+
+def map_hubert_features(raw_feats, target_len):
+    """utils/hubert.py:83-134 (get_mapped_features, numpy f32). raw_feats [src_len, D] -> [target_len, D]:
+    the same 15:8 repeat/average as Whisper but without the 2812 cap or the fast_mapping truncation;
+    a shortfall of at most 3 rows is filled with the last mapped row, anything larger is an error."""
+    source_hop, target_hop = 480, 256
+    g = np.gcd(source_hop, target_hop)
+    source_hop //= g
+    target_hop //= g
+    source_len, width = raw_feats.shape
+    const = source_len * source_hop // target_hop * target_hop
+    up = np.repeat(raw_feats, source_hop, axis=0)
+    down = np.average(up[:const].reshape(-1, target_hop, width), axis=1)
+    err = abs(target_len - len(down))
+    if err > 3:
+        raise MappingError(f"content vector maps to {len(down)} frames, mel has {target_len}")
+    if len(down) < target_len:
+        down = np.concatenate([down, down[-1][None, :].repeat(err, axis=0)], axis=0)
+    return down[:target_len]
+
+
 # ----------------------------------------------------------------------------- F0 pitch shift, mel denorm
 
 

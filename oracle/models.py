@@ -1,6 +1,6 @@
 """ORACLE (test infrastructure only) — network restatement in torch-CPU float32 (functional form).
 
-Rows A6 (Whisper encoder), A10 (conditioner), A11 (DiffSVC), A12 (samplers), A14 (BigVGAN) of
+Rows A6 (Whisper encoder), A8 (HuBERT/ContentVec variant), A10 (conditioner), A11 (DiffSVC), A12 (samplers), A14 (BigVGAN) of
 SURVEY.md §8(a). Parameters are dicts in the reference's state_dict naming (see
 svc_inference_pipeline_amd/weights.py); values may be numpy or torch.
 """
@@ -48,6 +48,70 @@ def whisper_encoder(sd, mel, n_head):
     return F.layer_norm(x, (x.shape[-1],), _t(sd, "encoder.ln_post.weight"), _t(sd, "encoder.ln_post.bias"))
 
 
+# ============================================================================ HuBERT / ContentVec (variant, A8)
+
+
+def hubert_content(sd, wav16, output_layer=9):
+    """utils/hubert.py:31-47 (get_hubert_content): fairseq HubertModel.extract_features(source,
+    padding_mask=all-False, output_layer=9) then final_proj, returned here time-major [B, frames, final_dim].
+
+    fairseq is not installed and the reference pins no version; this restates its
+    published modules (fairseq/models/wav2vec/wav2vec2.py ConvFeatureExtractionModel mode "default",
+    TransformerEncoder + TransformerSentenceEncoderLayer with layer_norm_first=False;
+    fairseq/models/hubert/hubert.py HubertModel.forward_features / forward(features_only=True)):
+      conv_layers[0]: conv(1->C, k10 s5, no bias) -> Fp32GroupNorm(C, C) (per channel over time, eps 1e-5) -> GELU
+      conv_layers[1..6]: conv(k3/k2, s2, no bias) -> GELU
+      LayerNorm(C) -> post_extract_proj (C -> D)
+      x += GELU(SamePad(weight_norm(dim=2) grouped conv k=128, pad 64)(x)); LayerNorm(D)
+      layers 0..output_layer-1, post-LN: x = LN(x + MHA(x)); x = LN(x + fc2(GELU(fc1(x))))
+      q = (x Wq + bq) * dh^-1/2, softmax in f32.
+    Padding masks are all False (utils/hubert.py:37) so they drop out. wav16 f32 [B, N]."""
+    x = wav16.unsqueeze(1)
+    i = 0
+    while f"feature_extractor.conv_layers.{i}.0.weight" in sd:
+        w = _t(sd, f"feature_extractor.conv_layers.{i}.0.weight")
+        stride = 5 if i == 0 else 2
+        x = F.conv1d(x, w, stride=stride)
+        if i == 0:
+            x = F.group_norm(x, x.shape[1], _t(sd, "feature_extractor.conv_layers.0.2.weight"),
+                             _t(sd, "feature_extractor.conv_layers.0.2.bias"), eps=1e-5)
+        x = F.gelu(x)
+        i += 1
+    x = x.transpose(1, 2)
+    x = F.layer_norm(x, (x.shape[-1],), _t(sd, "layer_norm.weight"), _t(sd, "layer_norm.bias"))
+    x = F.linear(x, _t(sd, "post_extract_proj.weight"), _t(sd, "post_extract_proj.bias"))
+    # weight_norm(name="weight", dim=2): w = g * v / ||v|| with the norm over dims (0, 1) per tap
+    v = _t(sd, "encoder.pos_conv.0.weight_v")
+    g = _t(sd, "encoder.pos_conv.0.weight_g")
+    w = g * v / torch.sqrt((v * v).sum(dim=(0, 1), keepdim=True))
+    kp = v.shape[2]
+    groups = x.shape[-1] // v.shape[1]
+    xc = F.conv1d(x.transpose(1, 2), w, _t(sd, "encoder.pos_conv.0.bias"), padding=kp // 2, groups=groups)
+    if kp % 2 == 0:
+        xc = xc[:, :, :-1]  # SamePad
+    x = x + F.gelu(xc).transpose(1, 2)
+    D = x.shape[-1]
+    x = F.layer_norm(x, (D,), _t(sd, "encoder.layer_norm.weight"), _t(sd, "encoder.layer_norm.bias"))
+    H = D // 64
+    for li in range(output_layer):
+        p = f"encoder.layers.{li}."
+        B, L, _ = x.shape
+        q = F.linear(x, _t(sd, p + "self_attn.q_proj.weight"), _t(sd, p + "self_attn.q_proj.bias")) * (64 ** -0.5)
+        k = F.linear(x, _t(sd, p + "self_attn.k_proj.weight"), _t(sd, p + "self_attn.k_proj.bias"))
+        vv = F.linear(x, _t(sd, p + "self_attn.v_proj.weight"), _t(sd, p + "self_attn.v_proj.bias"))
+        q = q.view(B, L, H, 64).transpose(1, 2)
+        k = k.view(B, L, H, 64).transpose(1, 2)
+        vv = vv.view(B, L, H, 64).transpose(1, 2)
+        a = F.softmax((q @ k.transpose(-1, -2)).float(), dim=-1)
+        o = (a @ vv).transpose(1, 2).reshape(B, L, D)
+        x = x + F.linear(o, _t(sd, p + "self_attn.out_proj.weight"), _t(sd, p + "self_attn.out_proj.bias"))
+        x = F.layer_norm(x, (D,), _t(sd, p + "self_attn_layer_norm.weight"), _t(sd, p + "self_attn_layer_norm.bias"))
+        h = F.gelu(F.linear(x, _t(sd, p + "fc1.weight"), _t(sd, p + "fc1.bias")))
+        x = x + F.linear(h, _t(sd, p + "fc2.weight"), _t(sd, p + "fc2.bias"))
+        x = F.layer_norm(x, (D,), _t(sd, p + "final_layer_norm.weight"), _t(sd, p + "final_layer_norm.bias"))
+    return F.linear(x, _t(sd, "final_proj.weight"), _t(sd, "final_proj.bias"))
+
+
 # ============================================================================ conditioner
 
 
@@ -60,11 +124,14 @@ def conditioner(sd, content, f0, energy, singer, content_type="whisper"):
     """modules/encoder.py:165-201, merge_mode "add". content f32[B,T,D], f0 f64[B,T], energy f32[B,T],
     singer int[B,1]. Summation order: content, melody, loudness, singer (ModuleDict order)."""
     p = "0.registered_modules_dict."
-    c = F.linear(content, _t(sd, p + f"content_{content_type}.nn.weight"), _t(sd, p + f"content_{content_type}.nn.bias"))
+    if not isinstance(content, dict):  # one content type; a dict {type: f32[B,T,D_type]} sums several
+        content = {content_type: content}
+    cs = [F.linear(x, _t(sd, p + f"content_{ct}.nn.weight"), _t(sd, p + f"content_{ct}.nn.bias"))
+          for ct, x in content.items()]
     m = F.embedding(torch.bucketize(f0, _t(sd, p + "melody.melody_bins")), _t(sd, p + "melody.nn.weight"))
     l = F.embedding(torch.bucketize(energy, _t(sd, p + "loudness.energy_bins")), _t(sd, p + "loudness.nn.weight"))
-    s = F.embedding(singer, _t(sd, p + "singer.nn.weight")).expand(-1, c.shape[1], -1)
-    return torch.sum(torch.cat([o[None] for o in (c, m, l, s)], dim=0), dim=0)
+    s = F.embedding(singer, _t(sd, p + "singer.nn.weight")).expand(-1, cs[0].shape[1], -1)
+    return torch.sum(torch.cat([o[None] for o in (*cs, m, l, s)], dim=0), dim=0)
 
 
 # ============================================================================ DiffSVC epsilon predictor

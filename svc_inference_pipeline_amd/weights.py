@@ -7,6 +7,7 @@ parameters whose NAMES and SHAPES are exactly the reference's state_dict keys:
   mapper   : torch.nn.ModuleList([EncoderFramework, DiffSVC])   (utils/load_models.py:17-20)
   vocoder  : bigvgan.Generator                                   (modules/bigvgan.py:519-622)
   whisper  : Whisper.encoder (AudioEncoder)                      (utils/whisper_extractor/model.py:132-160)
+  hubert   : fairseq HubertModel (ContentVec)                     (utils/hubert.py:14-47)
 
 Random tensors come from numpy PCG64 keyed by (seed, crc32(name)), so any subset is reproducible
 independently of generation order. Model BUFFERS the reference builds at construction time
@@ -126,9 +127,9 @@ def make_mapper_state(mcfg, seed=0):
     constant; here it is random like every other layer."""
     sd = {}
     C = mcfg.residual_channels
-    ct = mcfg.content_feature[0]
     p = "0.registered_modules_dict."
-    _linear(sd, seed, p + f"content_{ct}.nn", mcfg.encoder_content_dim, mcfg.input_content_dim[ct])
+    for ct in mcfg.content_feature:  # one ContentEncoder per content type (modules/encoder.py:144-148)
+        _linear(sd, seed, p + f"content_{ct}.nn", mcfg.encoder_content_dim, mcfg.input_content_dim[ct])
     sd[p + "melody.melody_bins"] = melody_bins(mcfg.n_bins_melody).numpy()
     sd[p + "melody.nn.weight"] = _normal(seed, p + "melody.nn.weight", (mcfg.n_bins_melody, mcfg.encoder_melody_dim), 0.5)
     sd[p + "loudness.energy_bins"] = energy_bins(mcfg.n_bins_loudness).numpy()
@@ -229,6 +230,81 @@ def whisper_dims_from_state(sd):
     n_layer = 1 + max(int(k.split(".")[2]) for k in sd if k.startswith("encoder.blocks."))
     return dict(n_mels=sd["encoder.conv1.weight"].shape[1], n_audio_ctx=sd["encoder.positional_embedding"].shape[0],
                 n_audio_state=D, n_audio_head=D // 64, n_audio_layer=n_layer)
+
+
+HUBERT_DIMS = {
+    # fairseq HubertModel as ContentVec ships it (utils/hubert.py:14-28 loads it through
+    # fairseq.checkpoint_utils): conv extractor [(512,10,5)] + [(512,3,2)]*4 + [(512,2,2)]*2, 768-wide
+    # post-LN transformer (12 heads, FFN 3072), conv_pos 128 / 16 groups, final_proj 768 -> 256.
+    # utils/hubert.py:42 reads output_layer=9, so only layers 0..8 are evaluated.
+    "contentvec": dict(conv_dim=512, embed_dim=768, n_head=12, ffn_dim=3072, n_layer=12, final_dim=256,
+                       conv_pos=128, conv_pos_groups=16, output_layer=9),
+    "tiny-test": dict(conv_dim=64, embed_dim=128, n_head=2, ffn_dim=256, n_layer=3, final_dim=32,
+                      conv_pos=128, conv_pos_groups=16, output_layer=2),
+}
+HUBERT_CONV_LAYERS = [(10, 5)] + [(3, 2)] * 4 + [(2, 2)] * 2  # (kernel, stride) of the feature extractor
+
+
+def make_hubert_state(dims, seed=0):
+    """State dict of a fairseq HubertModel (ContentVec) with fairseq's own key names:
+    feature_extractor.conv_layers.{i}.0.weight (bias-free convs; layer 0 adds Fp32GroupNorm at .2),
+    layer_norm, post_extract_proj, encoder.pos_conv.0.{weight_g,weight_v,bias} (weight_norm over dim 2),
+    encoder.layer_norm, encoder.layers.{i}.{self_attn.{q,k,v,out}_proj, self_attn_layer_norm, fc1, fc2,
+    final_layer_norm}, final_proj. fairseq is not installed; names follow its published modules
+    (fairseq/models/wav2vec/wav2vec2.py ConvFeatureExtractionModel / TransformerEncoder,
+    fairseq/models/hubert/hubert.py HubertModel)."""
+    sd = {}
+    Cc, D, Fd = dims["conv_dim"], dims["embed_dim"], dims["ffn_dim"]
+    cin = 1
+    for i, (k, _s) in enumerate(HUBERT_CONV_LAYERS):
+        name = f"feature_extractor.conv_layers.{i}.0.weight"
+        sd[name] = _normal(seed, name, (Cc, cin, k), math.sqrt(2.0 / (cin * k)))
+        cin = Cc
+    for n in ("weight", "bias"):
+        name = f"feature_extractor.conv_layers.0.2.{n}"
+        sd[name] = _normal(seed, name, (Cc,), 0.05 if n == "weight" else 0.02, mean=1.0 if n == "weight" else 0.0)
+    sd["layer_norm.weight"] = _normal(seed, "layer_norm.weight", (Cc,), 0.05, mean=1.0)
+    sd["layer_norm.bias"] = _normal(seed, "layer_norm.bias", (Cc,), 0.02)
+    _linear(sd, seed, "post_extract_proj", D, Cc)
+    kp, G = dims["conv_pos"], dims["conv_pos_groups"]
+    v = _normal(seed, "encoder.pos_conv.0.weight_v", (D, D // G, kp), math.sqrt(4.0 / (kp * D)))
+    sd["encoder.pos_conv.0.weight_v"] = v
+    # weight_norm(dim=2): g has shape [1, 1, k]; start from ||v|| over dims (0, 1) scaled like a trained model
+    norm = np.sqrt((v.astype(np.float64) ** 2).sum(axis=(0, 1), keepdims=True))
+    sd["encoder.pos_conv.0.weight_g"] = (norm * _uniform(seed, "encoder.pos_conv.0.weight_g", (1, 1, kp), 0.5, 1.5)).astype(np.float32)
+    sd["encoder.pos_conv.0.bias"] = _normal(seed, "encoder.pos_conv.0.bias", (D,), 0.02)
+    sd["encoder.layer_norm.weight"] = _normal(seed, "encoder.layer_norm.weight", (D,), 0.05, mean=1.0)
+    sd["encoder.layer_norm.bias"] = _normal(seed, "encoder.layer_norm.bias", (D,), 0.02)
+    for i in range(dims["n_layer"]):
+        p = f"encoder.layers.{i}."
+        for proj in ("q_proj", "k_proj", "v_proj"):
+            _linear(sd, seed, p + "self_attn." + proj, D, D)
+        _linear(sd, seed, p + "self_attn.out_proj", D, D, gain=0.5)
+        for ln in ("self_attn_layer_norm", "final_layer_norm"):
+            sd[p + ln + ".weight"] = _normal(seed, p + ln + ".weight", (D,), 0.05, mean=1.0)
+            sd[p + ln + ".bias"] = _normal(seed, p + ln + ".bias", (D,), 0.02)
+        _linear(sd, seed, p + "fc1", Fd, D)
+        _linear(sd, seed, p + "fc2", D, Fd, gain=0.5)
+    _linear(sd, seed, "final_proj", dims["final_dim"], D)
+    return sd
+
+
+def hubert_dims_from_state(sd, output_layer=9):
+    Cc = sd["feature_extractor.conv_layers.0.0.weight"].shape[0]
+    D = sd["post_extract_proj.weight"].shape[0]
+    n_layer = 1 + max(int(k.split(".")[2]) for k in sd if k.startswith("encoder.layers."))
+    kp = sd["encoder.pos_conv.0.weight_v"].shape[2]
+    return dict(conv_dim=Cc, embed_dim=D, n_head=D // 64, ffn_dim=sd["encoder.layers.0.fc1.weight"].shape[0],
+                n_layer=n_layer, final_dim=sd["final_proj.weight"].shape[0], conv_pos=kp,
+                conv_pos_groups=D // sd["encoder.pos_conv.0.weight_v"].shape[1], output_layer=min(output_layer, n_layer))
+
+
+def hubert_frames(n_samples):
+    """Frames of the conv feature extractor for n 16 kHz samples (499 for 10 s)."""
+    t = n_samples
+    for k, s in HUBERT_CONV_LAYERS:
+        t = (t - k) // s + 1
+    return t
 
 
 # ----------------------------------------------------------------------------- real checkpoints (F2)

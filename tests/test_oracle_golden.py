@@ -155,3 +155,45 @@ def test_format_golden(golden):
     w = np.linspace(-0.5, 0.2, 5000).astype(np.float32)
     pcm = OF.save_audio_pcm16(w, 24000)
     assert len(pcm) == 5000 + 2400 and pcm.min() == -29491
+
+
+# ---------------------------------------------------------------------------- A8: HuBERT / ContentVec variant
+def test_hubert_map_reference(golden):
+    """utils/hubert.py:83-134 restated; fixtures from the reference's own function."""
+    g = golden("hubert_map")
+    for s, t in g["cases"]:
+        out = OF.map_hubert_features(g[f"raw_{s}_{t}"], int(t))
+        ref = g[f"out_{s}_{t}"]
+        assert out.shape == ref.shape == (t, 24)
+        assert np.array_equal(out, ref), (s, t)
+    for s, t, exited in g["exits"]:
+        assert exited == 1
+        with pytest.raises(OF.MappingError):
+            OF.map_hubert_features(np.zeros((int(s), 4), np.float32), int(t))
+
+
+def test_hubert_encoder_tiny(golden):
+    """oracle.models.hubert_content vs transformers.HubertModel (independent implementation of fairseq's
+    HuBERT; fairseq itself is absent and unpinned — SURVEY.md §8c)."""
+    g = golden("hubert_encoder_tiny")
+    dims = W.HUBERT_DIMS["tiny-test"]
+    sd = W.make_hubert_state(dims, seed=0)
+    with torch.no_grad():
+        feats = OM.hubert_content(sd, torch.from_numpy(g["wav16"]), dims["output_layer"])
+    assert feats.shape[1] == W.hubert_frames(g["wav16"].shape[1])
+    np.testing.assert_allclose(feats.numpy(), g["feats"], rtol=0, atol=1e-5)
+
+
+def test_conditioner_multi_content(golden):
+    """EncoderFramework with content_feature ["whisper", "contentvec"] and ["contentvec"] (reference fixtures)."""
+    g = golden("conditioner_multi_content")
+    for tag, types_ in (("multi", ["whisper", "contentvec"]), ("cv", ["contentvec"])):
+        mcfg = C.load_config().mapper
+        mcfg.content_feature = types_
+        mcfg.input_content_dim["whisper"] = 128
+        mcfg.input_content_dim["contentvec"] = 32
+        sd = W.make_mapper_state(mcfg, seed=0)
+        content = {ct: torch.from_numpy(g[f"content_{ct}"]) for ct in types_}
+        cond = OM.conditioner(sd, content, torch.from_numpy(g["f0"]), torch.from_numpy(g["energy"]),
+                              torch.from_numpy(g["singer"]).long())
+        np.testing.assert_allclose(cond.numpy(), g[f"cond_{tag}"], rtol=0, atol=2e-5)
