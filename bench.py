@@ -38,25 +38,50 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def synth_inputs(uids, seconds):
+def synth_inputs(uids, seconds, float16k=False):
+    """24 kHz f32 clips and their 16 kHz copies: int16-quantised for Whisper (ffmpeg s16le,
+    utils/whisper_extractor/audio.py:41-49), float for ContentVec (librosa, utils/hubert.py:55)."""
     from svc_inference_pipeline_amd.synth import synth_clip, synth_clip_16k_quantised
     w24 = np.stack([synth_clip(int(u), seconds, 24000) for u in uids])
-    w16 = np.stack([synth_clip_16k_quantised(int(u), seconds) for u in uids])
+    if float16k:
+        w16 = np.stack([synth_clip(int(u), seconds, 16000) for u in uids]).astype(np.float32)
+    else:
+        w16 = np.stack([synth_clip_16k_quantised(int(u), seconds) for u in uids])
     return w24, w16
 
 
-def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads):
+def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads, hs=None, fast=True):
     """The oracle (CPU restatement of the reference path, torch-CPU fp32) on ONE clip of the same
     workload, timed on this host: mel/energy, F0, pitch shift, Whisper-medium, map, conditioner,
     PLMS (speedup 10 = 101 denoiser calls), de-normalisation, BigVGAN, fade."""
     from oracle import pipeline as OP
     torch.set_num_threads(threads)
-    w24, w16 = synth_inputs([0], seconds)
+    w24, w16 = synth_inputs([0], seconds, float16k=hs is not None)
+    if fast:
+        t0 = time.time()
+        OP.convert(cfg, ws, ms, vs, w24[0], w16[0], singer=1, speedup=speedup, seed=0, hs=hs)
+        dt = time.time() - t0
+        return {"value": round(seconds / dt, 4), "unit": "audio-s/s", "cores": threads, "kind": "port",
+                "sample": f"1 x {seconds:g} s clip, full oracle path (PLMS speedup {speedup}), torch-CPU fp32, "
+                          f"{threads} threads, {dt:.1f} s"}
+    # DDPM-1000 on the CPU is ~2 min per clip: time the path once with PLMS speedup 250 (5 denoiser calls) and
+    # 10 more denoiser calls alone, then extrapolate the sampler to 1000 calls.
+    from oracle import models as OM
     t0 = time.time()
-    OP.convert(cfg, ws, ms, vs, w24[0], w16[0], singer=1, speedup=speedup, seed=0)
-    dt = time.time() - t0
+    OP.convert(cfg, ws, ms, vs, w24[0], w16[0], singer=1, speedup=250, seed=0, hs=hs)
+    t_path = time.time() - t0
+    T = (w24.shape[1] + 768 - 1024) // 256 + 1
+    cond = torch.randn(1, T, cfg.mapper.residual_channels)
+    x = torch.randn(1, T, cfg.mapper.n_mel)
+    table = W.step_embedding_table(1000)
+    t0 = time.time()
+    for i in range(10):
+        OM.diffsvc_forward(ms, cfg.mapper, x, cond, torch.tensor([999 - i]), table)
+    t_call = (time.time() - t0) / 10
+    dt = t_path + (1000 - 5) * t_call
     return {"value": round(seconds / dt, 4), "unit": "audio-s/s", "cores": threads, "kind": "port",
-            "sample": f"1 x {seconds:g} s clip, full oracle path (PLMS speedup {speedup}), torch-CPU fp32, {threads} threads, {dt:.1f} s"}
+            "sample": f"1 x {seconds:g} s clip, oracle path with 5 denoiser calls ({t_path:.1f} s) + 995 x "
+                      f"{t_call * 1e3:.0f} ms timed denoiser calls (DDPM-1000 extrapolated), torch-CPU fp32, {threads} threads"}
 
 
 def family(prof):
@@ -80,20 +105,31 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--content", choices=["whisper", "contentvec"], default="whisper",
+                    help="content encoder (BASELINE config 5: contentvec = the HuBERT/ContentVec variant)")
+    ap.add_argument("--sampler", choices=["plms", "ddpm"], default="plms",
+                    help="plms = the reference's fast_inference PLMS (speedup --speedup); ddpm = 1000-step DDPM")
     args = ap.parse_args()
 
     dist = DistContext.from_env()
     torch.cuda.set_device(dist.local_rank)
     cfg = C.load_config()
     t_setup = time.time()
-    ws = W.make_whisper_state(W.WHISPER_DIMS["medium"], seed=0)
+    ws = hs = None
+    if args.content == "whisper":
+        ws = W.make_whisper_state(W.WHISPER_DIMS["medium"], seed=0)
+    else:
+        cfg.mapper.content_feature = ["contentvec"]
+        cfg.mapper.input_content_dim["contentvec"] = W.HUBERT_DIMS["contentvec"]["final_dim"]
+        hs = W.make_hubert_state(W.HUBERT_DIMS["contentvec"], seed=0)
     ms = W.make_mapper_state(cfg.mapper, seed=0)
     vs = W.make_vocoder_state(cfg.vocoder, seed=0)
-    eng = SVCEngine(cfg, dist.local_rank, whisper_state=ws, mapper_state=ms, vocoder_state=vs)
+    eng = SVCEngine(cfg, dist.local_rank, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs)
+    fast = args.sampler == "plms"
     pipe = SVCPipeline(eng)
     B = args.batch
     uids = np.arange(dist.rank * B, (dist.rank + 1) * B)
-    w24, w16 = synth_inputs(uids, args.seconds)
+    w24, w16 = synth_inputs(uids, args.seconds, float16k=args.content == "contentvec")
     d24 = torch.from_numpy(w24).cuda()
     d16 = torch.from_numpy(w16).cuda()
     singer = torch.from_numpy((uids % 5).astype(np.int32)).cuda()
@@ -101,7 +137,8 @@ def main():
     log(f"rank {dist.rank}/{dist.world}: setup {time.time() - t_setup:.1f}s, weights {eng.memory()[0] / 1e9:.2f} GB")
 
     def step():
-        res = pipe.convert(d24, d16, singer, fast_inference=True, speedup=args.speedup, seed=1234, utt_ids=utt)
+        res = pipe.convert(d24, d16, singer, fast_inference=fast, speedup=args.speedup, seed=1234, utt_ids=utt,
+                           wav16_float=d16 if hs is not None else None)
         return dist.gather_waveforms(res.wav)
 
     # Warmup. The last warmup step runs with every launch profiled (HIP events around each kernel): that
@@ -221,15 +258,17 @@ def main():
     cpu = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, 1 clip)...")
-        cpu = cpu_baseline(cfg, ws, ms, vs, args.seconds, args.speedup, args.cpu_threads)
+        cpu = cpu_baseline(cfg, ws, ms, vs, args.seconds, args.speedup, args.cpu_threads, hs=hs, fast=fast)
     if dist.rank == 0:
         line = {
             "metric": "converted audio sec/sec (RTF^-1) end-to-end, 10 s clips",
             "value": round(value, 2), "unit": "audio-s/s", "n_gpus": dist.world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
-            "config": {"workload": f"batch={B}/GPU x {args.seconds:g} s synthetic clips, Whisper-medium + PLMS-100 "
-                                   f"DiffSVC (speedup {args.speedup}) + BigVGAN, fp16 MFMA operands / fp32 accumulate",
+            "config": {"workload": f"batch={B}/GPU x {args.seconds:g} s synthetic clips, "
+                                   + ("Whisper-medium" if hs is None else "HuBERT/ContentVec (layer 9)")
+                                   + (f" + PLMS-100 DiffSVC (speedup {args.speedup})" if fast else " + DDPM-1000 DiffSVC")
+                                   + " + BigVGAN, fp16 MFMA operands / fp32 accumulate",
                        "global_batch": dist.world * B, "seq_len_frames": int((d24.shape[1] + 768 - 1024) // 256 + 1),
                        "parallelism": f"dp{dist.world} (per-utterance shards, RCCL gather)"},
             "roofline": roof, "cpu_baseline": cpu,

@@ -72,7 +72,27 @@ svc_status svc_whisper_encode(svc_ctx* ctx, const float* wav16k, int B, int64_t 
 svc_status svc_map_content(svc_ctx* ctx, const float* feats, int B, int src_rows, int T, int D, void* content_f16,
                            void* stream);
 
-/* A10: content f16 [B*T][D], f0 f64 [B*T], energy f32 [B*T], singer int32 [B] -> cond f32 [B*T][384]. */
+/* A7/A8 mapping with an output row stride: feats [B*src_rows][D] f32 -> out f16 [B*T] rows of ld_out halves
+   (columns 0..D-1 written; pass a column-offset pointer to fill one content type of a concatenated buffer).
+   mode 0: Whisper rule (utils/whisper.py:31-81, T <= 2812, source truncated to T*8/15+1 rows);
+   mode 1: HuBERT rule (utils/hubert.py:83-134, all src_rows frames, <= 3 missing rows repeat the last mapped
+   row; |T - src_rows*15/8| > 3 is SVC_ERR_INVALID where the reference calls exit()). */
+svc_status svc_map_content_ex(svc_ctx* ctx, const float* feats, int B, int src_rows, int T, int D, int mode,
+                              void* out_f16, int ld_out, void* stream);
+
+/* A8 (variant): HuBERT/ContentVec content encoder, replacing utils/hubert.py:31-47 get_hubert_content
+   (fairseq HubertModel.extract_features(output_layer = config "hubert.output_layer", default 9) + final_proj).
+   wav16k [B][n_samples] f32 (librosa-loaded 16 kHz float audio, utils/hubert.py:55) -> feats
+   [B*svc_hubert_frames(n)][final_dim] f32. Parameters are added as "hubert." + fairseq state_dict keys. */
+svc_status svc_hubert_encode(svc_ctx* ctx, const float* wav16k, int B, int64_t n_samples, float* feats, void* stream);
+/* frames of the conv feature extractor for n samples (499 for 160 000) */
+int64_t svc_hubert_frames(int64_t n_samples);
+svc_status svc_hubert_dims(svc_ctx* ctx, int* final_dim, int* embed_dim);
+
+/* A10: content f16 [B*T][D], f0 f64 [B*T], energy f32 [B*T], singer int32 [B] -> cond f32 [B*T][384].
+   With several content types (config mapper.content_feature) D is the sum of their widths and the
+   content columns are concatenated in ascending type-name order (e.g. contentvec | whisper); the
+   per-type Linear layers (modules/encoder.py:144-148) are summed as one GEMM. */
 svc_status svc_condition(svc_ctx* ctx, const void* content_f16, const double* f0, const float* energy,
                          const int32_t* singer, int B, int T, float* cond, void* stream);
 

@@ -93,7 +93,8 @@ def hubert_content(sd, wav16, output_layer=9):
     D = x.shape[-1]
     x = F.layer_norm(x, (D,), _t(sd, "encoder.layer_norm.weight"), _t(sd, "encoder.layer_norm.bias"))
     H = D // 64
-    for li in range(output_layer):
+    n_layers = 1 + max(int(k.split(".")[2]) for k in sd if k.startswith("encoder.layers."))
+    for li in range(min(output_layer, n_layers)):  # fairseq runs every layer when output_layer exceeds them
         p = f"encoder.layers.{li}."
         B, L, _ = x.shape
         q = F.linear(x, _t(sd, p + "self_attn.q_proj.weight"), _t(sd, p + "self_attn.q_proj.bias")) * (64 ** -0.5)

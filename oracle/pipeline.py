@@ -1,7 +1,7 @@
 """ORACLE (test infrastructure only) — the whole infer.py path on the CPU (torch-CPU fp32 / numpy f64),
 one utterance: the CPU baseline `bench.py` times, and the end-to-end reference for parity tests.
 
-infer.py:53 features -> :59 pitch shift -> :64 Whisper content -> :79 DiffSVC sampler ->
+infer.py:53 features -> :59 pitch shift -> :64 Whisper (or :65 ContentVec) content -> :79 DiffSVC sampler ->
 :80 de-normalisation -> :86 BigVGAN synthesis (fade). Pitch: oracle.praat_ac (parity unpinned).
 """
 import numpy as np
@@ -40,17 +40,30 @@ def whisper_content(ws, wav16, T):
     return np.concatenate(parts, 0)
 
 
-def convert(cfg, ws, ms, vs, wav24, wav16, singer, speedup=10, seed=0, fast_inference=True, x_T=None, f0=None):
-    """Returns dict(wav f32[T*hop], mel, f0, x0)."""
+def hubert_content(hs, wav16, T, output_layer=9):
+    """utils/hubert.py:137-143 (contentVec_feature_extractor) for one utterance -> f32 [T, final_dim]."""
+    feats = OM.hubert_content(hs, torch.from_numpy(np.asarray(wav16, np.float32))[None], output_layer)[0].numpy()
+    return OF.map_hubert_features(feats, T)
+
+
+def convert(cfg, ws, ms, vs, wav24, wav16, singer, speedup=10, seed=0, fast_inference=True, x_T=None, f0=None,
+            hs=None, wav16_float=None, hubert_output_layer=9):
+    """Returns dict(wav f32[T*hop], mel, f0, x0). Content types follow cfg.mapper.content_feature: "whisper"
+    uses ws on wav16, "contentvec" uses the HuBERT state hs on wav16_float (default wav16)."""
     mel = OF.mel_spectrogram(torch.from_numpy(np.asarray(wav24, np.float32))[None], cfg)  # [1,100,T]
     energy = OF.energy_from_mel(mel)
     T = mel.shape[-1]
     if f0 is None:
         f0 = PA.f0_features(wav24, T, fs=cfg.fs, hop=cfg.hop_length, floor=cfg.f0_min, ceiling=cfg.f0_max)
     f0 = OF.pitch_shift(f0, C.load_stats(cfg)["target_f0_median"])
-    content = whisper_content(ws, wav16, T)
-    cond = OM.conditioner(ms, torch.from_numpy(content)[None], torch.from_numpy(f0)[None], energy,
-                          torch.tensor([[int(singer)]]))
+    content = {}
+    for ct in cfg.mapper.content_feature:
+        if ct == "whisper":
+            c = whisper_content(ws, wav16, T)
+        else:
+            c = hubert_content(hs, wav16 if wav16_float is None else wav16_float, T, hubert_output_layer)
+        content[ct] = torch.from_numpy(np.asarray(c, np.float32))[None]
+    cond = OM.conditioner(ms, content, torch.from_numpy(f0)[None], energy, torch.tensor([[int(singer)]]))
     table = W.step_embedding_table(len(C.noise_schedule(cfg.mapper)))
     consts = OM.schedule_constants(C.noise_schedule(cfg.mapper))
     den = lambda x, t: OM.diffsvc_forward(ms, cfg.mapper, x, cond, t, table)

@@ -2,6 +2,7 @@
 // conditioner bucketize,
 // sampler updates (DDPM / PLMS), mel de-normalisation, conv_post+tanh+fade.
 // All tensors are time-major [rows = b*T + t][channels].
+#include <cstdlib>
 #include "common.h"
 
 namespace svc {
@@ -134,22 +135,37 @@ int denorm_mel(const float* x, f16* y, float* y32, int ldy, int rows, int C, con
 // utils/whisper.py:31-81: 15:8 repeat/average. Row j of the output averages the 8 repeated rows
 // 8j..8j+7 of np.repeat(raw, 15): source rows (8j+i)//15, summed sequentially in f32 then /8.
 __global__ void content_map_kernel(const float* __restrict__ src, int src_rows_per_utt, int ld_src,
-                                   f16* __restrict__ dst, int ld_dst, int T, int D) {
-  const int j = blockIdx.x;  // output frame
+                                   f16* __restrict__ dst, int ld_dst, int T, int D, int n_down) {
+  const int jo = blockIdx.x;  // output frame
+  const int j = min(jo, n_down - 1);  // HuBERT: frames past the mapped length repeat the last one
   const int b = blockIdx.y;
   const float* sb = src + (int64_t)b * src_rows_per_utt * ld_src;
   for (int c = threadIdx.x; c < D; c += blockDim.x) {
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc += sb[(int64_t)((8 * j + i) / 15) * ld_src + c];
-    dst[((int64_t)b * T + j) * ld_dst + c] = (f16)(acc / 8.0f);
+    dst[((int64_t)b * T + jo) * ld_dst + c] = (f16)(acc / 8.0f);
   }
 }
 
 int content_map(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst, hipStream_t s) {
   // the reference caps the target at 2812 frames (utils/whisper.py:56); longer clips are chunked by the host
   SVC_REQUIRE(T >= 1 && T <= 2812 && (T * 8 / 15 + 1) <= src_rows, "content_map: T=%d src_rows=%d", T, src_rows);
-  hipLaunchKernelGGL(content_map_kernel, dim3(T, B), dim3(256), 0, s, src, src_rows, ld_src, dst, ld_dst, T, D);
+  hipLaunchKernelGGL(content_map_kernel, dim3(T, B), dim3(256), 0, s, src, src_rows, ld_src, dst, ld_dst, T, D, T);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+// utils/hubert.py:83-134 (get_mapped_features): the same 15:8 average over all src_rows frames, no cap;
+// n_down = src_rows*15//8 mapped frames, at most 3 missing frames repeat the last one, and a larger
+// mismatch is an error (the reference calls exit()).
+int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
+                       hipStream_t s) {
+  const int n_down = (int)((int64_t)src_rows * 15 / 8);
+  SVC_REQUIRE(T >= 1 && src_rows >= 1 && n_down >= 1 && std::abs(T - n_down) <= 3,
+              "content_map_hubert: %d content frames map to %d rows but T=%d (|diff| > 3; utils/hubert.py:114-120)",
+              src_rows, n_down, T);
+  hipLaunchKernelGGL(content_map_kernel, dim3(T, B), dim3(256), 0, s, src, src_rows, ld_src, dst, ld_dst, T, D, n_down);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

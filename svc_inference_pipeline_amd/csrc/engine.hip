@@ -112,6 +112,13 @@ int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
+int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
+                       hipStream_t s);
+int hubert_frames5(const float* wav, int B, int64_t n, f16* out, hipStream_t s);
+int groupnorm_gelu(const float* x, int B, int T, int C, const float* gamma, const float* beta, double* part,
+                   int max_chunks, float2* ss, f16* y, hipStream_t s);
+int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f16* y16, int rows, int D,
+                   hipStream_t s);
 int pack_qkv(const float* q, const float* k, const float* v, f16* qkv, int64_t rows, int D, float scale, hipStream_t s);
 int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double time_step, double floor_hz,
                 double ceiling_hz, double voicing_threshold, int T, double* f0_out, void* workspace, size_t ws_bytes,
@@ -204,6 +211,11 @@ struct WBlock {
   PackedGemm qkv, out, fc1, fc2;
 };
 
+struct HBlock {  // post-LN fairseq TransformerSentenceEncoderLayer
+  float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
+  PackedGemm qkv, out, fc1, fc2;
+};
+
 struct ActP {
   float *alpha, *beta, *filt;
 };
@@ -241,6 +253,15 @@ struct svc_ctx {
   PackedGemm wconv1, wconv2;
   float *wpos = nullptr, *wlnp_g = nullptr, *wlnp_b = nullptr;
   std::vector<WBlock> wblocks;
+  // hubert / contentvec (A8)
+  bool has_hubert = false;
+  int hC = 512, hD = 768, hH = 12, hLayers = 9, hFinal = 256, hPosK = 128, hPosG = 16;
+  std::vector<PackedGemm> hconv;    // feature extractor conv_layers 0..6 (layer 0 as a 2-tap GEMM over 5-sample rows)
+  std::vector<int> hconv_k, hconv_s;
+  float *hgn_g = nullptr, *hgn_b = nullptr, *hln_g = nullptr, *hln_b = nullptr, *henc_ln_g = nullptr, *henc_ln_b = nullptr;
+  PackedGemm hproj, hfinal;
+  std::vector<PackedGemm> hpos;     // one GEMM per pos_conv group
+  std::vector<HBlock> hblocks;
   // mapper
   bool has_mapper = false;
   int C = 384, n_mel = 100, n_layers = 20, dil_cycle = 4, steps = 1000, content_dim = 1024, n_bins = 256;
@@ -534,6 +555,124 @@ int build_whisper(svc_ctx* c) {
   return SVC_OK;
 }
 
+// ---------------------------------------------------------------------------- finalize: hubert (A8)
+// fairseq HubertModel (ContentVec) as utils/hubert.py:14-47 drives it; parameter names are fairseq's.
+int build_hubert(svc_ctx* c) {
+  GETP(c0, "hubert.feature_extractor.conv_layers.0.0.weight", -1, 1, 10);
+  const int Cc = (int)c0->shape[0];
+  GETP(pw, "hubert.post_extract_proj.weight", -1, Cc);
+  const int D = (int)pw->shape[0];
+  SVC_REQUIRE(D % 64 == 0 && D <= 1024 && Cc % 64 == 0 && Cc <= 1024, "hubert: embed %d / conv dim %d", D, Cc);
+  c->hC = Cc;
+  c->hD = D;
+  c->hH = D / 64;
+  int L = 0;
+  while (c->params.count("hubert.encoder.layers." + std::to_string(L) + ".fc1.weight")) ++L;
+  const int want = (int)cfgv(c, "hubert.output_layer", 9);
+  SVC_REQUIRE(want >= 1 && L >= 1, "hubert: output_layer %d, %d layers", want, L);
+  c->hLayers = std::min(want, L);  // fairseq's TransformerEncoder runs every layer when output_layer exceeds them
+  int st;
+  // conv_layers[0]: W0[n][0][tap*5 + j] -> packed K index tap*8 + j over rows of 5 samples
+  c->hconv.assign(7, PackedGemm());
+  c->hconv_k = {10, 3, 3, 3, 3, 2, 2};
+  c->hconv_s = {5, 2, 2, 2, 2, 2, 2};
+  st = pack_gemm(
+      c, c->hconv[0], Cc, 5, 8, 2, [&](int n, int ci, int t) { return c0->host[(int64_t)n * 10 + t * 5 + ci]; },
+      [&](int) { return 0.0f; });
+  if (st) return st;
+  c->hconv[0].tap_mul = 1;
+  c->hconv[0].tap_add = 0;
+  c->hconv[0].istride = 1;
+  for (int i = 1; i < 7; ++i) {
+    GETP(w, "hubert.feature_extractor.conv_layers." + std::to_string(i) + ".0.weight", Cc, Cc, c->hconv_k[i]);
+    if ((st = pack_conv1d(c, c->hconv[i], w->host, nullptr, Cc, Cc, c->hconv_k[i], Cc, 1, 0, 2))) return st;
+  }
+  GETP(gng, "hubert.feature_extractor.conv_layers.0.2.weight", Cc);
+  GETP(gnb, "hubert.feature_extractor.conv_layers.0.2.bias", Cc);
+  GETP(lng, "hubert.layer_norm.weight", Cc);
+  GETP(lnb, "hubert.layer_norm.bias", Cc);
+  GETP(pb, "hubert.post_extract_proj.bias", D);
+  if ((st = upload_param(c, gng, &c->hgn_g)) || (st = upload_param(c, gnb, &c->hgn_b)) ||
+      (st = upload_param(c, lng, &c->hln_g)) || (st = upload_param(c, lnb, &c->hln_b)))
+    return st;
+  if ((st = pack_conv1d(c, c->hproj, pw->host, pb->host, D, Cc, 1, Cc, 1, 0, 1))) return st;
+  // pos_conv: weight_norm(dim=2) -> w[o][i][k] = g[k] * v[o][i][k] / ||v[:, :, k]||; one GEMM per group
+  GETP(pv, "hubert.encoder.pos_conv.0.weight_v", D, -1, -1);
+  const int Cg = (int)pv->shape[1], kp = (int)pv->shape[2];
+  GETP(pg, "hubert.encoder.pos_conv.0.weight_g", 1, 1, kp);
+  GETP(pcb, "hubert.encoder.pos_conv.0.bias", D);
+  SVC_REQUIRE(D % Cg == 0 && Cg % 8 == 0 && kp % 2 == 0, "hubert: pos_conv groups of %d, k=%d", Cg, kp);
+  c->hPosK = kp;
+  c->hPosG = D / Cg;
+  std::vector<double> kscale(kp);
+  for (int k = 0; k < kp; ++k) {
+    double acc = 0;
+    for (int64_t oi = 0; oi < (int64_t)D * Cg; ++oi) {
+      const double v = pv->host[oi * kp + k];
+      acc += v * v;
+    }
+    kscale[k] = (double)pg->host[k] / sqrt(acc);
+  }
+  c->hpos.assign(c->hPosG, PackedGemm());
+  for (int gi = 0; gi < c->hPosG; ++gi) {
+    st = pack_gemm(
+        c, c->hpos[gi], Cg, Cg, Cg, kp,
+        [&](int n, int ci, int t) {
+          return (float)((double)pv->host[((int64_t)(gi * Cg + n) * Cg + ci) * kp + t] * kscale[t]);
+        },
+        [&](int n) { return pcb->host[gi * Cg + n]; });
+    if (st) return st;
+    c->hpos[gi].tap_mul = 1;
+    c->hpos[gi].tap_add = -kp / 2;  // padding k/2, SamePad drops the extra last frame
+    c->hpos[gi].istride = 1;
+  }
+  GETP(elg, "hubert.encoder.layer_norm.weight", D);
+  GETP(elb, "hubert.encoder.layer_norm.bias", D);
+  if ((st = upload_param(c, elg, &c->henc_ln_g)) || (st = upload_param(c, elb, &c->henc_ln_b))) return st;
+  c->hblocks.resize(c->hLayers);
+  for (int i = 0; i < c->hLayers; ++i) {
+    const std::string p = "hubert.encoder.layers." + std::to_string(i) + ".";
+    HBlock& b = c->hblocks[i];
+    GETP(qw, p + "self_attn.q_proj.weight", D, D);
+    GETP(qb, p + "self_attn.q_proj.bias", D);
+    GETP(kw, p + "self_attn.k_proj.weight", D, D);
+    GETP(kb, p + "self_attn.k_proj.bias", D);
+    GETP(vw, p + "self_attn.v_proj.weight", D, D);
+    GETP(vb, p + "self_attn.v_proj.bias", D);
+    GETP(ow, p + "self_attn.out_proj.weight", D, D);
+    GETP(ob, p + "self_attn.out_proj.bias", D);
+    GETP(l1g, p + "self_attn_layer_norm.weight", D);
+    GETP(l1b, p + "self_attn_layer_norm.bias", D);
+    GETP(l2g, p + "final_layer_norm.weight", D);
+    GETP(l2b, p + "final_layer_norm.bias", D);
+    GETP(f1w, p + "fc1.weight", -1, D);
+    const int Fd = (int)f1w->shape[0];
+    GETP(f1b, p + "fc1.bias", Fd);
+    GETP(f2w, p + "fc2.weight", D, Fd);
+    GETP(f2b, p + "fc2.bias", D);
+    st = pack_gemm(
+        c, b.qkv, 3 * D, D, D, 1,
+        [&](int n, int ci, int) {
+          const Param* w = n < D ? qw : (n < 2 * D ? kw : vw);
+          return w->host[(int64_t)(n % D) * D + ci];
+        },
+        [&](int n) { return n < D ? qb->host[n] : (n < 2 * D ? kb->host[n - D] : vb->host[n - 2 * D]); });
+    if (st) return st;
+    if ((st = pack_conv1d(c, b.out, ow->host, ob->host, D, D, 1, D, 1, 0, 1))) return st;
+    if ((st = pack_conv1d(c, b.fc1, f1w->host, f1b->host, Fd, D, 1, D, 1, 0, 1))) return st;
+    if ((st = pack_conv1d(c, b.fc2, f2w->host, f2b->host, D, Fd, 1, (int)round_up(Fd, 8), 1, 0, 1))) return st;
+    if ((st = upload_param(c, l1g, &b.ln1_g)) || (st = upload_param(c, l1b, &b.ln1_b)) ||
+        (st = upload_param(c, l2g, &b.ln2_g)) || (st = upload_param(c, l2b, &b.ln2_b)))
+      return st;
+  }
+  GETP(fw, "hubert.final_proj.weight", -1, D);
+  c->hFinal = (int)fw->shape[0];
+  GETP(fb, "hubert.final_proj.bias", c->hFinal);
+  if ((st = pack_conv1d(c, c->hfinal, fw->host, fb->host, c->hFinal, D, 1, D, 1, 0, 1))) return st;
+  c->has_hubert = true;
+  return SVC_OK;
+}
+
 // ---------------------------------------------------------------------------- finalize: mapper
 int build_mapper(svc_ctx* c) {
   const int C = (int)cfgv(c, "mapper.residual_channels", 384);
@@ -550,9 +689,28 @@ int build_mapper(svc_ctx* c) {
     return SVC_ERR_INVALID;
   }
   const std::string p = "mapper.0.registered_modules_dict.";
-  GETP(cw, p + "content_whisper.nn.weight", C, -1);
-  GETP(cb, p + "content_whisper.nn.bias", C);
-  c->content_dim = (int)cw->shape[1];
+  // One ContentEncoder Linear per content type (modules/encoder.py:144-148), summed with the other encoders:
+  // packed as ONE GEMM over the content types' features concatenated along K in ascending name order
+  // (the order of this map), with the biases summed.
+  std::vector<const Param*> cws, cbs;
+  {
+    const std::string pre = p + "content_", suf = ".nn.weight";
+    for (auto& kv : c->params) {
+      const std::string& k = kv.first;
+      if (k.rfind(pre, 0) == 0 && k.size() > pre.size() + suf.size() && k.compare(k.size() - suf.size(), suf.size(), suf) == 0) {
+        const std::string ct = k.substr(pre.size(), k.size() - pre.size() - suf.size());
+        GETP(w_, k, C, -1);
+        GETP(b_, p + "content_" + ct + ".nn.bias", C);
+        SVC_REQUIRE(w_->shape[1] % 8 == 0, "mapper: content_%s width %lld not a multiple of 8", ct.c_str(),
+                    (long long)w_->shape[1]);
+        cws.push_back(w_);
+        cbs.push_back(b_);
+      }
+    }
+  }
+  SVC_REQUIRE(!cws.empty(), "missing parameter 'mapper.0.registered_modules_dict.content_<type>.nn.weight'");
+  c->content_dim = 0;
+  for (auto* w_ : cws) c->content_dim += (int)w_->shape[1];
   GETP(mb, p + "melody.melody_bins", -1);
   GETP(me, p + "melody.nn.weight", -1, C);
   GETP(eb, p + "loudness.energy_bins", mb->shape[0]);
@@ -564,8 +722,22 @@ int build_mapper(svc_ctx* c) {
     return SVC_ERR_INVALID;
   }
   int st;
-  if ((st = pack_conv1d(c, c->content_lin, cw->host, cb->host, C, c->content_dim, 1, c->content_dim, 1, 0, 1)))
-    return st;
+  st = pack_gemm(
+      c, c->content_lin, C, c->content_dim, c->content_dim, 1,
+      [&](int n, int ci, int) {
+        for (auto* w_ : cws) {
+          const int d = (int)w_->shape[1];
+          if (ci < d) return w_->host[(int64_t)n * d + ci];
+          ci -= d;
+        }
+        return 0.0f;
+      },
+      [&](int n) {
+        float b = 0.0f;
+        for (auto* b_ : cbs) b += b_->host[n];
+        return b;
+      });
+  if (st) return st;
   if ((st = upload_param(c, mb, &c->mbins)) || (st = upload_param(c, eb, &c->ebins)) ||
       (st = upload_param(c, me, &c->emb_m)) || (st = upload_param(c, le, &c->emb_l)) ||
       (st = upload_param(c, se, &c->emb_s)))
@@ -892,13 +1064,15 @@ svc_status svc_ctx_finalize(svc_ctx* c) {
   SVC_HIP_CHECK(hipSetDevice(c->device));
   int st;
   if ((st = build_features(c))) return st;
-  bool any_w = false, any_m = false, any_v = false;
+  bool any_w = false, any_m = false, any_v = false, any_h = false;
   for (auto& kv : c->params) {
     any_w |= kv.first.rfind("whisper.", 0) == 0;
+    any_h |= kv.first.rfind("hubert.", 0) == 0;
     any_m |= kv.first.rfind("mapper.", 0) == 0;
     any_v |= kv.first.rfind("vocoder.", 0) == 0;
   }
   if (any_w && (st = build_whisper(c))) return st;
+  if (any_h && (st = build_hubert(c))) return st;
   if (any_m && (st = build_mapper(c))) return st;
   if (any_v && (st = build_vocoder(c))) return st;
   c->params.clear();  // host arrays are no longer referenced
@@ -1122,6 +1296,142 @@ svc_status svc_map_content(svc_ctx* c, const float* feats, int B, int src_rows, 
   SVC_REQUIRE(c && feats && out, "map_content: null");
   SVC_HIP_CHECK(hipSetDevice(c->device));
   return content_map(feats, B, src_rows, D, T, D, (f16*)out, D, (hipStream_t)stream);
+}
+
+svc_status svc_map_content_ex(svc_ctx* c, const float* feats, int B, int src_rows, int T, int D, int mode, void* out,
+                              int ld_out, void* stream) {
+  SVC_REQUIRE(c && feats && out && B > 0 && D > 0 && ld_out >= D, "map_content_ex: bad args");
+  SVC_REQUIRE(mode == 0 || mode == 1, "map_content_ex: mode %d", mode);
+  SVC_HIP_CHECK(hipSetDevice(c->device));
+  if (mode == 0) return content_map(feats, B, src_rows, D, T, D, (f16*)out, ld_out, (hipStream_t)stream);
+  return content_map_hubert(feats, B, src_rows, D, T, D, (f16*)out, ld_out, (hipStream_t)stream);
+}
+
+// ---------------------------------------------------------------------------- hubert / contentvec (A8)
+static int64_t hubert_len(int64_t n, int upto) {
+  static const int k[7] = {10, 3, 3, 3, 3, 2, 2}, st[7] = {5, 2, 2, 2, 2, 2, 2};
+  for (int i = 0; i < upto; ++i) n = n < k[i] ? 0 : (n - k[i]) / st[i] + 1;
+  return n;
+}
+
+svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, float* feats, void* stream) {
+  CTX_READY(c);
+  SVC_REQUIRE(c->has_hubert, "hubert weights not loaded");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t F64 = hubert_len(n, 7);
+  SVC_REQUIRE(B > 0 && F64 >= 1 && (int64_t)B * hubert_len(n, 1) < (1LL << 31), "hubert: B=%d n=%lld", B,
+              (long long)n);
+  int64_t t[8];
+  for (int i = 0; i <= 7; ++i) t[i] = hubert_len(n, i);  // t[0] = n samples, t[7] = frames
+  const int Cc = c->hC, D = c->hD, F = (int)F64;
+  const int Fd = c->hblocks[0].fc1.N;
+  const int64_t R5 = cdiv64(n, 5);
+  const size_t rows0 = (size_t)B * t[1], rowsF = (size_t)B * F;
+  const int kChunks = 64;
+  size_t need = (size_t)B * R5 * 8 * 2 + rows0 * Cc * 4 + rows0 * Cc * 2 + (size_t)B * kChunks * Cc * 16 +
+                (size_t)B * Cc * 8 + (size_t)B * (t[2] + t[3]) * Cc * 2 + rowsF * Cc * 6 + rowsF * D * 6 +
+                rowsF * 3 * D * 2 + rowsF * D * 2 + rowsF * Fd * 2 + 32 * 4096;
+  int st;
+  if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
+  c->ws.reset();
+  // ---- feature extractor (wav2vec2 ConvFeatureExtractionModel, mode "default")
+  WS_GET(f16, f5, (size_t)B * R5 * 8);
+  WS_GET(float, c0, rows0 * Cc);
+  WS_GET(f16, g16, rows0 * Cc);
+  WS_GET(double, part, (size_t)B * kChunks * Cc * 2);
+  WS_GET(float2, gss, (size_t)B * Cc);
+  WS_GET(f16, pa, (size_t)B * t[2] * Cc);
+  WS_GET(f16, pb, (size_t)B * t[3] * Cc);
+  WS_GET(float, c6, rowsF * Cc);
+  WS_GET(f16, ln16, rowsF * Cc);
+  if ((st = hubert_frames5(wav16, B, n, f5, s))) return st;
+  EpiArgs e = epi();
+  e.out32 = c0;
+  e.ld32 = Cc;
+  if ((st = run_gemm(c->hconv[0], f5, 8, 8, B, (int)R5, (int)t[1], e, s, "hubert.conv0"))) return st;
+  if ((st = groupnorm_gelu(c0, B, (int)t[1], Cc, c->hgn_g, c->hgn_b, part, kChunks, gss, g16, s))) return st;
+  const f16* in = g16;
+  for (int i = 1; i < 7; ++i) {
+    e = epi();
+    e.act = ACT_GELU;
+    if (i == 6) {
+      e.out32 = c6;
+      e.ld32 = Cc;
+    } else {
+      e.out16 = (i & 1) ? pa : pb;
+      e.ld16 = Cc;
+    }
+    if ((st = run_gemm(c->hconv[i], in, Cc, Cc, B, (int)t[i], (int)t[i + 1], e, s, "hubert.convs"))) return st;
+    in = e.out16;
+  }
+  // ---- HubertModel.forward_features tail: LayerNorm(C) -> post_extract_proj
+  if ((st = layernorm_f16(c6, c->hln_g, c->hln_b, ln16, (int)rowsF, Cc, Cc, s))) return st;
+  WS_GET(float, x, rowsF * D);
+  WS_GET(f16, x16, rowsF * D);
+  e = epi();
+  e.out32 = x;
+  e.ld32 = D;
+  e.out16 = x16;
+  e.ld16 = D;
+  if ((st = run_gemm(c->hproj, ln16, Cc, Cc, B, F, F, e, s, "hubert.proj"))) return st;
+  // ---- TransformerEncoder: x += GELU(pos_conv(x)) per group, then LayerNorm (layer_norm_first = False)
+  const int Cg = D / c->hPosG;
+  for (int gi = 0; gi < c->hPosG; ++gi) {
+    e = epi();
+    e.act = ACT_GELU;
+    e.add_row = x + gi * Cg;
+    e.ld_add_row = D;
+    e.out32 = x + gi * Cg;
+    e.ld32 = D;
+    if ((st = run_gemm(c->hpos[gi], x16 + gi * Cg, D, Cg, B, F, F, e, s, "hubert.pos_conv"))) return st;
+  }
+  if ((st = layernorm_dual(x, c->henc_ln_g, c->henc_ln_b, x, x16, (int)rowsF, D, s))) return st;
+  WS_GET(f16, qkv, rowsF * 3 * D);
+  WS_GET(f16, o16, rowsF * D);
+  WS_GET(f16, h16, rowsF * Fd);
+  const float qk_scale = powf(64.0f, -0.25f);  // q * dh^-1/2 split over q and k
+  for (int i = 0; i < c->hLayers; ++i) {
+    HBlock& b = c->hblocks[i];
+    e = epi();
+    e.out16 = qkv;
+    e.ld16 = 3 * D;
+    e.scale_cols = 2 * D;
+    e.col_scale = qk_scale;
+    if ((st = run_gemm(b.qkv, x16, D, D, B, F, F, e, s, "hubert.qkv"))) return st;
+    if ((st = attention(qkv, o16, B, F, D, s))) return st;
+    e = epi();
+    e.add_row = x;
+    e.ld_add_row = D;
+    e.out32 = x;
+    e.ld32 = D;
+    if ((st = run_gemm(b.out, o16, D, D, B, F, F, e, s, "hubert.out"))) return st;
+    if ((st = layernorm_dual(x, b.ln1_g, b.ln1_b, x, x16, (int)rowsF, D, s))) return st;
+    e = epi();
+    e.act = ACT_GELU;
+    e.out16 = h16;
+    e.ld16 = Fd;
+    if ((st = run_gemm(b.fc1, x16, D, D, B, F, F, e, s, "hubert.fc1"))) return st;
+    e = epi();
+    e.add_row = x;
+    e.ld_add_row = D;
+    e.out32 = x;
+    e.ld32 = D;
+    if ((st = run_gemm(b.fc2, h16, Fd, Fd, B, F, F, e, s, "hubert.fc2"))) return st;
+    if ((st = layernorm_dual(x, b.ln2_g, b.ln2_b, x, x16, (int)rowsF, D, s))) return st;
+  }
+  e = epi();
+  e.out32 = feats;
+  e.ld32 = c->hFinal;
+  return run_gemm(c->hfinal, x16, D, D, B, F, F, e, s, "hubert.final_proj");
+}
+
+int64_t svc_hubert_frames(int64_t n_samples) { return hubert_len(n_samples, 7); }
+
+int svc_hubert_dims(svc_ctx* c, int* final_dim, int* embed_dim) {
+  SVC_REQUIRE(c && c->has_hubert, "hubert weights not loaded");
+  if (final_dim) *final_dim = c->hFinal;
+  if (embed_dim) *embed_dim = c->hD;
+  return SVC_OK;
 }
 
 // ---------------------------------------------------------------------------- conditioner

@@ -3,6 +3,7 @@
     mel, energy = acoutic_feature_extractor(...)        infer.py:53   -> SVCEngine.mel_energy + f0
     f0 = pitch_shift(f0, cfg)                           infer.py:59   -> SVCEngine.pitch_shift
     whisper_feature = whisper_feature_extractor(...)    infer.py:64   -> whisper_encode + map_content
+    contentVec_feature = contentVec_feature_extractor   infer.py:65   -> hubert_encode + map_content(rule="hubert")
     y_pred = svc_model_inference(...)                   infer.py:79   -> condition + diffsvc_sample
     y_pred = denormalize_mel_channel(y_pred, cfg)       infer.py:80   -> fused into bigvgan
     audio = synthesis_audios(...)                       infer.py:86   -> bigvgan (Generator, trim, fade)
@@ -29,6 +30,7 @@ from .runtime import SVCEngine
 WHISPER_WINDOW = 478720       # 16 kHz samples per long-input window (29.92 s)
 WINDOW_MEL_FRAMES = 2805      # = 1496 encoder frames * 15 / 8
 MAX_MAPPED = 2812             # utils/whisper.py:56 (1500 * 15 // 8)
+HUBERT_CONTENT_TYPES = ("contentvec", "content_vector", "hubert")  # config/config.json:35 names it content_vector
 
 
 @dataclass
@@ -43,7 +45,34 @@ class SVCPipeline:
     def __init__(self, engine: SVCEngine):
         self.engine = engine
 
-    def content(self, wav16, T):
+    def content(self, wav16, T, wav16_float=None):
+        """Content features of every type in cfg.mapper.content_feature mapped to T mel frames -> f16
+        [B, T, sum of widths], the types' columns concatenated in ascending name order (the order in which the
+        native conditioner packs their ContentEncoder Linears). "whisper" runs Whisper on the int16-quantised
+        16 kHz audio (utils/whisper.py:96-103); "contentvec" runs HuBERT/ContentVec on float 16 kHz audio
+        (utils/hubert.py:137-143; `wav16_float`, defaulting to wav16)."""
+        e = self.engine
+        m = e.cfg.mapper
+        types = sorted(m.content_feature)
+        if types == ["whisper"]:
+            return self.whisper_content(wav16, T)
+        widths = [int(m.input_content_dim[t]) for t in types]
+        B = wav16.shape[0]
+        out = torch.empty(B, T, sum(widths), device=wav16.device, dtype=torch.float16)
+        col = 0
+        for t, w in zip(types, widths):
+            view = out[:, :, col:col + w]
+            if t == "whisper":
+                view.copy_(self.whisper_content(wav16, T))
+            elif t in HUBERT_CONTENT_TYPES:
+                feats = e.hubert_encode(wav16 if wav16_float is None else wav16_float)
+                e.map_content(feats, T, rule="hubert", out=view)
+            else:
+                raise ValueError(f"content feature {t!r} is not supported (whisper, {', '.join(HUBERT_CONTENT_TYPES)})")
+            col += w
+        return out
+
+    def whisper_content(self, wav16, T):
         """Whisper content features mapped to T mel frames -> f16 [B, T, D]."""
         e = self.engine
         B = wav16.shape[0]
@@ -63,14 +92,14 @@ class SVCPipeline:
         return out[:, :T].contiguous()
 
     def convert(self, wav24, wav16, singer, fast_inference=True, speedup=10, seed=0, utt_ids=None, x_T=None,
-                noise=None, f0=None):
+                noise=None, f0=None, wav16_float=None):
         e = self.engine
         mel, energy = e.mel_energy(wav24)
         T = mel.shape[1]
         if f0 is None:
             f0 = e.f0(wav24, T)
         e.pitch_shift(f0)
-        content = self.content(wav16, T)
+        content = self.content(wav16, T, wav16_float)
         cond = e.condition(content, f0, energy, singer)
         if utt_ids is None and x_T is None:
             utt_ids = torch.arange(wav24.shape[0], device=wav24.device, dtype=torch.int32)

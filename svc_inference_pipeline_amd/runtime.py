@@ -31,10 +31,12 @@ def mel_frames(n_samples, n_fft=1024, hop=256):
 
 
 class SVCEngine:
-    """Stages of infer.py on one GPU. `whisper_state`, `mapper_state`, `vocoder_state` are dicts in the
-    reference's state_dict naming (svc_inference_pipeline_amd.weights); any subset may be given."""
+    """Stages of infer.py on one GPU. `whisper_state`, `mapper_state`, `vocoder_state`, `hubert_state` are dicts
+    in the reference's state_dict naming (svc_inference_pipeline_amd.weights; fairseq's for HuBERT); any subset
+    may be given. `hubert_output_layer` is utils/hubert.py:42's output_layer (9)."""
 
-    def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None):
+    def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None, hubert_state=None,
+                 hubert_output_layer=9):
         _lib.load()
         self.cfg = cfg
         self.device = device
@@ -46,6 +48,9 @@ class SVCEngine:
         if whisper_state is not None:
             self._add_state("whisper.", whisper_state)
             self.whisper_dims = W.whisper_dims_from_state(whisper_state)
+        if hubert_state is not None:
+            _lib.call("svc_ctx_set_config", self._ctx, b"hubert.output_layer", float(hubert_output_layer))
+            self._add_state("hubert.", hubert_state)
         if mapper_state is not None:
             self._add_state("mapper.", mapper_state)
             self._add("mapper.step_table", W.step_embedding_table(len(noise_schedule(cfg.mapper))).numpy())
@@ -144,12 +149,29 @@ class SVCEngine:
         _lib.call("svc_whisper_encode", self._ctx, _ptr(wav16), B, N, _ptr(feats), _stream())
         return feats
 
-    def map_content(self, feats, T):
-        """15:8 repeat/average to mel frames (utils/whisper.py:31-81) -> f16 [B, T, D]."""
+    def map_content(self, feats, T, rule="whisper", out=None):
+        """15:8 repeat/average to mel frames -> f16 [B, T, D]. rule "whisper": utils/whisper.py:31-81 (T <= 2812);
+        rule "hubert": utils/hubert.py:83-134 (no cap, <= 3 missing frames repeat the last one, more is an
+        error). `out` may be a column slice [B, T, D] of a wider f16 buffer (concatenated content types)."""
         B, S, D = feats.shape
-        out = torch.empty(B, T, D, device=feats.device, dtype=torch.float16)
-        _lib.call("svc_map_content", self._ctx, _ptr(feats), B, S, T, D, _ptr(out), _stream())
+        if out is None:
+            out = torch.empty(B, T, D, device=feats.device, dtype=torch.float16)
+        assert out.shape == (B, T, D) and out.stride(2) == 1 and out.stride(0) == T * out.stride(1)
+        mode = {"whisper": 0, "hubert": 1}[rule]
+        _lib.call("svc_map_content_ex", self._ctx, _ptr(feats.contiguous()), B, S, T, D, mode,
+                  ctypes.c_void_p(out.data_ptr()), out.stride(1), _stream())
         return out
+
+    def hubert_encode(self, wav16):
+        """get_hubert_content (utils/hubert.py:31-47): wav16 f32 [B, N] (16 kHz float audio) -> ContentVec
+        features f32 [B, frames, final_dim] (time-major; the reference returns the transpose)."""
+        B, N = wav16.shape
+        fd, _ = ctypes.c_int(), ctypes.c_int()
+        _lib.call("svc_hubert_dims", self._ctx, ctypes.byref(fd), None)
+        F = int(_lib.load().svc_hubert_frames(N))
+        feats = torch.empty(B, F, fd.value, device=wav16.device, dtype=torch.float32)
+        _lib.call("svc_hubert_encode", self._ctx, _ptr(wav16.contiguous()), B, N, _ptr(feats), _stream())
+        return feats
 
     def condition(self, content16, f0, energy, singer):
         """EncoderFramework.forward (modules/encoder.py:165-201) -> cond f32 [B, T, C]."""
