@@ -300,19 +300,24 @@ def bigvgan_forward(sd, vcfg, mel):
 
 
 # ============================================================================ fp16-operand emulation
-class Fp16Operands:
-    """Context manager: dense convolutions round their input and weight to binary16 (fp32 accumulate),
-    emulating the MFMA operand precision of the HIP path. Used to derive tolerances for chaotic
-    random-weight regimes (tests/test_gpu_stages.py::test_bigvgan); depthwise (grouped) convs are
-    untouched because the HIP path computes them in fp32."""
+class OperandRounding:
+    """Context manager: dense convolutions (and, with `linear=True`, F.linear and the attention matmuls of
+    the functional encoders) round their input and weight to `dtype` (float16 / bfloat16) and accumulate in
+    fp32, emulating MFMA operand precision. Used to derive tolerances for chaotic random-weight regimes
+    (tests/test_gpu_stages.py::test_bigvgan) and for the fp16-vs-bf16 sweep (tools/precision_sweep.py);
+    depthwise (grouped) convs are untouched because the HIP path computes them in fp32."""
+
+    def __init__(self, dtype=torch.float16, linear=False):
+        self.dtype, self.linear = dtype, linear
 
     def __enter__(self):
-        self._c, self._t = F.conv1d, F.conv_transpose1d
-        r = lambda t: t.half().float()
-        c, tr = self._c, self._t
+        self._c, self._t, self._l, self._m = F.conv1d, F.conv_transpose1d, F.linear, torch.Tensor.__matmul__
+        dt = self.dtype
+        r = lambda t: t.to(dt).float()  # noqa: E731
+        c, tr, li, mm = self._c, self._t, self._l, self._m
 
         def conv1d(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
-            if groups > 1:
+            if groups > 1 and w.shape[1] == 1:
                 return c(x, w, b, stride, padding, dilation, groups)
             return c(r(x), r(w), b, stride, padding, dilation, groups)
 
@@ -322,8 +327,19 @@ class Fp16Operands:
             return tr(r(x), r(w), b, stride, padding, output_padding, groups, dilation)
 
         F.conv1d, F.conv_transpose1d = conv1d, conv_t
+        if self.linear:
+            F.linear = lambda x, w, b=None: li(r(x), r(w), b)
+            torch.Tensor.__matmul__ = lambda a, b: mm(r(a), r(b))
         return self
 
     def __exit__(self, *a):
-        F.conv1d, F.conv_transpose1d = self._c, self._t
+        F.conv1d, F.conv_transpose1d, F.linear = self._c, self._t, self._l
+        torch.Tensor.__matmul__ = self._m
         return False
+
+
+class Fp16Operands(OperandRounding):
+    """fp16 conv operands (the BigVGAN tolerance derivation)."""
+
+    def __init__(self):
+        super().__init__(torch.float16, linear=False)

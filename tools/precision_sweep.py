@@ -1,0 +1,121 @@
+"""BASELINE config 5 tolerance sweep: HuBERT/ContentVec content + DDPM-1000 + BigVGAN, fp16 vs bf16 operands.
+
+The reference runs in fp32. The HIP path feeds MFMA with fp16 operands and accumulates in fp32 (DESIGN.md,
+"Dtypes"); bf16 runs at the same gfx950 MFMA rate but keeps 8 instead of 11 significand bits. This tool measures
+what that choice costs on the config-5 path, against the fp32 oracle on identical inputs, weights, x_T and
+per-step noise:
+
+  fp16-emu / bf16-emu : the oracle with every dense conv / linear / attention matmul rounding its operands to
+                        that type (oracle.models.OperandRounding), fp32 accumulation — the operand precision a
+                        bf16 build of the same kernels would have.
+  gpu-fp16            : the actual HIP path (--gpu; needs an MI355X), through the C-ABI.
+
+Metrics, per SURVEY.md §7.3: mel-L1 = mean |delta| of the de-normalised natural-log mel fed to the vocoder (the
+north-star target is <= 1e-3), plus the same in normalised units, the content features' and the waveform's
+relative L2. Random weights (no checkpoints offline) make BigVGAN chaotic, so the waveform figure is
+informational. Usage: python tools/precision_sweep.py [--gpu] [--seconds 1.0] > profiles/<round>_precision_sweep.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from oracle import features as OF  # noqa: E402
+from oracle import models as OM  # noqa: E402
+from oracle import noise as ON  # noqa: E402
+from svc_inference_pipeline_amd import config as C  # noqa: E402
+from svc_inference_pipeline_amd import weights as W  # noqa: E402
+
+
+def rel_l2(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def oracle_chain(cfg, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats):
+    mel = OF.mel_spectrogram(torch.from_numpy(w24)[None], cfg)
+    en = OF.energy_from_mel(mel)
+    T = mel.shape[-1]
+    f0s = torch.from_numpy(OF.pitch_shift(f0, stats["target_f0_median"]))[None]
+    with torch.no_grad():
+        hf = OM.hubert_content(hs, torch.from_numpy(w16)[None], 9)[0].numpy()
+        content = torch.from_numpy(OF.map_hubert_features(hf, T).astype(np.float32))[None]
+        cond = OM.conditioner(ms, {"contentvec": content}, f0s, en, torch.tensor([[2]]))
+        table = W.step_embedding_table(1000)
+        consts = OM.schedule_constants(C.noise_schedule(cfg.mapper))
+        den = lambda x, t: OM.diffsvc_forward(ms, cfg.mapper, x, cond, t, table)  # noqa: E731
+        x0 = OM.sample_ddpm(den, torch.from_numpy(xT), 1, T, 1000, consts, noise_fn)
+        mel_d = OF.denormalize_mel_channel(x0[0].numpy().T, stats["mel_min"], stats["mel_max"]).astype(np.float32)
+        wav = OM.bigvgan_forward(vs, cfg.vocoder, torch.from_numpy(mel_d)[None])
+        wav = OF.synthesis_fade(wav[0, 0], T).numpy()
+    return dict(content=content[0].numpy(), x0=x0[0].numpy(), mel=mel_d.T, wav=wav)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpu", action="store_true")
+    ap.add_argument("--seconds", type=float, default=1.0)
+    ap.add_argument("--threads", type=int, default=16)
+    args = ap.parse_args()
+    torch.set_num_threads(args.threads)
+    cfg = C.load_config()
+    cfg.mapper.content_feature = ["contentvec"]
+    cfg.mapper.input_content_dim["contentvec"] = W.HUBERT_DIMS["contentvec"]["final_dim"]
+    hs = W.make_hubert_state(W.HUBERT_DIMS["contentvec"], 0)
+    ms = W.make_mapper_state(cfg.mapper, 0)
+    vs = W.make_vocoder_state(cfg.vocoder, 0)
+    stats = C.load_stats(cfg)
+    w24 = ON.synth_clip(7, args.seconds, 24000).astype(np.float32)
+    w16 = ON.synth_clip(7, args.seconds, 16000).astype(np.float32)
+    T = OF.mel_frames(len(w24))
+    f0 = ON.synth_f0(4, T)
+    seed = 17
+    xT = ON.x_T(seed, 1, T)
+    noise_fn = lambda i: torch.from_numpy(ON.step_noise(seed, i, 1, T))  # noqa: E731
+
+    results = {}
+    t0 = time.time()
+    ref = oracle_chain(cfg, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats)
+    timing = {"fp32": round(time.time() - t0, 1)}
+    runs = {}
+    for name, dt in (("fp16-emu", torch.float16), ("bf16-emu", torch.bfloat16)):
+        t0 = time.time()
+        with OM.OperandRounding(dt, linear=True):
+            runs[name] = oracle_chain(cfg, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats)
+        timing[name] = round(time.time() - t0, 1)
+    if args.gpu:
+        from svc_inference_pipeline_amd.pipeline import SVCPipeline
+        from svc_inference_pipeline_amd.runtime import SVCEngine
+        e = SVCEngine(cfg, 0, mapper_state=ms, vocoder_state=vs, hubert_state=hs)
+        d = lambda a, t=torch.float32: torch.as_tensor(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
+        noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
+        pipe = SVCPipeline(e)
+        content = pipe.content(d(w16[None]), T, d(w16[None])).float().cpu().numpy()[0]
+        res = pipe.convert(d(w24[None]), d(w16[None]), d(np.array([2]), torch.int32), fast_inference=False,
+                           x_T=d(xT), noise=d(noise), f0=d(f0[None], torch.float64), wav16_float=d(w16[None]))
+        _, mel_d = e.bigvgan(res.x0, return_mel=True)
+        runs["gpu-fp16"] = dict(content=content, x0=res.x0[0].cpu().numpy(), mel=mel_d[0].cpu().numpy(),
+                                wav=res.wav[0].cpu().numpy())
+        e.close()
+    for name, r in runs.items():
+        results[name] = {
+            "mel_l1_denorm_ln": float(np.mean(np.abs(r["mel"] - ref["mel"]))),
+            "mel_l1_normalised": float(np.mean(np.abs(r["x0"] - ref["x0"]))),
+            "mel_l1_target_1e-3_met": bool(np.mean(np.abs(r["mel"] - ref["mel"])) <= 1e-3),
+            "content_rel_l2": rel_l2(r["content"], ref["content"]),
+            "wav_rel_l2": rel_l2(r["wav"], ref["wav"]),
+        }
+    print(json.dumps({"config": "BASELINE config 5: ContentVec (layer 9) + DDPM-1000 + BigVGAN, seeded random weights, "
+                                f"{args.seconds:g} s synthetic clip (T={T}), shared x_T and step noise; reference = "
+                                "fp32 oracle", "cpu_seconds": timing, "results": results}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
