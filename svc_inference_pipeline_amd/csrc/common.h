@@ -50,10 +50,31 @@ static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 static inline int64_t cdiv64(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static inline int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// exact-form GELU, x * Phi(x) (torch F.gelu default). erf by Abramowitz & Stegun 7.1.26 on the native
+// v_exp_f32 / v_rcp_f32 (|error| <= 1.5e-7 absolute, ~14 VALU instead of libm erff's branchy ~30): every
+// caller stores the result as fp16 or adds it to an fp32 stream whose other terms carry fp16 operand error.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(-1.4426950408889634f * ax * ax);
+  return copysignf(fmaf(-p * t, e, 1.0f), x);
+}
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 // saturating fp32 -> fp16 store (NaN stays NaN): random-weight regimes can exceed the fp16 range
 __device__ __forceinline__ f16 f16_sat(float v) { return (f16)(v > 65504.f ? 65504.f : (v < -65504.f ? -65504.f : v)); }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+// Gate math on the native v_exp_f32 / v_rcp_f32 (~1 ulp each): the products feed an fp16 store, so these
+// replace libm's expf / tanhf / IEEE division (~60 VALU per gate pair) in the MFMA kernels' epilogues.
+__device__ __forceinline__ float fast_sigmoid(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float fast_tanh(float x) {  // 1 - 2 / (1 + e^{2x}): +-1 at the saturated ends
+  return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(2.8853900817779268f * x));
+}
 
 // ------------------------------------------------------------------ implicit-GEMM descriptors
 // Y[m, n] = epilogue( sum_{tap, c} X[in_row(m, tap), c] * Wp[n, tap*Cp + c] )
