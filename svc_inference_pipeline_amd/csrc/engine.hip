@@ -112,6 +112,22 @@ int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
+struct DiffLayerArgs {
+  const f16* x16;
+  const f16* Wd;
+  const f16* cpF;
+  const f16* Wo;
+  const float* bo;
+  const float* dpn;
+  float* x32;
+  f16* x16n;
+  f16* g16;
+  int ldg;
+  int B, T, dil;
+  const f16* zpage;
+};
+int diff_layer(const DiffLayerArgs& a, bool out, hipStream_t s);
+int cp_fragment(const f16* cp16, int ldcp, const float* bdil, int rows, int rows_pad, f16* cpF, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s);
 int hubert_frames5(const float* wav, int B, int64_t n, f16* out, hipStream_t s);
@@ -267,6 +283,10 @@ struct svc_ctx {
   int C = 384, n_mel = 100, n_layers = 20, dil_cycle = 4, steps = 1000, content_dim = 1024, n_bins = 256;
   PackedGemm content_lin, cp_all, melpre, skipproj, outproj;
   std::vector<PackedGemm> dil, outres;  // per layer: dilated conv (paired), residual half of output_projection
+  // fused residual-layer kernel (diff_layer.hip): pair16-packed dilated conv [2C][3C], residual half of
+  // output_projection [C][C], its bias [C], the dilated conv bias [2C] (folded into the fragment-major cp)
+  std::vector<f16*> dl_wd, dl_wo;
+  std::vector<float*> dl_bo, dl_bdil;
   PackedGemm skip_all;                  // skip halves of all layers' output_projection, K = layers * C
   float *emb_m = nullptr, *emb_l = nullptr, *emb_s = nullptr, *mbins = nullptr, *ebins = nullptr;
   float* dproj = nullptr;  // [steps][layers][C]
@@ -777,6 +797,27 @@ int build_mapper(svc_ctx* c) {
     if ((st = pack_conv1d(c, c->dil[i], dw->host, db->host, 2 * C, C, 3, C, d, d, 1, &perm))) return st;
     // rows 0..C-1 of output_projection are the residual, C..2C-1 the skip (modules/diffsvc.py:229-231)
     if ((st = pack_conv1d(c, c->outres[i], ow->host, ob->host, C, C, 1, C, 1, 0, 1))) return st;
+    if (C == 384) {  // the fused layer kernel is specialised for the reference's 384 residual channels
+      std::vector<f16> wd((size_t)2 * C * 3 * C), wo((size_t)C * C);
+      for (int n = 0; n < 2 * C; ++n) {
+        const int o = ((n & 16) ? C : 0) + (n >> 5) * 16 + (n & 15);  // pair16: gate/filter of one channel
+        for (int tap = 0; tap < 3; ++tap)
+          for (int ci = 0; ci < C; ++ci)
+            wd[(size_t)n * 3 * C + tap * C + ci] = (f16)dw->host[((int64_t)o * C + ci) * 3 + tap];
+      }
+      for (int n = 0; n < C; ++n)
+        for (int ci = 0; ci < C; ++ci) wo[(size_t)n * C + ci] = (f16)ow->host[(int64_t)n * C + ci];
+      f16 *dwp, *wop;
+      float *bop, *bdp;
+      if ((st = upload_vec(c, wd, &dwp)) || (st = upload_vec(c, wo, &wop))) return st;
+      if ((st = dev_upload(c, ob->host, (size_t)C * 4, (void**)&bop)) ||
+          (st = dev_upload(c, db->host, (size_t)2 * C * 4, (void**)&bdp)))
+        return st;
+      c->dl_wd.push_back(dwp);
+      c->dl_wo.push_back(wop);
+      c->dl_bo.push_back(bop);
+      c->dl_bdil.push_back(bdp);
+    }
     opw_l[i] = ow;
     opb_l[i] = ob;
   }
@@ -1471,12 +1512,24 @@ svc_status svc_condition(svc_ctx* c, const void* content16, const double* f0, co
 // ---------------------------------------------------------------------------- DiffSVC denoiser
 struct DenoiseBufs {
   f16* cp16;     // [rows][NL*2C] conditioner projections of every layer (hoisted out of the sampler loop)
+  f16* cpF;      // fused path: [NL][rows_pad][2C] fragment-major cp + dilated bias (diff_layer.hip)
+  int rows_pad;  // rows of this (sub-)batch rounded up to 64
+  f16* y16b;     // [rows][C] ping-pong partner of y16 (the fused layer reads one and writes the other)
   float* h32;    // [rows][C] residual stream
   f16* y16;      // [rows][C] next layer input x + diffusion_projection
   f16* g16;      // [rows][NL*C] gate outputs of every layer (A operand of the skip GEMM)
   f16* s16;      // [rows][C] sum(skip) / sqrt(NL)
   f16* u16;      // [rows][C] relu(skip_projection)
 };
+
+// The fused residual-layer kernel (diff_layer.hip) is opt-in (SVC_DIFF_FUSED=1): owning all 768 gate columns
+// per 64-row tile makes every workgroup stream the whole 1.77 MB dilated-conv weight, and at the measured
+// ~12 B/clk/CU L2->LDS fill rate that costs more (155 us/layer at B=32) than it saves over the two tiled GEMMs
+// (97 + 45 us) — DESIGN.md, "Fused residual layer (measured, not adopted)".
+static bool fused_layers(svc_ctx* c) {
+  const char* v = getenv("SVC_DIFF_FUSED");  // read per call (A/B runs and tests switch it)
+  return (int)c->dl_wd.size() == c->n_layers && v && atoi(v) == 1;
+}
 
 static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s) {
   const int C = c->C, NL = c->n_layers, rows = B * T;
@@ -1491,7 +1544,31 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
   if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
-  for (int i = 0; i < NL; ++i) {
+  if (fused_layers(c)) {
+    f16* cur = bb.y16;
+    f16* nxt = bb.y16b;
+    for (int i = 0; i < NL; ++i) {
+      DiffLayerArgs a{};
+      a.x16 = cur;
+      a.Wd = c->dl_wd[i];
+      a.cpF = bb.cpF + (size_t)i * bb.rows_pad * 2 * C;
+      a.Wo = c->dl_wo[i];
+      a.bo = c->dl_bo[i];
+      a.dpn = i + 1 < NL ? dp + (size_t)(i + 1) * C : nullptr;
+      a.x32 = bb.h32;
+      a.x16n = nxt;
+      a.g16 = bb.g16 + (size_t)i * C;
+      a.ldg = NL * C;
+      a.B = B;
+      a.T = T;
+      a.dil = 1 << (i % c->dil_cycle);
+      a.zpage = zero_page();
+      prof_site("diffsvc.layer");
+      if ((st = diff_layer(a, i + 1 < NL, s))) return st;
+      std::swap(cur, nxt);
+    }
+  }
+  for (int i = 0; i < NL && !fused_layers(c); ++i) {
     EpiArgs g = epi();
     g.kind = EPI_GATE;
     g.cp = bb.cp16 + (size_t)i * 2 * C;
@@ -1533,19 +1610,36 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
 
 static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   const size_t rows = (size_t)B * T, C = c->C;
+  const size_t fm_rows = fused_layers(c) ? rows + 64 * kMaxSubStreams : 0;  // sub-batch regions padded to 64 rows
   WS_GET(f16, cp16, rows * c->n_layers * 2 * C);
+  WS_GET(f16, cpF, fm_rows * c->n_layers * 2 * C + 8);
   WS_GET(float, h32, rows * C);
   WS_GET(f16, y16, rows * C);
+  WS_GET(f16, y16b, rows * C);
   WS_GET(f16, g16, rows * c->n_layers * C);
   WS_GET(f16, s16, rows * C);
   WS_GET(f16, u16, rows * C);
-  bb = DenoiseBufs{cp16, h32, y16, g16, s16, u16};
+  bb = DenoiseBufs{cp16, cpF, (int)round_up((int64_t)rows, 64), y16b, h32, y16, g16, s16, u16};
   return SVC_OK;
 }
 
 static size_t denoise_bytes(svc_ctx* c, int B, int T) {
   const size_t rows = (size_t)B * T, C = c->C;
-  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 3) + 16 * 4096;
+  return rows * c->n_layers * 2 * C * 2 + (fused_layers(c) ? rows + 64 * kMaxSubStreams : 0) * c->n_layers * 2 * C * 2 +
+         rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 4) + 20 * 4096;
+}
+
+// fused path: the hoisted conditioner projection of one (sub-)batch -> fragment-major records with the dilated
+// conv bias folded in (bb.cpF / bb.rows_pad describe that sub-batch's region; cp16 points at its first row)
+static int fragment_cp(svc_ctx* c, const DenoiseBufs& bb, int rows, hipStream_t s) {
+  if (!fused_layers(c)) return SVC_OK;
+  const int C = c->C, NL = c->n_layers;
+  int st;
+  for (int l = 0; l < NL; ++l)
+    if ((st = cp_fragment(bb.cp16 + (size_t)l * 2 * C, NL * 2 * C, c->dl_bdil[l], rows, bb.rows_pad,
+                          bb.cpF + (size_t)l * bb.rows_pad * 2 * C, s)))
+      return st;
+  return SVC_OK;
 }
 
 static int project_cond(svc_ctx* c, const float* cond, int B, int T, const DenoiseBufs& bb, hipStream_t s) {
@@ -1573,6 +1667,7 @@ svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B,
   DenoiseBufs bb;
   if ((st = alloc_denoise(c, B, T, bb))) return st;
   if ((st = project_cond(c, cond, B, T, bb, s))) return st;
+  if ((st = fragment_cp(c, bb, rows, s))) return st;
   WS_GET(f16, x16, (size_t)rows * ld16);
   if ((st = f32_to_f16(x, c->n_mel, x16, ld16, rows, c->n_mel, ld16, s))) return st;
   return denoise(c, bb, x16, B, T, t, eps, s);
@@ -1626,20 +1721,29 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
     hipStream_t s;
   } sub[kMaxSubStreams];
   if ((st = c->ensure_sub_streams(S))) return st;
-  SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
   for (int h = 0; h < S; ++h) {
     sub[h].b0 = h * B / S;
     sub[h].B = (h + 1) * B / S - sub[h].b0;
     sub[h].r0 = (size_t)sub[h].b0 * T;
     sub[h].s = S == 1 ? s : c->sub_streams[h];
-    if (S > 1) SVC_HIP_CHECK(hipStreamWaitEvent(sub[h].s, c->ev_fork, 0));
+  }
+  size_t fm_off[kMaxSubStreams];  // start of each sub-batch's fragment-major cp region (rows padded to 64)
+  for (int h = 0, acc = 0; h < S; ++h) {
+    fm_off[h] = (size_t)acc;
+    acc += (int)round_up((int64_t)sub[h].B * T, 64);
   }
   auto sub_bufs = [&](const Sub& u) {
     const size_t r = u.r0;
     const int C = c->C, NL = c->n_layers;
-    return DenoiseBufs{bb.cp16 + r * NL * 2 * C, bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * NL * C, bb.s16 + r * C,
-                       bb.u16 + r * C};
+    const int h = (int)(&u - sub);
+    const int rp = (int)round_up((int64_t)u.B * T, 64);
+    return DenoiseBufs{bb.cp16 + r * NL * 2 * C, bb.cpF + fm_off[h] * NL * 2 * C, rp, bb.y16b + r * C,
+                       bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * NL * C, bb.s16 + r * C, bb.u16 + r * C};
   };
+  for (int h = 0; h < S; ++h)
+    if ((st = fragment_cp(c, sub_bufs(sub[h]), sub[h].B * T, s))) return st;
+  SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
+  for (int h = 0; h < S && S > 1; ++h) SVC_HIP_CHECK(hipStreamWaitEvent(sub[h].s, c->ev_fork, 0));
   auto join = [&]() -> int {
     if (S == 1) return SVC_OK;
     for (int h = 0; h < S; ++h) {

@@ -92,10 +92,34 @@ def test_eps_single_step(engine, cfg, states, golden):
         assert rel_l2(eps.cpu().numpy(), g[f"eps_t{t}"]) < 5e-3, t
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700)])
+def test_fused_layer_vs_oracle(engine, states, cfg, fused, B, T, monkeypatch):
+    """The fused residual-layer kernel (diff_layer.hip, opt-in) and the default GEMM path against the oracle on
+    ragged shapes (B*T not a multiple of the 64-row tile, utterance boundaries inside a tile), and against each
+    other: relative L2 <= 5e-3 vs the oracle (fp16 operands), <= 2e-3 between the two HIP paths."""
+    rng = np.random.default_rng(B * 1000 + T)
+    cond = rng.standard_normal((B, T, 384)).astype(np.float32)
+    x = rng.standard_normal((B, T, 100)).astype(np.float32)
+    table = W.step_embedding_table(1000)
+    monkeypatch.setenv("SVC_DIFF_FUSED", fused)
+    for t in (3, 640):
+        eps = engine.diffsvc_eps(dev(cond), dev(x), t).cpu().numpy()
+        with torch.no_grad():
+            ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond),
+                                     torch.full((B,), t, dtype=torch.long), table).numpy()
+        assert rel_l2(eps, ref) < 5e-3, (t, rel_l2(eps, ref))
+        monkeypatch.setenv("SVC_DIFF_FUSED", "1" if fused == "0" else "0")
+        other = engine.diffsvc_eps(dev(cond), dev(x), t).cpu().numpy()
+        monkeypatch.setenv("SVC_DIFF_FUSED", fused)
+        assert rel_l2(eps, other) < 2e-3
+
+
 @pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15"])
 def test_eps_gemm_variants(engine, golden, variant, monkeypatch):
-    """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant."""
+    """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path)."""
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
+    monkeypatch.setenv("SVC_DIFF_FUSED", "0")
     g = golden("conditioner_diffsvc")
     eps = engine.diffsvc_eps(dev(g["cond"]), dev(g["x_in"]), 500)
     assert rel_l2(eps.cpu().numpy(), g["eps_t500"]) < 5e-3
