@@ -107,3 +107,36 @@ class SVCPipeline:
                               utt_ids=utt_ids)
         wav = e.bigvgan(x0)
         return ConvertResult(wav=wav, mel=mel, f0=f0, x0=x0)
+
+    def convert_many(self, wavs24, wavs16, singers, wavs16_float=None, fast_inference=True, speedup=10, seed=0,
+                     utt_ids=None):
+        """Ragged requests: lists of per-utterance device tensors (24 kHz f32 [N_i],
+        16 kHz [N16_i], optional float 16 kHz for ContentVec) and singer ids -> list of waveforms f32 [T_i*hop] in
+        input order. Utterances are bucketed by exact length and each bucket runs as one batch; no kernel mixes
+        utterances and every per-element reduction order is independent of the batch composition, so each output
+        is bit-identical to converting that clip alone with the same utterance id (tests/test_gpu_ragged.py).
+        utt_ids (default: list positions) key the device noise, as in convert()."""
+        n = len(wavs24)
+        if not (len(wavs16) == n == len(singers)) or (wavs16_float is not None and len(wavs16_float) != n):
+            raise ValueError("convert_many: wavs24, wavs16, singers (and wavs16_float) must have one entry per utterance")
+        ids = list(range(n)) if utt_ids is None else [int(u) for u in utt_ids]
+        buckets = {}
+        for i in range(n):
+            key = (int(wavs24[i].shape[-1]), int(wavs16[i].shape[-1]),
+                   int(wavs16_float[i].shape[-1]) if wavs16_float is not None else 0)
+            buckets.setdefault(key, []).append(i)
+        out = [None] * n
+        dev = wavs24[0].device
+        for key in sorted(buckets):
+            idx = buckets[key]
+            w24 = torch.stack([wavs24[i].reshape(-1) for i in idx]).contiguous()
+            w16 = torch.stack([wavs16[i].reshape(-1) for i in idx]).contiguous()
+            w16f = torch.stack([wavs16_float[i].reshape(-1) for i in idx]).contiguous() if wavs16_float is not None else None
+            sing = torch.tensor([int(singers[i]) for i in idx], device=dev, dtype=torch.int32)
+            uid = torch.tensor([ids[i] for i in idx], device=dev, dtype=torch.int32)
+            res = self.convert(w24, w16, sing, fast_inference=fast_inference, speedup=speedup, seed=seed,
+                               utt_ids=uid, wav16_float=w16f)
+            for j, i in enumerate(idx):
+                out[i] = res.wav[j]
+        return out
+
