@@ -93,6 +93,7 @@ struct ConvGemmArgs {
   int B, T_out;
   int N;         // valid (packed) output columns
   int ntiles_n;
+  int halo;      // conv_gemm3 tap-reuse mode: max |tap shift| (0 = off); set by conv_gemm3 itself
 };
 
 // Epilogue kinds (runtime-selected inside one kernel family)

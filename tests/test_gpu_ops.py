@@ -33,10 +33,18 @@ def _tm(x):  # [B, C, T] -> time-major [B*T, C]
     (3, 17, 384, 100, 1, 1, 1, 0, 0),        # output projection (N=100)
     (3, 700, 384, 768, 3, 1, 2, 2, 0),       # several M tiles + M tail (gemm3 tile shapes)
     (2, 333, 256, 512, 3, 1, 4, 4, 2),
+    (2, 300, 384, 384, 11, 1, 5, 25, 0),     # BigVGAN stage 2 k=11 d=5: tap-reuse halo H=25
+    (1, 150, 768, 768, 7, 1, 3, 9, 0),       # BigVGAN stage 1 k=7 d=3
+    (3, 129, 192, 192, 11, 1, 3, 15, 0),     # ragged utterances inside the halo image
+    (1, 90, 128, 256, 7, 1, 7, 21, 0),       # |shift| 21, T < tile
 ])
 @pytest.mark.parametrize("variant", ["0", "1", "-1", "10", "11", "12", "13", "14", "15"])
-def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, monkeypatch):
+@pytest.mark.parametrize("halo", ["1", "0"])
+def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, halo, monkeypatch):
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)  # -1: v1, 0..4: conv_gemm2 tiles, 10..14: conv_gemm3 tiles, 15: auto
+    monkeypatch.setenv("SVC_GEMM_HALO", halo)        # conv_gemm3 tap reuse (multi-tap, Cin % 64 == 0, |shift| <= 32)
+    if halo == "0" and variant not in ("10", "14", "15"):
+        pytest.skip("the halo switch only affects conv_gemm3")
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, Cin, T, generator=g)
     w = torch.randn(Cout, Cin, k, generator=g) / np.sqrt(Cin * k)
