@@ -1,0 +1,196 @@
+// Fourth-generation implicit-GEMM Conv1d for gfx950: a 4-wave 128 x 128 tile built for 2 workgroups per CU.
+//
+// conv_gemm3 (8 waves, staggered ping-pong inside one workgroup) pays for its phase barriers with a small amount of
+// MFMA work per phase on 128-wide tiles (4 MFMAs per wave per phase at 128 x 128) and cannot overlap its prologue
+// and epilogue with anything. This kernel takes the other route on the short-K DiffSVC / BigVGAN shapes:
+//   * 4 waves = 2 (M) x 2 (N), wave tile 64 x 64: 32 v_mfma_f32_16x16x32_f16 per wave per K-tile (BK = 64), fragments
+//     read straight from LDS;
+//   * 2 LDS K-tile stages (A 128 rows + B 128 rows of 128 B each, 32 KiB per stage) filled by LDS-DMA one K-tile ahead,
+//     one barrier per K-tile;
+//     with the C-staging epilogue the workgroup needs 66 KiB, so two workgroups share a CU and one's prologue /
+//     epilogue runs beside the other's MFMAs (inter-workgroup overlap in place of intra-workgroup staggering);
+//   * the same operand images (128-B rows, 16-B chunk swizzle kv ^ (row & 6)), A loader (per-tap row shifts, zero
+//     rows outside the utterance) and LDS-staged vector epilogue (epilogue.h) as conv_gemm3.
+#include "common.h"
+#include "epilogue.h"
+
+namespace svc {
+
+constexpr int G4_BM = 128, G4_BN = 128, G4_NT = 256;
+constexpr int G4_STAGE = (G4_BM + G4_BN) * 128;  // 32 KiB
+constexpr int G4_LDC = G4_BN + 4;
+constexpr int G4_LDS = (2 * G4_STAGE > G4_BM * G4_LDC * 4) ? 2 * G4_STAGE : G4_BM * G4_LDC * 4;
+
+__device__ __forceinline__ int sw4(int row, int kv) { return kv ^ (row & 6); }
+
+__device__ __forceinline__ void g4_dma(const void* src, unsigned char* lds) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void g4_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void g4_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool CP64, bool PAIR>
+__global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage, float inv_cp) {
+  extern __shared__ __align__(16) unsigned char sm4[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tile_n = wgid % a.ntiles_n, tile_m = wgid / a.ntiles_n;
+  const int m0 = tile_m * G4_BM, n0 = tile_n * G4_BN;
+  const int M = a.B * a.T_out;
+  const int nk = a.Kpad / 64;
+  const f16* zsrc = zpage + lane * 8;
+
+  // DMA slots: image rows (wave * 4 + v) * 8 + (lane >> 3), v < 4, for A and for B
+  int a_t[4], a_kv[4];
+  const f16* a_p[4];
+  const f16* b_p[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int row = (wave * 4 + v) * 8 + (lane >> 3);
+    const int kv = sw4(row, lane & 7);
+    a_kv[v] = kv;
+    const int m = m0 + row;
+    if (m < M) {
+      const int b = m / a.T_out, t = m - b * a.T_out;
+      a_t[v] = t * a.istride;
+      a_p[v] = a.X + (int64_t)b * a.T_in * a.ldx + kv * 8;
+    } else {
+      a_t[v] = -(1 << 29);
+      a_p[v] = a.X;
+    }
+    b_p[v] = a.W + (int64_t)(n0 + row) * a.Kpad + kv * 8;
+  }
+  auto issue = [&](int kt) {
+    unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
+    unsigned char* Bm = A + G4_BM * 128;
+    const bool live = kt < nk;
+    if constexpr (CP64) {
+      const int kg = kt * 64;
+      const int tap = kg / a.Cp;
+      const int c0 = kg - tap * a.Cp;
+      const int shift = tap * a.tap_mul + a.tap_add;
+      const int64_t off = (int64_t)shift * a.ldx + c0;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int st = a_t[v] + shift;
+        const bool ok = live && st >= 0 && st < a.T_in;
+        g4_dma(ok ? (const void*)(a_p[v] + (int64_t)a_t[v] * a.ldx + off) : (const void*)zsrc,
+               A + (wave * 4 + v) * 1024);
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int kg = kt * 64 + a_kv[v] * 8;
+        int tap = (int)((float)kg * inv_cp);
+        if ((tap + 1) * a.Cp <= kg) ++tap;
+        if (tap * a.Cp > kg) --tap;
+        const int c = kg - tap * a.Cp;
+        const int st = a_t[v] + tap * a.tap_mul + a.tap_add;
+        const bool ok = live && kg < a.K && st >= 0 && st < a.T_in;
+        g4_dma(ok ? (const void*)(a_p[v] + (int64_t)st * a.ldx + (c - a_kv[v] * 8)) : (const void*)zsrc,
+               A + (wave * 4 + v) * 1024);
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+      g4_dma(live ? (const void*)(b_p[v] + kt * 64) : (const void*)zsrc, Bm + (wave * 4 + v) * 1024);
+  };
+
+  floatx4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fk = lane >> 4;
+
+  // One barrier per K-tile: DMA(kt + 1) is issued right after the barrier of iteration kt (which also proves every wave
+  // has finished reading that stage in iteration kt - 1) and lands under the MFMAs of iteration kt.
+  issue(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    g4_vmwait<0>();  // this wave's DMAs of stage kt have landed (nothing younger is outstanding)
+    g4_barrier();    // ... and everyone's; stage (kt + 1) & 1 is free
+    if (kt + 1 < nk) issue(kt + 1);
+    const unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
+    const unsigned char* Bm = A + G4_BM * 128;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      half8 af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        af[i] = *reinterpret_cast<const half8*>(A + row * 128 + (sw4(row, s * 4 + fk) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wn * 64 + j * 16 + fr;
+        bf[j] = *reinterpret_cast<const half8*>(Bm + row * 128 + (sw4(row, s * 4 + fk) << 4));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  g4_vmwait<0>();
+  __syncthreads();
+  // acc[i][j][r] = C[wm*64 + i*16 + fk*4 + r][wn*64 + j*16 + fr]
+  float* Cs = reinterpret_cast<float*>(sm4);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Cs[(wm * 64 + i * 16 + fk * 4 + r) * G4_LDC + wn * 64 + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  epilogue_pass<G4_BM, G4_BN, G4_LDC, G4_NT, PAIR>(Cs, m0, n0, M, a, e, tid);
+}
+
+int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipStream_t s) {
+  ConvGemmArgs a = a0;
+  SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0 && a.N % 4 == 0, "conv_gemm4: layout");
+  SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm4: 16-B alignment");
+  const bool pair = e.kind == EPI_GATE;
+  SVC_REQUIRE(!pair || a.N % 64 == 0, "conv_gemm4: paired epilogue needs N %% 64 == 0");
+  const int M = a.B * a.T_out;
+  a.ntiles_n = cdiv(a.N, G4_BN);
+  a.halo = 0;
+  const int64_t grid = (int64_t)cdiv(M, G4_BM) * a.ntiles_n;
+  SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm4: bad grid");
+  const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
+  static bool attr[2][2] = {};
+  if (!attr[cp64][pair]) {
+    const void* fn = cp64 ? (pair ? (const void*)conv_gemm4_kernel<true, true> : (const void*)conv_gemm4_kernel<true, false>)
+                          : (pair ? (const void*)conv_gemm4_kernel<false, true> : (const void*)conv_gemm4_kernel<false, false>);
+    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G4_LDS));
+    attr[cp64][pair] = true;
+  }
+  const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
+  const int tok = prof_begin(pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>", 2.0 * M * (double)a.N * kreal,
+                             0.0, s);
+  const dim3 g((unsigned)grid), b(G4_NT);
+  const float inv = 1.0f / (float)a.Cp;
+  if (cp64 && pair) hipLaunchKernelGGL((conv_gemm4_kernel<true, true>), g, b, G4_LDS, s, a, e, zpage, inv);
+  else if (cp64) hipLaunchKernelGGL((conv_gemm4_kernel<true, false>), g, b, G4_LDS, s, a, e, zpage, inv);
+  else if (pair) hipLaunchKernelGGL((conv_gemm4_kernel<false, true>), g, b, G4_LDS, s, a, e, zpage, inv);
+  else hipLaunchKernelGGL((conv_gemm4_kernel<false, false>), g, b, G4_LDS, s, a, e, zpage, inv);
+  prof_end(tok, s);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+}  // namespace svc

@@ -115,7 +115,7 @@ def test_fused_layer_vs_oracle(engine, states, cfg, fused, B, T, monkeypatch):
         assert rel_l2(eps, other) < 2e-3
 
 
-@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15"])
+@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15", "20"])
 def test_eps_gemm_variants(engine, golden, variant, monkeypatch):
     """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path)."""
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
