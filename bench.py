@@ -109,6 +109,9 @@ def main():
                     help="content encoder (BASELINE config 5: contentvec = the HuBERT/ContentVec variant)")
     ap.add_argument("--sampler", choices=["plms", "ddpm"], default="plms",
                     help="plms = the reference's fast_inference PLMS (speedup --speedup); ddpm = 1000-step DDPM")
+    ap.add_argument("--content-split", action="store_true",
+                    help="content encoder GEMMs on split-fp16 operands (the precision mode that meets the 1e-3 mel-L1 "
+                         "target in tools/precision_sweep.py)")
     args = ap.parse_args()
 
     dist = DistContext.from_env()
@@ -124,7 +127,8 @@ def main():
         hs = W.make_hubert_state(W.HUBERT_DIMS["contentvec"], seed=0)
     ms = W.make_mapper_state(cfg.mapper, seed=0)
     vs = W.make_vocoder_state(cfg.vocoder, seed=0)
-    eng = SVCEngine(cfg, dist.local_rank, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs)
+    eng = SVCEngine(cfg, dist.local_rank, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs,
+                    content_split=args.content_split)
     fast = args.sampler == "plms"
     pipe = SVCPipeline(eng)
     B = args.batch
@@ -268,7 +272,8 @@ def main():
             "config": {"workload": f"batch={B}/GPU x {args.seconds:g} s synthetic clips, "
                                    + ("Whisper-medium" if hs is None else "HuBERT/ContentVec (layer 9)")
                                    + (f" + PLMS-100 DiffSVC (speedup {args.speedup})" if fast else " + DDPM-1000 DiffSVC")
-                                   + " + BigVGAN, fp16 MFMA operands / fp32 accumulate",
+                                   + " + BigVGAN, fp16 MFMA operands / fp32 accumulate"
+                                   + (", split-fp16 content encoder" if args.content_split else ""),
                        "global_batch": dist.world * B, "seq_len_frames": int((d24.shape[1] + 768 - 1024) // 256 + 1),
                        "parallelism": f"dp{dist.world} (per-utterance shards, RCCL gather)"},
             "roofline": roof, "cpu_baseline": cpu,

@@ -123,6 +123,9 @@ struct EpiArgs {
   // conditioner
   const int* idx_m; const int* idx_l; const int* singer;
   const float* emb_m; const float* emb_l; const float* emb_s; int ld_emb;
+  // split-fp16 operand output ("fp16x3", elementwise.hip f32_to_f16x3): when > 0, out16 also receives the
+  // residual lo = f16(v - hi) at column split16 + n and hi again at 2 * split16 + n
+  int split16;
 };
 
 int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);

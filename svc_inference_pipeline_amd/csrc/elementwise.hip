@@ -9,7 +9,7 @@ namespace svc {
 
 // ============================================================================ LayerNorm
 // utils/whisper_extractor/model.py:29-31 (LayerNorm in fp32), eps 1e-5, biased variance.
-template <typename OutT>
+template <typename OutT, bool SPLIT = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gam,
                                                         const float* __restrict__ bet, OutT* __restrict__ y, int rows,
                                                         int D, int ldy) {
@@ -44,13 +44,24 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   for (int i = 0; i < 16; ++i)
     if (i < per) {
       int c = i * 64 + lane;
-      yr[c] = (OutT)((v[i] - mean) * rstd * gam[c] + bet[c]);
+      const float o = (v[i] - mean) * rstd * gam[c] + bet[c];
+      yr[c] = (OutT)o;
+      if constexpr (SPLIT) {  // split-fp16 operand [hi | lo | hi] (ldy >= 3 D)
+        yr[D + c] = (OutT)(o - (float)yr[c]);
+        yr[2 * D + c] = yr[c];
+      }
     }
 }
 
 int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int rows, int D, int ldy, hipStream_t s) {
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm: D=%d", D);
   hipLaunchKernelGGL(layernorm_kernel<f16>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s) {
+  SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm: D=%d", D);
+  hipLaunchKernelGGL((layernorm_kernel<f16, true>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, 3 * D);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -76,6 +87,51 @@ __global__ void f32_to_f16_kernel(const float* __restrict__ x, int ldx, f16* __r
 int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s) {
   int64_t n = (int64_t)rows * Cpad;
   hipLaunchKernelGGL(f32_to_f16_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, x, ldx, y, ldy, rows, C, Cpad);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+// Split-fp16 operand ("fp16x3"): x f32 [rows][ldx] -> y f16 [rows][3C] = [hi | lo | hi], hi = f16(x),
+// lo = f16(x - hi). A GEMM over these 3C columns against weights packed [W_hi; W_hi; W_lo] (pack_gemm_split3)
+// computes x_hi W_hi + x_lo W_hi + x_hi W_lo: ~19 significand bits instead of fp16's 11, at 3x the MFMA work.
+__global__ void f32_to_f16x3_kernel(const float* __restrict__ x, int ldx, f16* __restrict__ y, int rows, int C) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * C) return;
+  const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
+  const float v = x[(int64_t)r * ldx + c];
+  const f16 hi = f16_sat(v);
+  const f16 lo = (f16)(v - (float)hi);
+  f16* yr = y + (int64_t)r * 3 * C;
+  yr[c] = hi;
+  yr[C + c] = lo;
+  yr[2 * C + c] = hi;
+}
+
+// grouped layout for grouped convolutions: group g's split operand is contiguous, [g][hi | lo | hi] of Cg columns
+__global__ void f32_to_f16x3_grouped_kernel(const float* __restrict__ x, f16* __restrict__ y, int rows, int C, int Cg) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)rows * C) return;
+  const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
+  const int g = c / Cg, j = c - g * Cg;
+  const float v = x[i];
+  const f16 hi = f16_sat(v);
+  f16* yg = y + (int64_t)r * 3 * C + (int64_t)g * 3 * Cg;
+  yg[j] = hi;
+  yg[Cg + j] = (f16)(v - (float)hi);
+  yg[2 * Cg + j] = hi;
+}
+
+int f32_to_f16x3_grouped(const float* x, f16* y, int rows, int C, int Cg, hipStream_t s) {
+  SVC_REQUIRE(C % Cg == 0, "f16x3 grouped: C=%d Cg=%d", C, Cg);
+  const int64_t n = (int64_t)rows * C;
+  hipLaunchKernelGGL(f32_to_f16x3_grouped_kernel, dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, y, rows, C, Cg);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s) {
+  const int64_t n = (int64_t)rows * C;
+  hipLaunchKernelGGL(f32_to_f16x3_kernel, dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, ldx, y, rows, C);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

@@ -107,8 +107,12 @@ struct DftArgs {
 int dft_frames(const DftArgs& a, int B, hipStream_t s);
 int mel_log(const float* spec, int nbins, const float* fb, int n_mels, float* out, int rows, int mode, hipStream_t s);
 int energy_from_mel(const float* mel, int n_mels, float* en, int rows, hipStream_t s);
-int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s);
+int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s,
+                      int split_c);
+int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s);
+int f32_to_f16x3_grouped(const float* x, f16* y, int rows, int C, int Cg, hipStream_t s);
 int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
+int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s);
 int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s);
@@ -131,10 +135,10 @@ int diff_layer(const DiffLayerArgs& a, bool out, hipStream_t s);
 int cp_fragment(const f16* cp16, int ldcp, const float* bdil, int rows, int rows_pad, f16* cpF, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s);
-int hubert_frames5(const float* wav, int B, int64_t n, f16* out, hipStream_t s);
+int hubert_frames5(const float* wav, int B, int64_t n, f16* out, bool split, hipStream_t s);
 int groupnorm_gelu(const float* x, int B, int T, int C, const float* gamma, const float* beta, double* part,
-                   int max_chunks, float2* ss, f16* y, hipStream_t s);
-int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f16* y16, int rows, int D,
+                   int max_chunks, float2* ss, f16* y, bool split, hipStream_t s);
+int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f16* y16, int rows, int D, bool split,
                    hipStream_t s);
 int pack_qkv(const float* q, const float* k, const float* v, f16* qkv, int64_t rows, int D, float scale, hipStream_t s);
 int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double time_step, double floor_hz,
@@ -264,6 +268,9 @@ struct svc_ctx {
   float *fb24 = nullptr, *fb16 = nullptr, *win_mel = nullptr, *win16 = nullptr;
   int n_fft = 1024, hop = 256, n_mels = 100, fs = 24000;
   double fmin = 0, fmax = 12000, f0_min = 65, f0_max = 800;
+  // content encoders in split-fp16 precision ("content.split" = 1 at finalize): every GEMM operand of Whisper /
+  // HuBERT except the attention path is [hi | lo | hi] against [W_hi; W_hi; W_lo] weights (3x MFMA work)
+  bool content_split = false;
   // whisper
   bool has_whisper = false;
   int wD = 0, wH = 0, wL = 0, wctx = 0, wmels = 80;
@@ -385,6 +392,22 @@ int pack_gemm(svc_ctx* c, PackedGemm& g, int N, int Cin, int Cp, int taps, WG wg
   return upload_vec(c, b, &g.bias);
 }
 
+// Split-fp16 packing of a 1-tap GEMM for the [x_hi | x_lo | x_hi] operand of f32_to_f16x3:
+// W'[n] = [f16(w) | f16(w) | f16(w - f16(w))] over K = 3 * Cin.
+template <typename WG, typename BG>
+int pack_gemm_split3(svc_ctx* c, PackedGemm& g, int N, int Cin, WG wget, BG bget, int taps = 1) {
+  return pack_gemm(
+      c, g, N, 3 * Cin, 3 * Cin, taps,
+      [&](int n, int ci, int t) {
+        const int seg = ci / Cin;
+        const float w = wget(n, ci - seg * Cin, t);
+        const float hi = (float)(f16)w;
+        return seg < 2 ? hi : w - hi;
+      },
+      bget);
+}
+
+
 // Conv1d weight [Cout][Cin][k] (optionally weight-normed along dim 0) into a packed GEMM
 int pack_conv1d(svc_ctx* c, PackedGemm& g, const float* w, const float* bias, int Cout, int Cin, int k, int Cp,
                 int dil, int pad, int stride, const std::vector<int>* perm = nullptr, const float* wn_g = nullptr) {
@@ -407,6 +430,19 @@ int pack_conv1d(svc_ctx* c, PackedGemm& g, const float* w, const float* bias, in
         return (float)((double)w[((int64_t)o * Cin + ci) * k + t] * scale[o]);
       },
       [&](int n) { return bias ? bias[src(n)] : 0.0f; });
+  g.tap_mul = dil;
+  g.tap_add = -pad;
+  g.istride = stride;
+  return st;
+}
+
+// Conv1d [Cout][Cin][k] (+ bias) packed for a split-fp16 operand when `split`, else as pack_conv1d
+int pack_conv1d_opt(svc_ctx* c, PackedGemm& g, const float* w, const float* bias, int Cout, int Cin, int k, int Cp,
+                    int dil, int pad, int stride, bool split) {
+  if (!split) return pack_conv1d(c, g, w, bias, Cout, Cin, k, Cp, dil, pad, stride);
+  int st = pack_gemm_split3(
+      c, g, Cout, Cin, [&](int n, int ci, int t) { return w[((int64_t)n * Cin + ci) * k + t]; },
+      [&](int n) { return bias ? bias[n] : 0.0f; }, k);
   g.tap_mul = dil;
   g.tap_add = -pad;
   g.istride = stride;
@@ -533,9 +569,11 @@ int build_whisper(svc_ctx* c) {
   GETP(c1b, "whisper.encoder.conv1.bias", D);
   GETP(c2w, "whisper.encoder.conv2.weight", D, D, 3);
   GETP(c2b, "whisper.encoder.conv2.bias", D);
-  int st = pack_conv1d(c, c->wconv1, c1w->host, c1b->host, D, nm, 3, (int)round_up(nm, 8), 1, 1, 1);
+  const bool sp = c->content_split;
+  SVC_REQUIRE(!sp || nm % 8 == 0, "whisper split precision: n_mels %d", nm);
+  int st = pack_conv1d_opt(c, c->wconv1, c1w->host, c1b->host, D, nm, 3, (int)round_up(nm, 8), 1, 1, 1, sp);
   if (st) return st;
-  st = pack_conv1d(c, c->wconv2, c2w->host, c2b->host, D, D, 3, D, 1, 1, 2);
+  st = pack_conv1d_opt(c, c->wconv2, c2w->host, c2b->host, D, D, 3, D, 1, 1, 2, sp);
   if (st) return st;
   if ((st = upload_param(c, pos, &c->wpos))) return st;
   c->wblocks.resize(L);
@@ -557,17 +595,17 @@ int build_whisper(svc_ctx* c) {
     GETP(f1b, p + "mlp.0.bias", 4 * D);
     GETP(f2w, p + "mlp.2.weight", D, 4 * D);
     GETP(f2b, p + "mlp.2.bias", D);
-    st = pack_gemm(
-        c, b.qkv, 3 * D, D, D, 1,
-        [&](int n, int ci, int) {
-          const Param* w = n < D ? qw : (n < 2 * D ? kw : vw);
-          return w->host[(int64_t)(n % D) * D + ci];
-        },
-        [&](int n) { return n < D ? qb->host[n] : (n < 2 * D ? 0.0f : vb->host[n - 2 * D]); });
+    auto qkv_w = [&](int n, int ci, int) {
+      const Param* w = n < D ? qw : (n < 2 * D ? kw : vw);
+      return w->host[(int64_t)(n % D) * D + ci];
+    };
+    auto qkv_b = [&](int n) { return n < D ? qb->host[n] : (n < 2 * D ? 0.0f : vb->host[n - 2 * D]); };
+    st = sp ? pack_gemm_split3(c, b.qkv, 3 * D, D, qkv_w, qkv_b) : pack_gemm(c, b.qkv, 3 * D, D, D, 1, qkv_w, qkv_b);
     if (st) return st;
+    // the attention output (A of `out`) stays fp16: the attention kernel's P.V path is fp16 either way
     if ((st = pack_conv1d(c, b.out, ow->host, ob->host, D, D, 1, D, 1, 0, 1))) return st;
-    if ((st = pack_conv1d(c, b.fc1, f1w->host, f1b->host, 4 * D, D, 1, D, 1, 0, 1))) return st;
-    if ((st = pack_conv1d(c, b.fc2, f2w->host, f2b->host, D, 4 * D, 1, 4 * D, 1, 0, 1))) return st;
+    if ((st = pack_conv1d_opt(c, b.fc1, f1w->host, f1b->host, 4 * D, D, 1, D, 1, 0, 1, sp))) return st;
+    if ((st = pack_conv1d_opt(c, b.fc2, f2w->host, f2b->host, D, 4 * D, 1, 4 * D, 1, 0, 1, sp))) return st;
     if ((st = upload_param(c, l1g, &b.ln1_g)) || (st = upload_param(c, l1b, &b.ln1_b)) ||
         (st = upload_param(c, l2g, &b.ln2_g)) || (st = upload_param(c, l2b, &b.ln2_b)))
       return st;
@@ -600,16 +638,29 @@ int build_hubert(svc_ctx* c) {
   c->hconv.assign(7, PackedGemm());
   c->hconv_k = {10, 3, 3, 3, 3, 2, 2};
   c->hconv_s = {5, 2, 2, 2, 2, 2, 2};
-  st = pack_gemm(
-      c, c->hconv[0], Cc, 5, 8, 2, [&](int n, int ci, int t) { return c0->host[(int64_t)n * 10 + t * 5 + ci]; },
-      [&](int) { return 0.0f; });
+  const bool sp = c->content_split;
+  if (sp)  // split-fp16 frames rows [hi(5) | lo(5) | hi(5) | 0] against [W_hi | W_hi | W_lo | 0] per tap
+    st = pack_gemm(
+        c, c->hconv[0], Cc, 16, 16, 2,
+        [&](int n, int ci, int t) {
+          if (ci >= 15) return 0.0f;
+          const int seg = ci / 5;
+          const float w = c0->host[(int64_t)n * 10 + t * 5 + (ci - seg * 5)];
+          const float hi = (float)(f16)w;
+          return seg < 2 ? hi : w - hi;
+        },
+        [&](int) { return 0.0f; });
+  else
+    st = pack_gemm(
+        c, c->hconv[0], Cc, 5, 8, 2, [&](int n, int ci, int t) { return c0->host[(int64_t)n * 10 + t * 5 + ci]; },
+        [&](int) { return 0.0f; });
   if (st) return st;
   c->hconv[0].tap_mul = 1;
   c->hconv[0].tap_add = 0;
   c->hconv[0].istride = 1;
   for (int i = 1; i < 7; ++i) {
     GETP(w, "hubert.feature_extractor.conv_layers." + std::to_string(i) + ".0.weight", Cc, Cc, c->hconv_k[i]);
-    if ((st = pack_conv1d(c, c->hconv[i], w->host, nullptr, Cc, Cc, c->hconv_k[i], Cc, 1, 0, 2))) return st;
+    if ((st = pack_conv1d_opt(c, c->hconv[i], w->host, nullptr, Cc, Cc, c->hconv_k[i], Cc, 1, 0, 2, sp))) return st;
   }
   GETP(gng, "hubert.feature_extractor.conv_layers.0.2.weight", Cc);
   GETP(gnb, "hubert.feature_extractor.conv_layers.0.2.bias", Cc);
@@ -619,7 +670,7 @@ int build_hubert(svc_ctx* c) {
   if ((st = upload_param(c, gng, &c->hgn_g)) || (st = upload_param(c, gnb, &c->hgn_b)) ||
       (st = upload_param(c, lng, &c->hln_g)) || (st = upload_param(c, lnb, &c->hln_b)))
     return st;
-  if ((st = pack_conv1d(c, c->hproj, pw->host, pb->host, D, Cc, 1, Cc, 1, 0, 1))) return st;
+  if ((st = pack_conv1d_opt(c, c->hproj, pw->host, pb->host, D, Cc, 1, Cc, 1, 0, 1, sp))) return st;
   // pos_conv: weight_norm(dim=2) -> w[o][i][k] = g[k] * v[o][i][k] / ||v[:, :, k]||; one GEMM per group
   GETP(pv, "hubert.encoder.pos_conv.0.weight_v", D, -1, -1);
   const int Cg = (int)pv->shape[1], kp = (int)pv->shape[2];
@@ -639,12 +690,11 @@ int build_hubert(svc_ctx* c) {
   }
   c->hpos.assign(c->hPosG, PackedGemm());
   for (int gi = 0; gi < c->hPosG; ++gi) {
-    st = pack_gemm(
-        c, c->hpos[gi], Cg, Cg, Cg, kp,
-        [&](int n, int ci, int t) {
-          return (float)((double)pv->host[((int64_t)(gi * Cg + n) * Cg + ci) * kp + t] * kscale[t]);
-        },
-        [&](int n) { return pcb->host[gi * Cg + n]; });
+    auto pw_ = [&](int n, int ci, int t) {
+      return (float)((double)pv->host[((int64_t)(gi * Cg + n) * Cg + ci) * kp + t] * kscale[t]);
+    };
+    auto pb_ = [&](int n) { return pcb->host[gi * Cg + n]; };
+    st = sp ? pack_gemm_split3(c, c->hpos[gi], Cg, Cg, pw_, pb_, kp) : pack_gemm(c, c->hpos[gi], Cg, Cg, Cg, kp, pw_, pb_);
     if (st) return st;
     c->hpos[gi].tap_mul = 1;
     c->hpos[gi].tap_add = -kp / 2;  // padding k/2, SamePad drops the extra last frame
@@ -674,17 +724,17 @@ int build_hubert(svc_ctx* c) {
     GETP(f1b, p + "fc1.bias", Fd);
     GETP(f2w, p + "fc2.weight", D, Fd);
     GETP(f2b, p + "fc2.bias", D);
-    st = pack_gemm(
-        c, b.qkv, 3 * D, D, D, 1,
-        [&](int n, int ci, int) {
-          const Param* w = n < D ? qw : (n < 2 * D ? kw : vw);
-          return w->host[(int64_t)(n % D) * D + ci];
-        },
-        [&](int n) { return n < D ? qb->host[n] : (n < 2 * D ? kb->host[n - D] : vb->host[n - 2 * D]); });
+    auto qkv_w = [&](int n, int ci, int) {
+      const Param* w = n < D ? qw : (n < 2 * D ? kw : vw);
+      return w->host[(int64_t)(n % D) * D + ci];
+    };
+    auto qkv_b = [&](int n) { return n < D ? qb->host[n] : (n < 2 * D ? kb->host[n - D] : vb->host[n - 2 * D]); };
+    st = sp ? pack_gemm_split3(c, b.qkv, 3 * D, D, qkv_w, qkv_b) : pack_gemm(c, b.qkv, 3 * D, D, D, 1, qkv_w, qkv_b);
     if (st) return st;
-    if ((st = pack_conv1d(c, b.out, ow->host, ob->host, D, D, 1, D, 1, 0, 1))) return st;
-    if ((st = pack_conv1d(c, b.fc1, f1w->host, f1b->host, Fd, D, 1, D, 1, 0, 1))) return st;
-    if ((st = pack_conv1d(c, b.fc2, f2w->host, f2b->host, D, Fd, 1, (int)round_up(Fd, 8), 1, 0, 1))) return st;
+    if ((st = pack_conv1d(c, b.out, ow->host, ob->host, D, D, 1, D, 1, 0, 1))) return st;  // A = attention output (fp16)
+    SVC_REQUIRE(Fd % 8 == 0, "hubert: ffn width %d", Fd);
+    if ((st = pack_conv1d_opt(c, b.fc1, f1w->host, f1b->host, Fd, D, 1, D, 1, 0, 1, sp))) return st;
+    if ((st = pack_conv1d_opt(c, b.fc2, f2w->host, f2b->host, D, Fd, 1, Fd, 1, 0, 1, sp))) return st;
     if ((st = upload_param(c, l1g, &b.ln1_g)) || (st = upload_param(c, l1b, &b.ln1_b)) ||
         (st = upload_param(c, l2g, &b.ln2_g)) || (st = upload_param(c, l2b, &b.ln2_b)))
       return st;
@@ -692,7 +742,7 @@ int build_hubert(svc_ctx* c) {
   GETP(fw, "hubert.final_proj.weight", -1, D);
   c->hFinal = (int)fw->shape[0];
   GETP(fb, "hubert.final_proj.bias", c->hFinal);
-  if ((st = pack_conv1d(c, c->hfinal, fw->host, fb->host, c->hFinal, D, 1, D, 1, 0, 1))) return st;
+  if ((st = pack_conv1d_opt(c, c->hfinal, fw->host, fb->host, c->hFinal, D, 1, D, 1, 0, 1, sp))) return st;
   c->has_hubert = true;
   return SVC_OK;
 }
@@ -840,9 +890,11 @@ int build_mapper(svc_ctx* c) {
       });
   if (st) return st;
   const int cond_sz = (int)cpw[0]->shape[1];
-  // all 20 conditioner projections as one GEMM (loop-invariant over diffusion steps: hoisted)
-  st = pack_gemm(
-      c, c->cp_all, NL * 2 * C, cond_sz, cond_sz, 1,
+  // all 20 conditioner projections as one GEMM (loop-invariant over diffusion steps: hoisted), in split-fp16
+  // precision: it runs once per batch, and its rounding is the largest single denoiser-side term of the
+  // mel-L1 error (precision sweep)
+  st = pack_gemm_split3(
+      c, c->cp_all, NL * 2 * C, cond_sz,
       [&](int n, int ci, int) {
         int layer = n / (2 * C), o = perm[n % (2 * C)];
         return cpw[layer]->host[(int64_t)o * cond_sz + ci];
@@ -1116,6 +1168,7 @@ svc_status svc_ctx_finalize(svc_ctx* c) {
     any_m |= kv.first.rfind("mapper.", 0) == 0;
     any_v |= kv.first.rfind("vocoder.", 0) == 0;
   }
+  c->content_split = cfgv(c, "content.split", 0) != 0;
   if (any_w && (st = build_whisper(c))) return st;
   if (any_h && (st = build_hubert(c))) return st;
   if (any_m && (st = build_mapper(c))) return st;
@@ -1260,14 +1313,15 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   SVC_REQUIRE(L * 2 == F, "whisper: n_ctx %d != 1500", L);
   const int nb = 201;
   const size_t rows1 = (size_t)B * F, rows2 = (size_t)B * L;
-  size_t need = rows1 * nb * 4 + rows1 * c->wmels * 4 + rows1 * c->wmels * 2 + rows1 * D * 2 /*h1*/ + rows2 * D * 4 +
-                rows2 * D * 2 + rows2 * 3 * D * 2 + rows2 * D * 2 + rows2 * 4 * D * 2 + 64 * 4096;
+  const int X3 = c->content_split ? 3 : 1;  // split-fp16 operands are [hi | lo | hi] rows
+  size_t need = rows1 * nb * 4 + rows1 * c->wmels * 4 + rows1 * c->wmels * 2 * X3 + rows1 * D * 2 * X3 /*h1*/ +
+                rows2 * D * 4 + rows2 * D * 2 * X3 + rows2 * 3 * D * 2 + rows2 * D * 2 + rows2 * 4 * D * 2 * X3 + 64 * 4096;
   int st;
   if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
   c->ws.reset();
   WS_GET(float, spec, rows1 * nb);
   WS_GET(float, ls, rows1 * c->wmels);
-  WS_GET(f16, lm16, rows1 * c->wmels);
+  WS_GET(f16, lm16, rows1 * c->wmels * X3);
   WS_GET(float, mx, B);
   DftArgs a{};
   a.wav = wav16;
@@ -1284,14 +1338,15 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   a.out = spec;
   if ((st = dft_frames(a, B, s))) return st;
   if ((st = mel_log(spec, nb, c->fb16, c->wmels, ls, (int)rows1, 1, s))) return st;
-  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s))) return st;
+  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s, X3 == 3 ? c->wmels : 0))) return st;
   // conv stem
-  WS_GET(f16, h1, rows1 * D);
+  WS_GET(f16, h1, rows1 * D * X3);
   EpiArgs e = epi();
   e.act = ACT_GELU;
   e.out16 = h1;
-  e.ld16 = D;
-  if ((st = run_gemm(c->wconv1, lm16, c->wmels, c->wmels, B, F, F, e, s, "whisper.conv1"))) return st;
+  e.ld16 = D * X3;
+  e.split16 = X3 == 3 ? D : 0;
+  if ((st = run_gemm(c->wconv1, lm16, c->wmels * X3, c->wmels * X3, B, F, F, e, s, "whisper.conv1"))) return st;
   WS_GET(float, x, rows2 * D);
   e = epi();
   e.act = ACT_GELU;
@@ -1299,21 +1354,24 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   e.ld_add_t = D;
   e.out32 = x;
   e.ld32 = D;
-  if ((st = run_gemm(c->wconv2, h1, D, D, B, F, L, e, s, "whisper.conv2"))) return st;
-  WS_GET(f16, n16, rows2 * D);
+  if ((st = run_gemm(c->wconv2, h1, D * X3, D * X3, B, F, L, e, s, "whisper.conv2"))) return st;
+  WS_GET(f16, n16, rows2 * D * X3);
   WS_GET(f16, qkv, rows2 * 3 * D);
   WS_GET(f16, o16, rows2 * D);
-  WS_GET(f16, h16, rows2 * 4 * D);
+  WS_GET(f16, h16, rows2 * 4 * D * X3);
   const float qk_scale = powf((float)(D / c->wH), -0.25f);
+  auto ln16 = [&](const float* g, const float* b) {
+    return X3 == 3 ? layernorm_f16x3(x, g, b, n16, (int)rows2, D, s) : layernorm_f16(x, g, b, n16, (int)rows2, D, D, s);
+  };
   for (int i = 0; i < c->wL; ++i) {
     WBlock& b = c->wblocks[i];
-    if ((st = layernorm_f16(x, b.ln1_g, b.ln1_b, n16, (int)rows2, D, D, s))) return st;
+    if ((st = ln16(b.ln1_g, b.ln1_b))) return st;
     e = epi();
     e.out16 = qkv;
     e.ld16 = 3 * D;
     e.scale_cols = 2 * D;
     e.col_scale = qk_scale;
-    if ((st = run_gemm(b.qkv, n16, D, D, B, L, L, e, s, "whisper.qkv"))) return st;
+    if ((st = run_gemm(b.qkv, n16, D * X3, D * X3, B, L, L, e, s, "whisper.qkv"))) return st;
     if ((st = attention(qkv, o16, B, L, D, s))) return st;
     e = epi();
     e.add_row = x;
@@ -1321,18 +1379,19 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
     e.out32 = x;
     e.ld32 = D;
     if ((st = run_gemm(b.out, o16, D, D, B, L, L, e, s, "whisper.out"))) return st;
-    if ((st = layernorm_f16(x, b.ln2_g, b.ln2_b, n16, (int)rows2, D, D, s))) return st;
+    if ((st = ln16(b.ln2_g, b.ln2_b))) return st;
     e = epi();
     e.act = ACT_GELU;
     e.out16 = h16;
-    e.ld16 = 4 * D;
-    if ((st = run_gemm(b.fc1, n16, D, D, B, L, L, e, s, "whisper.fc1"))) return st;
+    e.ld16 = 4 * D * X3;
+    e.split16 = X3 == 3 ? 4 * D : 0;
+    if ((st = run_gemm(b.fc1, n16, D * X3, D * X3, B, L, L, e, s, "whisper.fc1"))) return st;
     e = epi();
     e.add_row = x;
     e.ld_add_row = D;
     e.out32 = x;
     e.ld32 = D;
-    if ((st = run_gemm(b.fc2, h16, 4 * D, 4 * D, B, L, L, e, s, "whisper.fc2"))) return st;
+    if ((st = run_gemm(b.fc2, h16, 4 * D * X3, 4 * D * X3, B, L, L, e, s, "whisper.fc2"))) return st;
   }
   return layernorm_f32(x, c->wlnp_g, c->wlnp_b, feats, (int)rows2, D, D, s);
 }
@@ -1370,31 +1429,34 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
   for (int i = 0; i <= 7; ++i) t[i] = hubert_len(n, i);  // t[0] = n samples, t[7] = frames
   const int Cc = c->hC, D = c->hD, F = (int)F64;
   const int Fd = c->hblocks[0].fc1.N;
+  const bool sp = c->content_split;
+  const int X3 = sp ? 3 : 1;  // split-fp16 operands are [hi | lo | hi] rows
+  const int w5 = sp ? 16 : 8;
   const int64_t R5 = cdiv64(n, 5);
   const size_t rows0 = (size_t)B * t[1], rowsF = (size_t)B * F;
   const int kChunks = 64;
-  size_t need = (size_t)B * R5 * 8 * 2 + rows0 * Cc * 4 + rows0 * Cc * 2 + (size_t)B * kChunks * Cc * 16 +
-                (size_t)B * Cc * 8 + (size_t)B * (t[2] + t[3]) * Cc * 2 + rowsF * Cc * 6 + rowsF * D * 6 +
-                rowsF * 3 * D * 2 + rowsF * D * 2 + rowsF * Fd * 2 + 32 * 4096;
+  size_t need = (size_t)B * R5 * w5 * 2 + rows0 * Cc * 4 + rows0 * Cc * 2 * X3 + (size_t)B * kChunks * Cc * 16 +
+                (size_t)B * Cc * 8 + (size_t)B * (t[2] + t[3]) * Cc * 2 * X3 + rowsF * Cc * (4 + 2 * X3) +
+                rowsF * D * (4 + 2 * X3) + rowsF * 3 * D * 2 + rowsF * D * 2 + rowsF * Fd * 2 * X3 + 32 * 4096;
   int st;
   if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
   c->ws.reset();
   // ---- feature extractor (wav2vec2 ConvFeatureExtractionModel, mode "default")
-  WS_GET(f16, f5, (size_t)B * R5 * 8);
+  WS_GET(f16, f5, (size_t)B * R5 * w5);
   WS_GET(float, c0, rows0 * Cc);
-  WS_GET(f16, g16, rows0 * Cc);
+  WS_GET(f16, g16, rows0 * Cc * X3);
   WS_GET(double, part, (size_t)B * kChunks * Cc * 2);
   WS_GET(float2, gss, (size_t)B * Cc);
-  WS_GET(f16, pa, (size_t)B * t[2] * Cc);
-  WS_GET(f16, pb, (size_t)B * t[3] * Cc);
+  WS_GET(f16, pa, (size_t)B * t[2] * Cc * X3);
+  WS_GET(f16, pb, (size_t)B * t[3] * Cc * X3);
   WS_GET(float, c6, rowsF * Cc);
-  WS_GET(f16, ln16, rowsF * Cc);
-  if ((st = hubert_frames5(wav16, B, n, f5, s))) return st;
+  WS_GET(f16, ln16, rowsF * Cc * X3);
+  if ((st = hubert_frames5(wav16, B, n, f5, sp, s))) return st;
   EpiArgs e = epi();
   e.out32 = c0;
   e.ld32 = Cc;
-  if ((st = run_gemm(c->hconv[0], f5, 8, 8, B, (int)R5, (int)t[1], e, s, "hubert.conv0"))) return st;
-  if ((st = groupnorm_gelu(c0, B, (int)t[1], Cc, c->hgn_g, c->hgn_b, part, kChunks, gss, g16, s))) return st;
+  if ((st = run_gemm(c->hconv[0], f5, w5, w5, B, (int)R5, (int)t[1], e, s, "hubert.conv0"))) return st;
+  if ((st = groupnorm_gelu(c0, B, (int)t[1], Cc, c->hgn_g, c->hgn_b, part, kChunks, gss, g16, sp, s))) return st;
   const f16* in = g16;
   for (int i = 1; i < 7; ++i) {
     e = epi();
@@ -1404,23 +1466,29 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
       e.ld32 = Cc;
     } else {
       e.out16 = (i & 1) ? pa : pb;
-      e.ld16 = Cc;
+      e.ld16 = Cc * X3;
+      e.split16 = sp ? Cc : 0;
     }
-    if ((st = run_gemm(c->hconv[i], in, Cc, Cc, B, (int)t[i], (int)t[i + 1], e, s, "hubert.convs"))) return st;
+    if ((st = run_gemm(c->hconv[i], in, Cc * X3, Cc * X3, B, (int)t[i], (int)t[i + 1], e, s, "hubert.convs"))) return st;
     in = e.out16;
   }
   // ---- HubertModel.forward_features tail: LayerNorm(C) -> post_extract_proj
-  if ((st = layernorm_f16(c6, c->hln_g, c->hln_b, ln16, (int)rowsF, Cc, Cc, s))) return st;
+  if ((st = sp ? layernorm_f16x3(c6, c->hln_g, c->hln_b, ln16, (int)rowsF, Cc, s)
+               : layernorm_f16(c6, c->hln_g, c->hln_b, ln16, (int)rowsF, Cc, Cc, s)))
+    return st;
   WS_GET(float, x, rowsF * D);
-  WS_GET(f16, x16, rowsF * D);
+  WS_GET(f16, x16, rowsF * D * X3);
   e = epi();
   e.out32 = x;
   e.ld32 = D;
-  e.out16 = x16;
-  e.ld16 = D;
-  if ((st = run_gemm(c->hproj, ln16, Cc, Cc, B, F, F, e, s, "hubert.proj"))) return st;
+  if (!sp) {
+    e.out16 = x16;
+    e.ld16 = D;
+  }
+  if ((st = run_gemm(c->hproj, ln16, Cc * X3, Cc * X3, B, F, F, e, s, "hubert.proj"))) return st;
   // ---- TransformerEncoder: x += GELU(pos_conv(x)) per group, then LayerNorm (layer_norm_first = False)
   const int Cg = D / c->hPosG;
+  if (sp && (st = f32_to_f16x3_grouped(x, x16, (int)rowsF, D, Cg, s))) return st;  // group g: [hi | lo | hi] x Cg
   for (int gi = 0; gi < c->hPosG; ++gi) {
     e = epi();
     e.act = ACT_GELU;
@@ -1428,12 +1496,13 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
     e.ld_add_row = D;
     e.out32 = x + gi * Cg;
     e.ld32 = D;
-    if ((st = run_gemm(c->hpos[gi], x16 + gi * Cg, D, Cg, B, F, F, e, s, "hubert.pos_conv"))) return st;
+    if ((st = run_gemm(c->hpos[gi], x16 + (size_t)gi * Cg * X3, D * X3, Cg * X3, B, F, F, e, s, "hubert.pos_conv")))
+      return st;
   }
-  if ((st = layernorm_dual(x, c->henc_ln_g, c->henc_ln_b, x, x16, (int)rowsF, D, s))) return st;
+  if ((st = layernorm_dual(x, c->henc_ln_g, c->henc_ln_b, x, x16, (int)rowsF, D, sp, s))) return st;
   WS_GET(f16, qkv, rowsF * 3 * D);
   WS_GET(f16, o16, rowsF * D);
-  WS_GET(f16, h16, rowsF * Fd);
+  WS_GET(f16, h16, rowsF * Fd * X3);
   const float qk_scale = powf(64.0f, -0.25f);  // q * dh^-1/2 split over q and k
   for (int i = 0; i < c->hLayers; ++i) {
     HBlock& b = c->hblocks[i];
@@ -1442,7 +1511,7 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
     e.ld16 = 3 * D;
     e.scale_cols = 2 * D;
     e.col_scale = qk_scale;
-    if ((st = run_gemm(b.qkv, x16, D, D, B, F, F, e, s, "hubert.qkv"))) return st;
+    if ((st = run_gemm(b.qkv, x16, D * X3, D * X3, B, F, F, e, s, "hubert.qkv"))) return st;
     if ((st = attention(qkv, o16, B, F, D, s))) return st;
     e = epi();
     e.add_row = x;
@@ -1450,24 +1519,25 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
     e.out32 = x;
     e.ld32 = D;
     if ((st = run_gemm(b.out, o16, D, D, B, F, F, e, s, "hubert.out"))) return st;
-    if ((st = layernorm_dual(x, b.ln1_g, b.ln1_b, x, x16, (int)rowsF, D, s))) return st;
+    if ((st = layernorm_dual(x, b.ln1_g, b.ln1_b, x, x16, (int)rowsF, D, sp, s))) return st;
     e = epi();
     e.act = ACT_GELU;
     e.out16 = h16;
-    e.ld16 = Fd;
-    if ((st = run_gemm(b.fc1, x16, D, D, B, F, F, e, s, "hubert.fc1"))) return st;
+    e.ld16 = Fd * X3;
+    e.split16 = sp ? Fd : 0;
+    if ((st = run_gemm(b.fc1, x16, D * X3, D * X3, B, F, F, e, s, "hubert.fc1"))) return st;
     e = epi();
     e.add_row = x;
     e.ld_add_row = D;
     e.out32 = x;
     e.ld32 = D;
-    if ((st = run_gemm(b.fc2, h16, Fd, Fd, B, F, F, e, s, "hubert.fc2"))) return st;
-    if ((st = layernorm_dual(x, b.ln2_g, b.ln2_b, x, x16, (int)rowsF, D, s))) return st;
+    if ((st = run_gemm(b.fc2, h16, Fd * X3, Fd * X3, B, F, F, e, s, "hubert.fc2"))) return st;
+    if ((st = layernorm_dual(x, b.ln2_g, b.ln2_b, x, x16, (int)rowsF, D, sp, s))) return st;
   }
   e = epi();
   e.out32 = feats;
   e.ld32 = c->hFinal;
-  return run_gemm(c->hfinal, x16, D, D, B, F, F, e, s, "hubert.final_proj");
+  return run_gemm(c->hfinal, x16, D * X3, D * X3, B, F, F, e, s, "hubert.final_proj");
 }
 
 int64_t svc_hubert_frames(int64_t n_samples) { return hubert_len(n_samples, 7); }
@@ -1648,13 +1718,13 @@ static int fragment_cp(svc_ctx* c, const DenoiseBufs& bb, int rows, hipStream_t 
 
 static int project_cond(svc_ctx* c, const float* cond, int B, int T, const DenoiseBufs& bb, hipStream_t s) {
   const int rows = B * T, C = c->C;
-  WS_GET(f16, cond16, (size_t)rows * C);
+  WS_GET(f16, cond16, (size_t)rows * 3 * C);
   int st;
-  if ((st = f32_to_f16(cond, C, cond16, C, rows, C, C, s))) return st;
+  if ((st = f32_to_f16x3(cond, C, cond16, rows, C, s))) return st;  // [hi | lo | hi] split-fp16 operand
   EpiArgs e = epi();
   e.out16 = bb.cp16;
   e.ld16 = c->n_layers * 2 * C;
-  return run_gemm(c->cp_all, cond16, C, C, B, T, T, e, s, "diffsvc.condproj");
+  return run_gemm(c->cp_all, cond16, 3 * C, 3 * C, B, T, T, e, s, "diffsvc.condproj");
 }
 
 svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B, int T, int t, float* eps,
@@ -1665,7 +1735,7 @@ svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B,
   hipStream_t s = (hipStream_t)stream;
   const int rows = B * T, ld16 = (int)round_up(c->n_mel, 8);
   int st;
-  if ((st = c->ws.reserve(std::max(denoise_bytes(c, B, T) + (size_t)rows * (ld16 * 2 + c->C * 2) + 8192, c->ws.cap))))
+  if ((st = c->ws.reserve(std::max(denoise_bytes(c, B, T) + (size_t)rows * (ld16 * 2 + c->C * 6) + 8192, c->ws.cap))))
     return st;
   c->ws.reset();
   DenoiseBufs bb;
@@ -1687,7 +1757,7 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
   hipStream_t s = (hipStream_t)stream;
   const int rows = B * T, nm = c->n_mel, ld16 = (int)round_up(nm, 8);
   int st;
-  const size_t extra = (size_t)rows * (ld16 * 2 * 2 + nm * 4 * 8 + c->C * 2) + 32 * 4096;
+  const size_t extra = (size_t)rows * (ld16 * 2 * 2 + nm * 4 * 8 + c->C * 6) + 32 * 4096;
   if ((st = c->ws.reserve(std::max(denoise_bytes(c, B, T) + extra, c->ws.cap)))) return st;
   c->ws.reset();
   DenoiseBufs bb;

@@ -67,6 +67,13 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
         union { uint2 u; f16 h[4]; } pk;
         pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
         *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
+        if (e.split16) {
+          union { uint2 u; f16 h[4]; } lo;
+          lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);
+          lo.h[2] = (f16)(w.z - (float)pk.h[2]); lo.h[3] = (f16)(w.w - (float)pk.h[3]);
+          *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + e.split16 + n) = lo.u;
+          *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + 2 * e.split16 + n) = pk.u;
+        }
       }
     }
   } else {

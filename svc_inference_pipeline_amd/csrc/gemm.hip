@@ -193,7 +193,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
           if (e.acc_div != 1.0f) v = v / e.acc_div;
         }
         if (e.out32) e.out32[orow * e.ld32 + n] = v;
-        if (e.out16) e.out16[orow * e.ld16 + n] = f16_sat(e.add16 ? v + e.add16[n] : v);
+        if (e.out16) {
+          const float w = e.add16 ? v + e.add16[n] : v;
+          const f16 hi = f16_sat(w);
+          e.out16[orow * e.ld16 + n] = hi;
+          if (e.split16) {
+            e.out16[orow * e.ld16 + e.split16 + n] = (f16)(w - (float)hi);
+            e.out16[orow * e.ld16 + 2 * e.split16 + n] = hi;
+          }
+        }
       }
     }
   }

@@ -13,23 +13,38 @@
 
 namespace svc {
 
+// SPLIT: 16 halves per row = [hi(5) | lo(5) | hi(5) | 0] (split-fp16 operand of the split-packed conv_layers[0])
+template <bool SPLIT>
 __global__ void frames5_kernel(const float* __restrict__ wav, int64_t n, int64_t rows, f16* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one output row (8 halves = 16 B)
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one output row (8 or 16 halves)
   const int b = blockIdx.y;
   if (i >= rows) return;
   const float* w = wav + (int64_t)b * n;
-  union { uint4 u; f16 h[8]; } pk;
+  constexpr int W = SPLIT ? 16 : 8;
+  union { uint4 u[W / 8]; f16 h[W]; } pk;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < W; ++j) pk.h[j] = (f16)0.0f;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
     const int64_t k = 5 * i + j;
-    pk.h[j] = (j < 5 && k < n) ? (f16)w[k] : (f16)0.0f;
+    const float v = k < n ? w[k] : 0.0f;
+    const f16 hi = (f16)v;
+    pk.h[j] = hi;
+    if constexpr (SPLIT) {
+      pk.h[5 + j] = (f16)(v - (float)hi);
+      pk.h[10 + j] = hi;
+    }
   }
-  *reinterpret_cast<uint4*>(out + ((int64_t)b * rows + i) * 8) = pk.u;
+#pragma unroll
+  for (int q = 0; q < W / 8; ++q) *reinterpret_cast<uint4*>(out + ((int64_t)b * rows + i) * W + q * 8) = pk.u[q];
 }
 
-int hubert_frames5(const float* wav, int B, int64_t n, f16* out, hipStream_t s) {
+int hubert_frames5(const float* wav, int B, int64_t n, f16* out, bool split, hipStream_t s) {
   const int64_t rows = cdiv64(n, 5);
-  hipLaunchKernelGGL(frames5_kernel, dim3(cdiv(rows, 256), B), dim3(256), 0, s, wav, n, rows, out);
+  if (split)
+    hipLaunchKernelGGL(frames5_kernel<true>, dim3(cdiv(rows, 256), B), dim3(256), 0, s, wav, n, rows, out);
+  else
+    hipLaunchKernelGGL(frames5_kernel<false>, dim3(cdiv(rows, 256), B), dim3(256), 0, s, wav, n, rows, out);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -80,6 +95,7 @@ __global__ void gn_finalize_kernel(const double* __restrict__ part, int nck, int
   ss[(int64_t)b * C + c] = make_float2(scale, be[c] - (float)mean * scale);
 }
 
+template <bool SPLIT>
 __global__ void gn_gelu_apply_kernel(const float* __restrict__ x, const float2* __restrict__ ss, f16* __restrict__ y,
                                      int64_t rows_per_utt, int C, int64_t nvec) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one vector of 8 channels
@@ -91,19 +107,28 @@ __global__ void gn_gelu_apply_kernel(const float* __restrict__ x, const float2* 
   const float4 a0 = *reinterpret_cast<const float4*>(x + row * C + c0);
   const float4 a1 = *reinterpret_cast<const float4*>(x + row * C + c0 + 4);
   const float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-  union { uint4 u; f16 h[8]; } pk;
+  union { uint4 u; f16 h[8]; } pk, lo;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float2 t = ss[(int64_t)b * C + c0 + j];
-    pk.h[j] = f16_sat(gelu_erf(v[j] * t.x + t.y));
+    const float o = gelu_erf(v[j] * t.x + t.y);
+    pk.h[j] = f16_sat(o);
+    lo.h[j] = (f16)(o - (float)pk.h[j]);
   }
-  *reinterpret_cast<uint4*>(y + row * C + c0) = pk.u;
+  if constexpr (SPLIT) {  // [hi | lo | hi] rows of 3 C
+    f16* yr = y + row * 3 * C;
+    *reinterpret_cast<uint4*>(yr + c0) = pk.u;
+    *reinterpret_cast<uint4*>(yr + C + c0) = lo.u;
+    *reinterpret_cast<uint4*>(yr + 2 * C + c0) = pk.u;
+  } else {
+    *reinterpret_cast<uint4*>(y + row * C + c0) = pk.u;
+  }
 }
 
 // Fp32GroupNorm(C, C) + GELU over x f32 [B][T][C] -> y f16 [B][T][C]. part: >= B * chunks * C * 2 doubles,
 // ss: B * C float2.
 int groupnorm_gelu(const float* x, int B, int T, int C, const float* gamma, const float* beta, double* part,
-                   int max_chunks, float2* ss, f16* y, hipStream_t s) {
+                   int max_chunks, float2* ss, f16* y, bool split, hipStream_t s) {
   SVC_REQUIRE(C % 8 == 0 && T > 0 && B > 0, "groupnorm: B=%d T=%d C=%d", B, T, C);
   const int chunks = std::max(1, std::min(max_chunks, cdiv(T, 256)));
   const int chunk = cdiv(T, chunks);
@@ -113,14 +138,20 @@ int groupnorm_gelu(const float* x, int B, int T, int C, const float* gamma, cons
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(cdiv(C, 256), B), dim3(256), 0, s, part, nck, T, C, gamma, beta, 1e-5f,
                      ss);
   const int64_t nvec = (int64_t)B * T * C / 8;
-  hipLaunchKernelGGL(gn_gelu_apply_kernel, dim3((unsigned)cdiv64(nvec, 256)), dim3(256), 0, s, x, ss, y, (int64_t)T, C,
-                     nvec);
+  if (split)
+    hipLaunchKernelGGL(gn_gelu_apply_kernel<true>, dim3((unsigned)cdiv64(nvec, 256)), dim3(256), 0, s, x, ss, y,
+                       (int64_t)T, C, nvec);
+  else
+    hipLaunchKernelGGL(gn_gelu_apply_kernel<false>, dim3((unsigned)cdiv64(nvec, 256)), dim3(256), 0, s, x, ss, y,
+                       (int64_t)T, C, nvec);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
 
-// One wave per row (D <= 1024, multiple of 64): y32 and y16 both written (y32 may alias x).
+// One wave per row (D <= 1024, multiple of 64): y32 and y16 both written (y32 may alias x); SPLIT: y16 rows are
+// the split-fp16 operand [hi | lo | hi] of 3 D columns.
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void layernorm_dual_kernel(const float* x, const float* __restrict__ gam,
                                                              const float* __restrict__ bet, float* y32,
                                                              f16* __restrict__ y16, int rows, int D) {
@@ -156,14 +187,25 @@ __global__ __launch_bounds__(256) void layernorm_dual_kernel(const float* x, con
       const int c = i * 64 + lane;
       const float o = (v[i] - mean) * rstd * gam[c] + bet[c];
       y32[(int64_t)row * D + c] = o;
-      y16[(int64_t)row * D + c] = f16_sat(o);
+      const f16 hi = f16_sat(o);
+      if constexpr (SPLIT) {
+        f16* yr = y16 + (int64_t)row * 3 * D;
+        yr[c] = hi;
+        yr[D + c] = (f16)(o - (float)hi);
+        yr[2 * D + c] = hi;
+      } else {
+        y16[(int64_t)row * D + c] = hi;
+      }
     }
 }
 
-int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f16* y16, int rows, int D,
+int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f16* y16, int rows, int D, bool split,
                    hipStream_t s) {
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm_dual: D=%d", D);
-  hipLaunchKernelGGL(layernorm_dual_kernel, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y32, y16, rows, D);
+  if (split)
+    hipLaunchKernelGGL(layernorm_dual_kernel<true>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y32, y16, rows, D);
+  else
+    hipLaunchKernelGGL(layernorm_dual_kernel<false>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y32, y16, rows, D);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

@@ -33,10 +33,12 @@ def mel_frames(n_samples, n_fft=1024, hop=256):
 class SVCEngine:
     """Stages of infer.py on one GPU. `whisper_state`, `mapper_state`, `vocoder_state`, `hubert_state` are dicts
     in the reference's state_dict naming (svc_inference_pipeline_amd.weights; fairseq's for HuBERT); any subset
-    may be given. `hubert_output_layer` is utils/hubert.py:42's output_layer (9)."""
+    may be given. `hubert_output_layer` is utils/hubert.py:42's output_layer (9). `content_split` runs the
+    Whisper / HuBERT GEMMs on split-fp16 operands ([hi | lo | hi] x [W_hi; W_hi; W_lo], ~19 significand bits, 3x the
+    MFMA work) — the content encoder is the largest term of the mel-L1 error (precision sweep)."""
 
     def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None, hubert_state=None,
-                 hubert_output_layer=9):
+                 hubert_output_layer=9, content_split=False):
         _lib.load()
         self.cfg = cfg
         self.device = device
@@ -45,6 +47,7 @@ class SVCEngine:
         _lib.call("svc_ctx_create", device, ctypes.byref(self._ctx))
         self._keep = []
         self._set_config()
+        _lib.call("svc_ctx_set_config", self._ctx, b"content.split", 1.0 if content_split else 0.0)
         if whisper_state is not None:
             self._add_state("whisper.", whisper_state)
             self.whisper_dims = W.whisper_dims_from_state(whisper_state)

@@ -93,17 +93,18 @@ def main():
     if args.gpu:
         from svc_inference_pipeline_amd.pipeline import SVCPipeline
         from svc_inference_pipeline_amd.runtime import SVCEngine
-        e = SVCEngine(cfg, 0, mapper_state=ms, vocoder_state=vs, hubert_state=hs)
-        d = lambda a, t=torch.float32: torch.as_tensor(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
-        noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
-        pipe = SVCPipeline(e)
-        content = pipe.content(d(w16[None]), T, d(w16[None])).float().cpu().numpy()[0]
-        res = pipe.convert(d(w24[None]), d(w16[None]), d(np.array([2]), torch.int32), fast_inference=False,
-                           x_T=d(xT), noise=d(noise), f0=d(f0[None], torch.float64), wav16_float=d(w16[None]))
-        _, mel_d = e.bigvgan(res.x0, return_mel=True)
-        runs["gpu-fp16"] = dict(content=content, x0=res.x0[0].cpu().numpy(), mel=mel_d[0].cpu().numpy(),
-                                wav=res.wav[0].cpu().numpy())
-        e.close()
+        for name, split in (("gpu-fp16", False), ("gpu-fp16, split-fp16 content encoder", True)):
+            e = SVCEngine(cfg, 0, mapper_state=ms, vocoder_state=vs, hubert_state=hs, content_split=split)
+            d = lambda a, t=torch.float32: torch.as_tensor(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
+            noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
+            pipe = SVCPipeline(e)
+            content = pipe.content(d(w16[None]), T, d(w16[None])).float().cpu().numpy()[0]
+            res = pipe.convert(d(w24[None]), d(w16[None]), d(np.array([2]), torch.int32), fast_inference=False,
+                               x_T=d(xT), noise=d(noise), f0=d(f0[None], torch.float64), wav16_float=d(w16[None]))
+            _, mel_d = e.bigvgan(res.x0, return_mel=True)
+            runs[name] = dict(content=content, x0=res.x0[0].cpu().numpy(), mel=mel_d[0].cpu().numpy(),
+                              wav=res.wav[0].cpu().numpy())
+            e.close()
     for name, r in runs.items():
         results[name] = {
             "mel_l1_denorm_ln": float(np.mean(np.abs(r["mel"] - ref["mel"]))),
