@@ -2261,7 +2261,11 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters >= 1, "gemm_bench: bad args");
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
-  float* bias;
+  float *bias, *R = nullptr;
+  if (epi_kind == 2) {  // DiffSVC residual epilogue: x32 read-modify-write + next f16 input
+    SVC_HIP_CHECK(hipMalloc(&R, (size_t)M * N * 4));
+    SVC_HIP_CHECK(hipMemset(R, 0, (size_t)M * N * 4));
+  }
   SVC_HIP_CHECK(hipMalloc(&X, (size_t)M * Cin * 2));
   SVC_HIP_CHECK(hipMalloc(&W, (size_t)Npad * Kpad * 2));
   SVC_HIP_CHECK(hipMalloc(&Y, (size_t)M * N * 2));
@@ -2280,6 +2284,9 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
     e.kind = EPI_GATE; e.cp = cp; e.ld_cp = N; e.y16 = Y; e.ldy16 = N / 2;
   } else {
     e.out16 = Y; e.ld16 = N;
+    if (epi_kind == 2) {
+      e.acc32 = R; e.ld_acc = N; e.acc_div = 1.41421356237309515f; e.out32 = R; e.ld32 = N; e.add16 = bias;
+    }
   }
   hipEvent_t e0, e1;
   SVC_HIP_CHECK(hipEventCreate(&e0));
@@ -2301,6 +2308,6 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   *ms_out = ms / iters;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
-  for (void* p : {(void*)X, (void*)W, (void*)Y, (void*)cp, (void*)bias}) (void)hipFree(p);
+  for (void* p : {(void*)X, (void*)W, (void*)Y, (void*)cp, (void*)bias, (void*)R}) if (p) (void)hipFree(p);
   return st;
 }

@@ -11,6 +11,8 @@ SHAPES = [  # name, M, N, Cin, taps, epi
     ("diffsvc.dilated(gate)", 29984, 768, 384, 3, 1),
     ("diffsvc.dilated(store)", 29984, 768, 384, 3, 0),
     ("diffsvc.outproj(res)", 29984, 384, 384, 1, 0),
+    ("diffsvc.outproj(rmw)", 29984, 384, 384, 1, 2),   # with the real epilogue: f32 residual RMW + next f16 input
+    ("diffsvc.outproj(rmw,sub)", 9995, 384, 384, 1, 2),
     ("diffsvc.skipsum", 29984, 384, 7680, 1, 0),
     ("bigvgan.s2 k11", 32 * 14992, 384, 384, 11, 0),
     ("whisper.fc1", 48000, 4096, 1024, 1, 0),
