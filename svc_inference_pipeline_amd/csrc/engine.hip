@@ -1594,6 +1594,11 @@ struct DenoiseBufs {
   f16* g16;      // [rows][NL*C] gate outputs of every layer (A operand of the skip GEMM)
   f16* s16;      // [rows][C] sum(skip) / sqrt(NL)
   f16* u16;      // [rows][C] relu(skip_projection)
+  size_t cp_ls;  // elements between layers of cp16, which is LAYER-major [NL][rows_total][2C]: each layer's gate
+                 // epilogue reads one contiguous block (row-major over all layers put 30 KB between its rows)
+  size_t g_ls;   // elements between layers of g16, also layer-major [NL][rows_total][C]: the gate GEMM writes and the
+                 // residual GEMM reads one contiguous block; the skip GEMM reads the NL blocks as NL "taps" whose row
+                 // shift is the layer stride (tap_mul = rows_total)
 };
 
 // The fused residual-layer kernel (diff_layer.hip) is opt-in (SVC_DIFF_FUSED=1): owning all 768 gate columns
@@ -1631,8 +1636,8 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
       a.dpn = i + 1 < NL ? dp + (size_t)(i + 1) * C : nullptr;
       a.x32 = bb.h32;
       a.x16n = nxt;
-      a.g16 = bb.g16 + (size_t)i * C;
-      a.ldg = NL * C;
+      a.g16 = bb.g16 + (size_t)i * bb.g_ls;
+      a.ldg = C;
       a.B = B;
       a.T = T;
       a.dil = 1 << (i % c->dil_cycle);
@@ -1645,10 +1650,10 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   for (int i = 0; i < NL && !fused_layers(c); ++i) {
     EpiArgs g = epi();
     g.kind = EPI_GATE;
-    g.cp = bb.cp16 + (size_t)i * 2 * C;
-    g.ld_cp = NL * 2 * C;
-    g.y16 = bb.g16 + (size_t)i * C;
-    g.ldy16 = NL * C;
+    g.cp = bb.cp16 + (size_t)i * bb.cp_ls;
+    g.ld_cp = 2 * C;
+    g.y16 = bb.g16 + (size_t)i * bb.g_ls;
+    g.ldy16 = C;
     if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s, "diffsvc.dilated"))) return st;
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
     // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step)
@@ -1661,7 +1666,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     r.out16 = bb.y16;
     r.ld16 = C;
     r.add16 = dp + (size_t)(i + 1) * C;
-    if ((st = run_gemm(c->outres[i], bb.g16 + (size_t)i * C, NL * C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
+    if ((st = run_gemm(c->outres[i], bb.g16 + (size_t)i * bb.g_ls, C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
   }
   // skip = sum_i skip_i (modules/diffsvc.py:311); x = skip / sqrt(len(layers)) (:315)
   e = epi();
@@ -1669,7 +1674,16 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.col_scale = 1.0f / sqrtf((float)NL);
   e.out16 = bb.s16;
   e.ld16 = C;
-  if ((st = run_gemm(c->skip_all, bb.g16, NL * C, NL * C, B, T, T, e, s, "diffsvc.skipsum"))) return st;
+  {
+    PackedGemm sk = c->skip_all;  // K index l * C + k = "tap" l * Cp + k with Cp = C: same packed weights
+    sk.Cp = C;
+    sk.taps = NL;
+    sk.tap_mul = (int)(bb.g_ls / C);
+    sk.tap_add = 0;
+    sk.istride = 1;
+    const int rows_sub = B * T;
+    if ((st = run_gemm(sk, bb.g16, C, C, 1, NL * sk.tap_mul, rows_sub, e, s, "diffsvc.skipsum"))) return st;
+  }
   e = epi();
   e.act = ACT_RELU;
   e.out16 = bb.u16;
@@ -1693,7 +1707,7 @@ static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   WS_GET(f16, g16, rows * c->n_layers * C);
   WS_GET(f16, s16, rows * C);
   WS_GET(f16, u16, rows * C);
-  bb = DenoiseBufs{cp16, cpF, (int)round_up((int64_t)rows, 64), y16b, h32, y16, g16, s16, u16};
+  bb = DenoiseBufs{cp16, cpF, (int)round_up((int64_t)rows, 64), y16b, h32, y16, g16, s16, u16, rows * 2 * C, rows * C};
   return SVC_OK;
 }
 
@@ -1710,7 +1724,7 @@ static int fragment_cp(svc_ctx* c, const DenoiseBufs& bb, int rows, hipStream_t 
   const int C = c->C, NL = c->n_layers;
   int st;
   for (int l = 0; l < NL; ++l)
-    if ((st = cp_fragment(bb.cp16 + (size_t)l * 2 * C, NL * 2 * C, c->dl_bdil[l], rows, bb.rows_pad,
+    if ((st = cp_fragment(bb.cp16 + (size_t)l * bb.cp_ls, 2 * C, c->dl_bdil[l], rows, bb.rows_pad,
                           bb.cpF + (size_t)l * bb.rows_pad * 2 * C, s)))
       return st;
   return SVC_OK;
@@ -1721,10 +1735,19 @@ static int project_cond(svc_ctx* c, const float* cond, int B, int T, const Denoi
   WS_GET(f16, cond16, (size_t)rows * 3 * C);
   int st;
   if ((st = f32_to_f16x3(cond, C, cond16, rows, C, s))) return st;  // [hi | lo | hi] split-fp16 operand
-  EpiArgs e = epi();
-  e.out16 = bb.cp16;
-  e.ld16 = c->n_layers * 2 * C;
-  return run_gemm(c->cp_all, cond16, 3 * C, 3 * C, B, T, T, e, s, "diffsvc.condproj");
+  // one GEMM per layer over that layer's rows of the packed weights, writing its layer-major cp block
+  for (int l = 0; l < c->n_layers; ++l) {
+    PackedGemm g = c->cp_all;
+    g.W = c->cp_all.W + (size_t)l * 2 * C * c->cp_all.Kpad;
+    g.bias = c->cp_all.bias + (size_t)l * 2 * C;
+    g.N = 2 * C;
+    g.Npad = 2 * C;
+    EpiArgs e = epi();
+    e.out16 = bb.cp16 + (size_t)l * bb.cp_ls;
+    e.ld16 = 2 * C;
+    if ((st = run_gemm(g, cond16, 3 * C, 3 * C, B, T, T, e, s, "diffsvc.condproj"))) return st;
+  }
+  return SVC_OK;
 }
 
 svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B, int T, int t, float* eps,
@@ -1811,8 +1834,9 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
     const int C = c->C, NL = c->n_layers;
     const int h = (int)(&u - sub);
     const int rp = (int)round_up((int64_t)u.B * T, 64);
-    return DenoiseBufs{bb.cp16 + r * NL * 2 * C, bb.cpF + fm_off[h] * NL * 2 * C, rp, bb.y16b + r * C,
-                       bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * NL * C, bb.s16 + r * C, bb.u16 + r * C};
+    return DenoiseBufs{bb.cp16 + r * 2 * C, bb.cpF + fm_off[h] * NL * 2 * C, rp, bb.y16b + r * C,
+                       bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * C, bb.u16 + r * C,
+                       bb.cp_ls, bb.g_ls};
   };
   for (int h = 0; h < S; ++h)
     if ((st = fragment_cp(c, sub_bufs(sub[h]), sub[h].B * T, s))) return st;
