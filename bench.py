@@ -250,8 +250,12 @@ def main():
     if os.path.exists(args.pmc_json):
         pmc = json.load(open(args.pmc_json))
         if dom_name in pmc.get("kernels", {}):
-            roof["traffic"] = pmc["kernels"][dom_name].get("hbm_bytes_per_launch")
-            roof["traffic_source"] = os.path.relpath(args.pmc_json, REPO) + " (" + pmc.get("source_run", "?") + ")"
+            ent = pmc["kernels"][dom_name]
+            roof["traffic"] = ent.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = os.path.relpath(args.pmc_json, REPO) + " (" + pmc.get("source_run", "?") + \
+                (f", {ent['workgroups']}-workgroup launches" if "workgroups" in ent else "") + ")"
+            if "rocprof_trace_avg_us" in ent:
+                roof["rocprof_avg_launch_us"] = ent["rocprof_trace_avg_us"]
     # per-kernel breakdown of the fully profiled warmup step
     total_flops = sum(v["flops"] for v in prof_all.values())
     kernels = {k: {"ms_per_step": round(v["ms"], 3), "launches_per_step": v["launches"],

@@ -4,6 +4,10 @@ HBM bytes per dispatch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950 FETCH_S
 half of the bytes of a wide coalesced streaming read (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is
 exact for 16-B/lane stores (our epilogue stores are narrower: treat it as an estimate), both in KiB.
 Infinity-Cache hits are counted as fetches, so the figure is an upper bound on DRAM traffic.
+One kernel can serve launches of different sizes (conv_gemm4<128,128,pair> runs both the sampler's sub-batch
+launches and the full-batch launches of bench.py's single-stream roofline pass), so traffic and the rocprof trace
+durations are also split by grid size; a kernel's headline `hbm_bytes_per_launch` is that of its LARGEST grid, which
+is the roofline pass's full-batch launch.
 Usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<round-prefix>
 """
 import csv
@@ -60,13 +64,31 @@ def counter_rows(d):
 
 
 def per_kernel(rows, counter):
+    """{kernel tag: {grid size in threads: [counter value per dispatch]}}"""
     acc = {}
     for r in rows:
         if r.get("Counter_Name") != counter:
             continue
         k = short(r.get("Kernel_Name", ""))
-        acc.setdefault(k, []).append(float(r["Counter_Value"]))
+        acc.setdefault(k, {}).setdefault(int(r.get("Grid_Size", 0)), []).append(float(r["Counter_Value"]))
     return acc
+
+
+def trace_by_grid(src):
+    """{kernel tag: {grid: (dispatches, average ns)}} from the rocprofv3 kernel trace."""
+    files = glob.glob(os.path.join(src, "trace", "**", "*kernel_trace.csv"), recursive=True)
+    acc = {}
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                k = short(r["Kernel_Name"])
+                g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+                acc.setdefault(k, {}).setdefault(g, []).append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return {k: {g: (len(v), sum(v) / len(v)) for g, v in d.items()} for k, d in acc.items()}
+
+
+def mean(v):
+    return sum(v) / len(v) if v else 0.0
 
 
 def main():
@@ -78,13 +100,21 @@ def main():
     fetch = per_kernel(counter_rows(os.path.join(src, "pmc_fetch")), "FETCH_SIZE")
     write = per_kernel(counter_rows(os.path.join(src, "pmc_write")), "WRITE_SIZE")
     out = {"method": __doc__.strip().splitlines()[2:5], "kernels": {}}
+    trace = trace_by_grid(src)
     for k in sorted(set(fetch) | set(write)):
-        f = fetch.get(k, [])
-        w = write.get(k, [])
-        fk = sum(f) / len(f) if f else 0.0
-        wk = sum(w) / len(w) if w else 0.0
-        out["kernels"][k] = {"dispatches": max(len(f), len(w)), "fetch_kib_per_launch": fk, "write_kib_per_launch": wk,
-                             "hbm_bytes_per_launch": (2 * fk + wk) * 1024.0}
+        grids = sorted(set(fetch.get(k, {})) | set(write.get(k, {})))
+        by_grid = {}
+        for g in grids:
+            f, w = fetch.get(k, {}).get(g, []), write.get(k, {}).get(g, [])
+            fk, wk = mean(f), mean(w)
+            e = {"workgroups": g // 256, "dispatches": max(len(f), len(w)), "fetch_kib_per_launch": fk,
+                 "write_kib_per_launch": wk, "hbm_bytes_per_launch": (2 * fk + wk) * 1024.0}
+            if g in trace.get(k, {}):
+                e["rocprof_trace_dispatches"], ns = trace[k][g]
+                e["rocprof_trace_avg_us"] = ns / 1000.0
+            by_grid[str(g)] = e
+        top = by_grid[str(grids[-1])]
+        out["kernels"][k] = dict(top, grid_threads=grids[-1], by_grid=by_grid)
     out["source_run"] = os.path.basename(os.path.normpath(src))
     for path in (dst + "_pmc_traffic.json", os.path.join(os.path.dirname(dst) or ".", "pmc_traffic.json")):
         with open(path, "w") as fh:
