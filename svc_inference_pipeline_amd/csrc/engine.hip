@@ -115,7 +115,8 @@ int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s);
 int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
-int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s);
+int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
+int conv_gemm5(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int ns, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 struct DiffLayerArgs {
   const f16* x16;
@@ -534,12 +535,15 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   const bool pair = e.kind == EPI_GATE;
   // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..14 = conv_gemm3 tile,
   // 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired epilogue, K = 1152),
-  // where the 2-workgroups-per-CU conv_gemm4 measured 6-9 % faster at full and sub-batch sizes; 20 = conv_gemm4
+  // where the 2-workgroups-per-CU conv_gemm4 measured 6-9 % faster at full and sub-batch sizes; 20 = conv_gemm4,
+  // 21 / 22 = conv_gemm5 (conv_gemm4 with a 4- / 5-slot ring of 32-deep K-steps), 24 = conv_gemm4 with the gate
+  // applied in registers (no LDS-staged epilogue)
   const char* venv = getenv("SVC_GEMM_VARIANT");  // read per call (A/B runs and tests switch it)
   int variant = venv ? atoi(venv) : 15;
-  if (variant == 15 && pair) variant = 20;
+  if (variant == 15 && pair) variant = 24;
   if (pair || g.N > 64) {
-    if (variant == 20) return conv_gemm4(a, e, zero_page(), s);
+    if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), s, variant == 24);
+    if (variant == 21 || variant == 22) return conv_gemm5(a, e, zero_page(), variant - 17, s);
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
     if (pair || variant >= 0) return conv_gemm2(a, e, zero_page(), variant < 0 ? 0 : variant, s);
   }
@@ -2283,6 +2287,7 @@ __global__ void fill_f16_kernel(f16* p, int64_t n, uint32_t seed) {
 
 extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_kind, int variant, int iters, double* ms_out) {
   SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters >= 1, "gemm_bench: bad args");
+  SVC_REQUIRE(epi_kind < 3 || variant == 24, "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float *bias, *R = nullptr;
@@ -2304,8 +2309,10 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   a.tap_mul = 1; a.tap_add = -(taps / 2); a.istride = 1; a.B = 1; a.T_out = M; a.N = N;
   EpiArgs e = epi();
   e.bias = bias; e.T_ostore = M; e.ostride = 1;
-  if (epi_kind == 1) {
-    e.kind = EPI_GATE; e.cp = cp; e.ld_cp = N; e.y16 = Y; e.ldy16 = N / 2;
+  if (epi_kind == 1 || epi_kind >= 3) {  // diagnostics: 3 = no cp read, no y store; 4 = no cp read; 5 = no y store
+    e.kind = EPI_GATE; e.cp = (epi_kind == 3 || epi_kind == 4) ? nullptr : cp; e.ld_cp = N;
+    e.y16 = (epi_kind == 3 || epi_kind == 5) ? nullptr : Y;
+    e.ldy16 = N / 2;
   } else {
     e.out16 = Y; e.ld16 = N;
     if (epi_kind == 2) {
@@ -2317,7 +2324,8 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_HIP_CHECK(hipEventCreate(&e1));
   int st = SVC_OK;
   auto run = [&]() {
-    if (variant == 20) return conv_gemm4(a, e, zero_page(), 0);
+    if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
+    if (variant == 21 || variant == 22) return conv_gemm5(a, e, zero_page(), variant - 17, 0);
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, 0);
     return variant < 0 ? conv_gemm(a, e, 0) : conv_gemm2(a, e, zero_page(), variant, 0);
   };

@@ -11,6 +11,8 @@
 //     epilogue runs beside the other's MFMAs (inter-workgroup overlap in place of intra-workgroup staggering);
 //   * the same operand images (128-B rows, 16-B chunk swizzle kv ^ (row & 6)), A loader (per-tap row shifts, zero
 //     rows outside the utterance) and LDS-staged vector epilogue (epilogue.h) as conv_gemm3.
+#include <type_traits>
+
 #include "common.h"
 #include "epilogue.h"
 
@@ -38,8 +40,14 @@ __device__ __forceinline__ void g4_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool CP64, bool PAIR>
+// DIRECT (gate epilogue only): the MFMAs run with the operands swapped, so a lane's accumulator holds 4 CONSECUTIVE
+// packed columns of one output row, and the gate column block j (< 2) and its filter partner j + 2 (packed column + 32)
+// sit in the same lane. The gate is then applied in registers: no 64 KiB f32 round trip through LDS, the conditioner
+// projection and bias are prefetched into registers under the last K-tile's MFMAs, and each lane stores 4 channels
+// (8 B) per row.
+template <bool CP64, bool PAIR, bool DIRECT>
 __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage, float inv_cp) {
+  static_assert(!DIRECT || PAIR, "the direct epilogue is the gate epilogue");
   extern __shared__ __align__(16) unsigned char sm4[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -116,6 +124,37 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
     for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fk = lane >> 4;
 
+  // DIRECT epilogue operands: rows m0 + wm*64 + i*16 + fr, packed columns nw + j*16 + fk*4 .. +3 (j < 2) and + 32
+  const int nw = n0 + wn * 64;
+  const bool wave_cols = nw < a.N;
+  union H4 { uint2 u; f16 h[4]; };
+  H4 cpg[4][2], cpf[4][2];
+  float4 bg[2], bfl[2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) cpg[i][j].u = cpf[i][j].u = make_uint2(0u, 0u);  // diagnostics runs without cp
+  bg[0] = bg[1] = bfl[0] = bfl[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+  // row group i of the epilogue operands; group 0 also loads the bias
+  auto prefetch = [&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if (!wave_cols || e.cp == nullptr) return;
+    if constexpr (i == 0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bg[j] = *reinterpret_cast<const float4*>(e.bias + nw + j * 16 + fk * 4);
+        bfl[j] = *reinterpret_cast<const float4*>(e.bias + nw + 32 + j * 16 + fk * 4);
+      }
+    }
+    const int m = min(m0 + wm * 64 + i * 16 + fr, M - 1);  // clamped rows are loaded but never stored
+    const f16* c = e.cp + (int64_t)m * e.ld_cp + nw + fk * 4;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      cpg[i][j].u = *reinterpret_cast<const uint2*>(c + j * 16);
+      cpf[i][j].u = *reinterpret_cast<const uint2*>(c + 32 + j * 16);
+    }
+  };
+
   // One barrier per K-tile: DMA(kt + 1) is issued right after the barrier of iteration kt (which also proves every wave
   // has finished reading that stage in iteration kt - 1) and lands under the MFMAs of iteration kt.
   issue(0);
@@ -123,6 +162,14 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
     g4_vmwait<0>();  // this wave's DMAs of stage kt have landed (nothing younger is outstanding)
     g4_barrier();    // ... and everyone's; stage (kt + 1) & 1 is free
     if (kt + 1 < nk) issue(kt + 1);
+    if constexpr (DIRECT) {
+      if (kt + 1 == nk) {  // under the last K-tile's MFMAs (spreading these over earlier K-steps measured no better)
+        prefetch(std::integral_constant<int, 0>{});
+        prefetch(std::integral_constant<int, 1>{});
+        prefetch(std::integral_constant<int, 2>{});
+        prefetch(std::integral_constant<int, 3>{});
+      }
+    }
     const unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
     const unsigned char* Bm = A + G4_BM * 128;
 #pragma unroll
@@ -142,9 +189,51 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (DIRECT)  // C^T fragment: acc[i][j][r] = C[row fr of block i][col fk*4 + r of block j]
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        }
       __builtin_amdgcn_s_setprio(0);
     }
+  }
+  if constexpr (DIRECT) {
+    if (!wave_cols) return;
+    if (e.y16 == nullptr) {  // diagnostics sink (svc_gemm_bench epi 3 / 5): keep the MFMAs and cp reads, no stores
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sum += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) sum += (float)cpg[i][j].h[0] + (float)cpf[i][j].h[3];
+      if (sum == 1.2345e-38f && e.out32) e.out32[0] = sum;
+      return;
+    }
+    const int chb = (nw >> 6) * 32 + fk * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + fr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float4 g = make_float4(acc[i][j][0] + bg[j].x, acc[i][j][1] + bg[j].y, acc[i][j][2] + bg[j].z,
+                                     acc[i][j][3] + bg[j].w);
+        const float4 f = make_float4(acc[i][j + 2][0] + bfl[j].x, acc[i][j + 2][1] + bfl[j].y,
+                                     acc[i][j + 2][2] + bfl[j].z, acc[i][j + 2][3] + bfl[j].w);
+        H4 pk;
+        pk.h[0] = f16_sat(fast_sigmoid(g.x + (float)cpg[i][j].h[0]) * fast_tanh(f.x + (float)cpf[i][j].h[0]));
+        pk.h[1] = f16_sat(fast_sigmoid(g.y + (float)cpg[i][j].h[1]) * fast_tanh(f.y + (float)cpf[i][j].h[1]));
+        pk.h[2] = f16_sat(fast_sigmoid(g.z + (float)cpg[i][j].h[2]) * fast_tanh(f.z + (float)cpf[i][j].h[2]));
+        pk.h[3] = f16_sat(fast_sigmoid(g.w + (float)cpg[i][j].h[3]) * fast_tanh(f.w + (float)cpf[i][j].h[3]));
+        // 4 channels (8 B) per lane and row; a 16-B form (quad exchange between lanes fk, fk ^ 1) measured 2-3 % slower
+        *reinterpret_cast<uint2*>(e.y16 + (int64_t)m * e.ldy16 + chb + j * 16) = pk.u;
+      }
+    }
+    return;
   }
   g4_vmwait<0>();
   __syncthreads();
@@ -160,7 +249,8 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
   epilogue_pass<G4_BM, G4_BN, G4_LDC, G4_NT, PAIR>(Cs, m0, n0, M, a, e, tid);
 }
 
-int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipStream_t s) {
+// direct_gate: the gate in registers (DIRECT) instead of the LDS-staged epilogue_pass
+int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate) {
   ConvGemmArgs a = a0;
   SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0 && a.N % 4 == 0, "conv_gemm4: layout");
   SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm4: 16-B alignment");
@@ -172,22 +262,25 @@ int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipSt
   const int64_t grid = (int64_t)cdiv(M, G4_BM) * a.ntiles_n;
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm4: bad grid");
   const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
-  static bool attr[2][2] = {};
-  if (!attr[cp64][pair]) {
-    const void* fn = cp64 ? (pair ? (const void*)conv_gemm4_kernel<true, true> : (const void*)conv_gemm4_kernel<true, false>)
-                          : (pair ? (const void*)conv_gemm4_kernel<false, true> : (const void*)conv_gemm4_kernel<false, false>);
+  const bool direct = pair && direct_gate;
+  static bool attr[2][2][2] = {};
+  const void* fns[2][2][2] = {
+      {{(const void*)conv_gemm4_kernel<false, false, false>, nullptr},
+       {(const void*)conv_gemm4_kernel<false, true, false>, (const void*)conv_gemm4_kernel<false, true, true>}},
+      {{(const void*)conv_gemm4_kernel<true, false, false>, nullptr},
+       {(const void*)conv_gemm4_kernel<true, true, false>, (const void*)conv_gemm4_kernel<true, true, true>}}};
+  const void* fn = fns[cp64][pair][direct];
+  if (!attr[cp64][pair][direct]) {
     SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G4_LDS));
-    attr[cp64][pair] = true;
+    attr[cp64][pair][direct] = true;
   }
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
-  const int tok = prof_begin(pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>", 2.0 * M * (double)a.N * kreal,
-                             0.0, s);
+  const char* tag = direct ? "conv_gemm4<128,128,gate>" : pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>";
+  const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);
   const dim3 g((unsigned)grid), b(G4_NT);
   const float inv = 1.0f / (float)a.Cp;
-  if (cp64 && pair) hipLaunchKernelGGL((conv_gemm4_kernel<true, true>), g, b, G4_LDS, s, a, e, zpage, inv);
-  else if (cp64) hipLaunchKernelGGL((conv_gemm4_kernel<true, false>), g, b, G4_LDS, s, a, e, zpage, inv);
-  else if (pair) hipLaunchKernelGGL((conv_gemm4_kernel<false, true>), g, b, G4_LDS, s, a, e, zpage, inv);
-  else hipLaunchKernelGGL((conv_gemm4_kernel<false, false>), g, b, G4_LDS, s, a, e, zpage, inv);
+  void* args[] = {&a, const_cast<EpiArgs*>(&e), const_cast<const f16**>(&zpage), const_cast<float*>(&inv)};
+  SVC_HIP_CHECK(hipLaunchKernel(fn, g, b, args, G4_LDS, s));
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;

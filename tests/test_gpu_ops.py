@@ -38,7 +38,7 @@ def _tm(x):  # [B, C, T] -> time-major [B*T, C]
     (3, 129, 192, 192, 11, 1, 3, 15, 0),     # ragged utterances inside the halo image
     (1, 90, 128, 256, 7, 1, 7, 21, 0),       # |shift| 21, T < tile
 ])
-@pytest.mark.parametrize("variant", ["0", "1", "-1", "10", "11", "12", "13", "14", "15", "20"])
+@pytest.mark.parametrize("variant", ["0", "1", "-1", "10", "11", "12", "13", "14", "15", "20", "21", "22", "24"])
 @pytest.mark.parametrize("halo", ["1", "0"])
 def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, halo, monkeypatch):
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)  # -1: v1, 0..4: conv_gemm2 tiles, 10..14: conv_gemm3 tiles, 15: auto
@@ -61,7 +61,7 @@ def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, halo, monkey
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k,s", [(2, 25, 768, 384, 8, 4), (1, 40, 96, 48, 4, 2), (2, 33, 48, 24, 4, 2),
                                               (1, 9, 1536, 768, 8, 4)])
-@pytest.mark.parametrize("variant", ["0", "-1", "10", "14", "15", "20"])
+@pytest.mark.parametrize("variant", ["0", "-1", "10", "14", "15", "20", "21", "22", "24"])
 def test_conv_transpose1d(B, T, Cin, Cout, k, s, variant, monkeypatch):
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
     g = torch.Generator().manual_seed(1)

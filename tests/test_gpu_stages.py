@@ -115,7 +115,25 @@ def test_fused_layer_vs_oracle(engine, states, cfg, fused, B, T, monkeypatch):
         assert rel_l2(eps, other) < 2e-3
 
 
-@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15", "20"])
+@pytest.mark.parametrize("variant", ["20", "24", "21"])
+@pytest.mark.parametrize("B,T", [(3, 50), (2, 700), (5, 937)])
+def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, monkeypatch):
+    """The DiffSVC gate GEMM kernels (LDS-staged and in-register gate epilogues, deep-ring variant) on ragged row
+    counts (B*T not a multiple of the 128-row tile, utterance boundaries inside tiles) against the oracle's eps."""
+    rng = np.random.default_rng(B * 7 + T)
+    cond = rng.standard_normal((B, T, 384)).astype(np.float32)
+    x = rng.standard_normal((B, T, 100)).astype(np.float32)
+    table = W.step_embedding_table(1000)
+    monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
+    monkeypatch.setenv("SVC_DIFF_FUSED", "0")
+    eps = engine.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()
+    with torch.no_grad():
+        ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond),
+                                 torch.full((B,), 250, dtype=torch.long), table).numpy()
+    assert rel_l2(eps, ref) < 5e-3
+
+
+@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15", "20", "21", "22", "24"])
 def test_eps_gemm_variants(engine, golden, variant, monkeypatch):
     """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path)."""
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)

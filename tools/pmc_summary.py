@@ -36,12 +36,18 @@ def short(name):
     m = re.search(r"conv_gemm3_kernelILi(\d+)ELi(\d+)ELb([01])ELb([01])ELb0E", name)  # rocprof keeps these mangled
     if m:
         return f"conv_gemm3<{m.group(1)},{m.group(2)}{',pair' if m.group(4) == '1' else ''}>"
-    m = re.search(r"conv_gemm4_kernel<(true|false), (true|false)>", name)
+    m = re.search(r"conv_gemm4_kernel<(true|false), (true|false), (true|false)>", name)
     if m:
-        return f"conv_gemm4<128,128{',pair' if m.group(2) == 'true' else ''}>"
-    m = re.search(r"conv_gemm4_kernelILb([01])ELb([01])E", name)
+        return f"conv_gemm4<128,128{',gate' if m.group(3) == 'true' else ',pair' if m.group(2) == 'true' else ''}>"
+    m = re.search(r"conv_gemm4_kernelILb([01])ELb([01])ELb([01])E", name)
     if m:
-        return f"conv_gemm4<128,128{',pair' if m.group(2) == '1' else ''}>"
+        return f"conv_gemm4<128,128{',gate' if m.group(3) == '1' else ',pair' if m.group(2) == '1' else ''}>"
+    m = re.search(r"conv_gemm5_kernel<(\d+), (true|false), (true|false)>", name)
+    if m:
+        return f"conv_gemm5<{m.group(1)}{',pair' if m.group(3) == 'true' else ''}>"
+    m = re.search(r"conv_gemm5_kernelILi(\d+)ELb([01])ELb([01])E", name)
+    if m:
+        return f"conv_gemm5<{m.group(1)}{',pair' if m.group(3) == '1' else ''}>"
     m = re.search(r"conv_gemm2_kernel<(\d+), (\d+), \d+, \d+, (\d+), (true|false)>", name)
     if m:
         return f"conv_gemm2<{m.group(1)},{m.group(2)}{',pair' if m.group(4) == 'true' else ''}>"
