@@ -116,6 +116,7 @@ int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s
 int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
+bool conv_gemm4_rmw_form(const ConvGemmArgs& a, const EpiArgs& e);
 int conv_gemm5(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int ns, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 struct DiffLayerArgs {
@@ -534,13 +535,19 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   if (!e.bias) e.bias = g.bias;
   const bool pair = e.kind == EPI_GATE;
   // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..14 = conv_gemm3 tile,
-  // 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired epilogue, K = 1152),
-  // where the 2-workgroups-per-CU conv_gemm4 measured 6-9 % faster at full and sub-batch sizes; 20 = conv_gemm4,
-  // 21 / 22 = conv_gemm5 (conv_gemm4 with a 4- / 5-slot ring of 32-deep K-steps), 24 = conv_gemm4 with the gate
-  // applied in registers (no LDS-staged epilogue)
+  // 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired epilogue, K = 1152)
+  // which runs conv_gemm4 with its register gate epilogue (24; 3-9 % faster than conv_gemm3); 20 = conv_gemm4,
+  // 21 / 22 = conv_gemm5 (conv_gemm4 with a 4- / 5-slot ring of 32-deep K-steps), 24 = conv_gemm4 with its register
+  // epilogues (gate; residual read-modify-write) where the epilogue has that form
   const char* venv = getenv("SVC_GEMM_VARIANT");  // read per call (A/B runs and tests switch it)
   int variant = venv ? atoi(venv) : 15;
-  if (variant == 15 && pair) variant = 24;
+  // SVC_GEMM4_RMW=1: the output projection on conv_gemm4's register epilogue too. Alone it is 12 % faster per sampler
+  // sub-batch launch (tools/gemm_bench.py), but beside the other sampler streams the whole step measured 1.5 % slower
+  // (703 vs 713 audio-s/s, same box), so it is opt-in.
+  const char* renv = getenv("SVC_GEMM4_RMW");
+  const char* genv = getenv("SVC_GEMM4_GATE");  // 0: the gate GEMM on conv_gemm4's LDS-staged epilogue (variant 20)
+  if (variant == 15 && pair) variant = (genv && !atoi(genv)) ? 20 : 24;
+  if (variant == 15 && renv && atoi(renv) && conv_gemm4_rmw_form(a, e)) variant = 24;
   if (pair || g.N > 64) {
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), s, variant == 24);
     if (variant == 21 || variant == 22) return conv_gemm5(a, e, zero_page(), variant - 17, s);

@@ -45,9 +45,12 @@ __device__ __forceinline__ void g4_barrier() {
 // sit in the same lane. The gate is then applied in registers: no 64 KiB f32 round trip through LDS, the conditioner
 // projection and bias are prefetched into registers under the last K-tile's MFMAs, and each lane stores 4 channels
 // (8 B) per row.
+//
+// DIRECT without PAIR: the same register epilogue for the residual read-modify-write (the DiffSVC output projection):
+// v = (acc32 + (C + bias)) / acc_div -> out32, f16(v + add16) -> out16, with rows stored in place (orow = m). Each lane
+// owns 4 consecutive columns of a row: 16-B f32 loads / stores, the acc32 tile prefetched under the last K-tile.
 template <bool CP64, bool PAIR, bool DIRECT>
 __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage, float inv_cp) {
-  static_assert(!DIRECT || PAIR, "the direct epilogue is the gate epilogue");
   extern __shared__ __align__(16) unsigned char sm4[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -136,8 +139,19 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
     for (int j = 0; j < 2; ++j) cpg[i][j].u = cpf[i][j].u = make_uint2(0u, 0u);  // diagnostics runs without cp
   bg[0] = bg[1] = bfl[0] = bfl[1] = make_float4(0.f, 0.f, 0.f, 0.f);
   // row group i of the epilogue operands; group 0 also loads the bias
+  float4 res[4][4];  // DIRECT && !PAIR: the acc32 (residual) tile
   auto prefetch = [&](auto ic) {
     constexpr int i = decltype(ic)::value;
+    if constexpr (!PAIR) {
+      if (!wave_cols) return;
+      const int m = min(m0 + wm * 64 + i * 16 + fr, M - 1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = min(nw + j * 16 + fk * 4, a.N - 4);  // clamped columns are loaded but never stored
+        res[i][j] = *reinterpret_cast<const float4*>(e.acc32 + (int64_t)m * e.ld_acc + n);
+      }
+      return;
+    }
     if (!wave_cols || e.cp == nullptr) return;
     if constexpr (i == 0) {
 #pragma unroll
@@ -198,7 +212,33 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
       __builtin_amdgcn_s_setprio(0);
     }
   }
-  if constexpr (DIRECT) {
+  if constexpr (DIRECT && !PAIR) {
+    if (!wave_cols) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = nw + j * 16 + fk * 4;
+      if (n >= a.N) continue;
+      const float4 bi = *reinterpret_cast<const float4*>(e.bias + n);
+      const float4 ad = *reinterpret_cast<const float4*>(e.add16 + n);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + i * 16 + fr;
+        if (m >= M) continue;
+        float4 v = make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w);
+        v.x = (res[i][j].x + v.x) / e.acc_div;  // the order and IEEE division of epilogue_pass
+        v.y = (res[i][j].y + v.y) / e.acc_div;
+        v.z = (res[i][j].z + v.z) / e.acc_div;
+        v.w = (res[i][j].w + v.w) / e.acc_div;
+        *reinterpret_cast<float4*>(e.out32 + (int64_t)m * e.ld32 + n) = v;
+        union { uint2 u; f16 h[4]; } pk;
+        pk.h[0] = f16_sat(v.x + ad.x); pk.h[1] = f16_sat(v.y + ad.y);
+        pk.h[2] = f16_sat(v.z + ad.z); pk.h[3] = f16_sat(v.w + ad.w);
+        *reinterpret_cast<uint2*>(e.out16 + (int64_t)m * e.ld16 + n) = pk.u;
+      }
+    }
+    return;
+  }
+  if constexpr (DIRECT && PAIR) {
     if (!wave_cols) return;
     if (e.y16 == nullptr) {  // diagnostics sink (svc_gemm_bench epi 3 / 5): keep the MFMAs and cp reads, no stores
       float sum = 0.f;
@@ -249,7 +289,15 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
   epilogue_pass<G4_BM, G4_BN, G4_LDC, G4_NT, PAIR>(Cs, m0, n0, M, a, e, tid);
 }
 
-// direct_gate: the gate in registers (DIRECT) instead of the LDS-staged epilogue_pass
+// the direct residual epilogue covers exactly the DiffSVC output projection's form
+bool conv_gemm4_rmw_form(const ConvGemmArgs& a, const EpiArgs& e) {
+  return e.kind == EPI_GENERIC && e.act == ACT_NONE && e.acc32 && e.out32 && e.out16 && e.add16 && !e.add_t &&
+         !e.add_row && e.scale_cols == 0 && e.split16 == 0 && e.T_ostore == a.T_out && e.ostride == 1 &&
+         e.ophase == 0 && a.N % 4 == 0 && e.ld_acc % 4 == 0 && e.ld32 % 4 == 0 && e.ld16 % 4 == 0;
+}
+
+// direct: the register epilogue (DIRECT: gate, or the residual read-modify-write) where the epilogue has that form,
+// otherwise the LDS-staged epilogue_pass
 int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate) {
   ConvGemmArgs a = a0;
   SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0 && a.N % 4 == 0, "conv_gemm4: layout");
@@ -262,12 +310,12 @@ int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipSt
   const int64_t grid = (int64_t)cdiv(M, G4_BM) * a.ntiles_n;
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm4: bad grid");
   const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
-  const bool direct = pair && direct_gate;
+  const bool direct = direct_gate && (pair || conv_gemm4_rmw_form(a, e));
   static bool attr[2][2][2] = {};
   const void* fns[2][2][2] = {
-      {{(const void*)conv_gemm4_kernel<false, false, false>, nullptr},
+      {{(const void*)conv_gemm4_kernel<false, false, false>, (const void*)conv_gemm4_kernel<false, false, true>},
        {(const void*)conv_gemm4_kernel<false, true, false>, (const void*)conv_gemm4_kernel<false, true, true>}},
-      {{(const void*)conv_gemm4_kernel<true, false, false>, nullptr},
+      {{(const void*)conv_gemm4_kernel<true, false, false>, (const void*)conv_gemm4_kernel<true, false, true>},
        {(const void*)conv_gemm4_kernel<true, true, false>, (const void*)conv_gemm4_kernel<true, true, true>}}};
   const void* fn = fns[cp64][pair][direct];
   if (!attr[cp64][pair][direct]) {
@@ -275,7 +323,8 @@ int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipSt
     attr[cp64][pair][direct] = true;
   }
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
-  const char* tag = direct ? "conv_gemm4<128,128,gate>" : pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>";
+  const char* tag = direct ? (pair ? "conv_gemm4<128,128,gate>" : "conv_gemm4<128,128,rmw>")
+                           : pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>";
   const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);
   const dim3 g((unsigned)grid), b(G4_NT);
   const float inv = 1.0f / (float)a.Cp;
