@@ -1990,6 +1990,10 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
   WS_GET(f16, next16, big);
   const char* amp_env = getenv("SVC_AMP_FUSED");  // "0" = unfused activation1d + GEMM everywhere (A/B runs)
   const bool use_amp = !(amp_env && amp_env[0] == '0');
+  const char* amp_max = getenv("SVC_AMP_MAXC");   // widest channel count that takes the fused kernel (A/B runs)
+  // C = 96 measured 1.2 % faster end to end as activation1d + conv_gemm3 (736 vs 727 audio-s/s, same box); C = 48
+  // unfused is 9 % slower (its N = 48 GEMMs are too narrow for the MFMA tiles)
+  const int amp_maxc = amp_max ? atoi(amp_max) : 48;
   const int ns = (int)c->vstages.size();
 
   // Utterance-aligned sub-batches on their own streams (as in svc_diffsvc_sample): every buffer is
@@ -2051,7 +2055,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
           const ActP& a1 = S.acts[j][2 * l];
           const ActP& a2 = S.acts[j][2 * l + 1];
           // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
-          const bool fuse = use_amp && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
+          const bool fuse = use_amp && ch <= amp_maxc && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
           EpiArgs e1 = epi();
           e1.out32 = tmph;
           e1.ld32 = ch;
