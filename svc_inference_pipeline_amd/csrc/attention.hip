@@ -20,8 +20,10 @@ __device__ __forceinline__ int kswz(int row, int kv) { return row * 64 + ((kv ^ 
 
 __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict__ qkv, f16* __restrict__ out, int L,
                                                            int D) {
-  __shared__ __align__(16) f16 Ks[ATT_KT * 64];
-  __shared__ __align__(16) f16 Vt[64 * VT_LD];
+  // double-buffered K / V^T tiles: tile kt + 1 is loaded into registers while tile kt is multiplied, then written to
+  // the other buffer (one barrier per tile)
+  __shared__ __align__(16) f16 Ksb[2][ATT_KT * 64];
+  __shared__ __align__(16) f16 Vtb[2][64 * VT_LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
   const int ld = 3 * D;
@@ -49,26 +51,40 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict
   const float LOG2E = 1.4426950408889634f;
 
   const int ntiles = (L + ATT_KT - 1) / ATT_KT;
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const int k0 = kt * ATT_KT;
-    // ---- stage K tile (row-major, swizzled) and V^T tile
+  uint4 kreg[2], vreg[2];
+  auto gload = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      int v = tid + 256 * i;  // 512 vectors of 8 f16
-      int row = v >> 3, kvv = v & 7;
-      int key = k0 + row;
-      uint4 kvec = make_uint4(0, 0, 0, 0), vvec = make_uint4(0, 0, 0, 0);
+      const int v = tid + 256 * i;  // 512 vectors of 8 f16
+      const int row = v >> 3, kvv = v & 7;
+      const int key = kt * ATT_KT + row;
+      kreg[i] = vreg[i] = make_uint4(0, 0, 0, 0);
       if (key < L) {
-        kvec = *reinterpret_cast<const uint4*>(base + (int64_t)key * ld + D + h * 64 + kvv * 8);
-        vvec = *reinterpret_cast<const uint4*>(base + (int64_t)key * ld + 2 * D + h * 64 + kvv * 8);
+        kreg[i] = *reinterpret_cast<const uint4*>(base + (int64_t)key * ld + D + h * 64 + kvv * 8);
+        vreg[i] = *reinterpret_cast<const uint4*>(base + (int64_t)key * ld + 2 * D + h * 64 + kvv * 8);
       }
-      *reinterpret_cast<uint4*>(Ks + kswz(row, kvv)) = kvec;
-      union { uint4 u; f16 e[8]; } vv;
-      vv.u = vvec;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Vt[(kvv * 8 + j) * VT_LD + row] = vv.e[j];
     }
-    __syncthreads();
+  };
+  auto lstore = [&](int buf) {  // K row-major (swizzled), V transposed
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int v = tid + 256 * i;
+      const int row = v >> 3, kvv = v & 7;
+      *reinterpret_cast<uint4*>(Ksb[buf] + kswz(row, kvv)) = kreg[i];
+      union { uint4 u; f16 e[8]; } vv;
+      vv.u = vreg[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) Vtb[buf][(kvv * 8 + j) * VT_LD + row] = vv.e[j];
+    }
+  };
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const int k0 = kt * ATT_KT;
+    const f16* Ks = Ksb[kt & 1];
+    const f16* Vt = Vtb[kt & 1];
+    if (kt + 1 < ntiles) gload(kt + 1);  // lands while this tile is multiplied
 
     // ---- S^T = K Q^T : s[kf][f][r] = S[q = f*16 + c16][key = kf*16 + 4g + r]
     floatx4 s[4][2];
@@ -100,7 +116,7 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict
       mx = fmaxf(mx, __shfl_xor(mx, 16));
       mx = fmaxf(mx, __shfl_xor(mx, 32));
       const float mnew = fmaxf(mrun[f], mx);
-      const float alpha = exp2f((mrun[f] - mnew) * LOG2E);
+      const float alpha = __builtin_amdgcn_exp2f((mrun[f] - mnew) * LOG2E);  // v_exp_f32 (arguments <= 0)
       mrun[f] = mnew;
       float psum = 0.f;
       float p[4][4];
@@ -108,7 +124,7 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict
       for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          p[kf][r] = exp2f((s[kf][f][r] - mnew) * LOG2E);
+          p[kf][r] = __builtin_amdgcn_exp2f((s[kf][f][r] - mnew) * LOG2E);
           psum += p[kf][r];
         }
       lrun[f] = lrun[f] * alpha + psum;
@@ -138,6 +154,7 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict
         for (int f = 0; f < 2; ++f) o[df][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va.h, pb[f][ks], o[df][f], 0, 0, 0);
       }
     }
+    if (kt + 1 < ntiles) lstore((kt + 1) & 1);  // that buffer was last read in iteration kt - 1, before its barrier
     __syncthreads();
   }
 
