@@ -13,6 +13,7 @@ struct AmpConvArgs {
   const f16* W;       // packed weights [Npad][Kpad], K index = tap*C + ci (pack_conv1d with Cp = C)
   int Kpad;
   const float* bias;
+  int dbg;  // diagnostics (tools/amp_bench.py, SVC_AMP_DBG): 1 = skip the activation phase, 2 = skip the conv phase
 };
 
 bool amp_conv_supported(int C, int k, int d);
