@@ -1371,38 +1371,65 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   WS_GET(f16, o16, rows2 * D);
   WS_GET(f16, h16, rows2 * 4 * D * X3);
   const float qk_scale = powf((float)(D / c->wH), -0.25f);
-  auto ln16 = [&](const float* g, const float* b) {
-    return X3 == 3 ? layernorm_f16x3(x, g, b, n16, (int)rows2, D, s) : layernorm_f16(x, g, b, n16, (int)rows2, D, D, s);
-  };
+  // The 24 blocks run as utterance-aligned sub-batches on their own streams (as the sampler does): rows are
+  // time-major per utterance, so a sub-batch is a row range of every buffer, and one sub-batch's HBM-bound GEMM
+  // epilogues / layer norms run beside the other's MFMA phases. SVC_WHISPER_STREAMS=1 disables the split.
+  const char* wenv = getenv("SVC_WHISPER_STREAMS");
+  const int NSW = std::max(1, std::min(std::min(wenv ? atoi(wenv) : 2, B), (int)kMaxSubStreams));
+  if ((st = c->ensure_sub_streams(NSW))) return st;
+  if (NSW > 1) {
+    SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
+    for (int h = 0; h < NSW; ++h) SVC_HIP_CHECK(hipStreamWaitEvent(c->sub_streams[h], c->ev_fork, 0));
+  }
   for (int i = 0; i < c->wL; ++i) {
     WBlock& b = c->wblocks[i];
-    if ((st = ln16(b.ln1_g, b.ln1_b))) return st;
-    e = epi();
-    e.out16 = qkv;
-    e.ld16 = 3 * D;
-    e.scale_cols = 2 * D;
-    e.col_scale = qk_scale;
-    if ((st = run_gemm(b.qkv, n16, D * X3, D * X3, B, L, L, e, s, "whisper.qkv"))) return st;
-    if ((st = attention(qkv, o16, B, L, D, s))) return st;
-    e = epi();
-    e.add_row = x;
-    e.ld_add_row = D;
-    e.out32 = x;
-    e.ld32 = D;
-    if ((st = run_gemm(b.out, o16, D, D, B, L, L, e, s, "whisper.out"))) return st;
-    if ((st = ln16(b.ln2_g, b.ln2_b))) return st;
-    e = epi();
-    e.act = ACT_GELU;
-    e.out16 = h16;
-    e.ld16 = 4 * D * X3;
-    e.split16 = X3 == 3 ? 4 * D : 0;
-    if ((st = run_gemm(b.fc1, n16, D * X3, D * X3, B, L, L, e, s, "whisper.fc1"))) return st;
-    e = epi();
-    e.add_row = x;
-    e.ld_add_row = D;
-    e.out32 = x;
-    e.ld32 = D;
-    if ((st = run_gemm(b.fc2, h16, 4 * D * X3, 4 * D * X3, B, L, L, e, s, "whisper.fc2"))) return st;
+    for (int h = 0; h < NSW; ++h) {
+      const int b0 = h * B / NSW, Bh = (h + 1) * B / NSW - b0;
+      const size_t r = (size_t)b0 * L, rows_h = (size_t)Bh * L;
+      hipStream_t hs = NSW == 1 ? s : c->sub_streams[h];
+      float* xh = x + r * D;
+      f16* n16h = n16 + r * D * X3;
+      f16* qkvh = qkv + r * 3 * D;
+      f16* o16h = o16 + r * D;
+      f16* h16h = h16 + r * 4 * D * X3;
+      auto ln16 = [&](const float* g, const float* bb) {
+        return X3 == 3 ? layernorm_f16x3(xh, g, bb, n16h, (int)rows_h, D, hs)
+                       : layernorm_f16(xh, g, bb, n16h, (int)rows_h, D, D, hs);
+      };
+      if ((st = ln16(b.ln1_g, b.ln1_b))) return st;
+      e = epi();
+      e.out16 = qkvh;
+      e.ld16 = 3 * D;
+      e.scale_cols = 2 * D;
+      e.col_scale = qk_scale;
+      if ((st = run_gemm(b.qkv, n16h, D * X3, D * X3, Bh, L, L, e, hs, "whisper.qkv"))) return st;
+      if ((st = attention(qkvh, o16h, Bh, L, D, hs))) return st;
+      e = epi();
+      e.add_row = xh;
+      e.ld_add_row = D;
+      e.out32 = xh;
+      e.ld32 = D;
+      if ((st = run_gemm(b.out, o16h, D, D, Bh, L, L, e, hs, "whisper.out"))) return st;
+      if ((st = ln16(b.ln2_g, b.ln2_b))) return st;
+      e = epi();
+      e.act = ACT_GELU;
+      e.out16 = h16h;
+      e.ld16 = 4 * D * X3;
+      e.split16 = X3 == 3 ? 4 * D : 0;
+      if ((st = run_gemm(b.fc1, n16h, D * X3, D * X3, Bh, L, L, e, hs, "whisper.fc1"))) return st;
+      e = epi();
+      e.add_row = xh;
+      e.ld_add_row = D;
+      e.out32 = xh;
+      e.ld32 = D;
+      if ((st = run_gemm(b.fc2, h16h, 4 * D * X3, 4 * D * X3, Bh, L, L, e, hs, "whisper.fc2"))) return st;
+    }
+  }
+  if (NSW > 1) {
+    for (int h = 0; h < NSW; ++h) {
+      SVC_HIP_CHECK(hipEventRecord(c->ev_join[h], c->sub_streams[h]));
+      SVC_HIP_CHECK(hipStreamWaitEvent(s, c->ev_join[h], 0));
+    }
   }
   return layernorm_f32(x, c->wlnp_g, c->wlnp_b, feats, (int)rows2, D, D, s);
 }
