@@ -509,9 +509,9 @@ const f16* zero_page() {
   return z;
 }
 
-int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
-             hipStream_t s, const char* site = "") {
-  prof_site(site);
+// the kernel arguments of one implicit-GEMM launch over the packed weights g (run_gemm, the dual launches)
+static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out,
+                              EpiArgs& e) {
   ConvGemmArgs a{};
   a.X = X;
   a.ldx = ldx;
@@ -533,6 +533,13 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
     e.ophase = 0;
   }
   if (!e.bias) e.bias = g.bias;
+  return a;
+}
+
+int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
+             hipStream_t s, const char* site = "") {
+  prof_site(site);
+  const ConvGemmArgs a = gemm_args(g, X, ldx, Cvalid, B, T_in, T_out, e);
   const bool pair = e.kind == EPI_GATE;
   // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..14 = conv_gemm3 tile,
   // 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired epilogue, K = 1152)

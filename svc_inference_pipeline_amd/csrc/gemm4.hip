@@ -49,15 +49,20 @@ __device__ __forceinline__ void g4_barrier() {
 // DIRECT without PAIR: the same register epilogue for the residual read-modify-write (the DiffSVC output projection):
 // v = (acc32 + (C + bias)) / acc_div -> out32, f16(v + add16) -> out16, with rows stored in place (orow = m). Each lane
 // owns 4 consecutive columns of a row: 16-B f32 loads / stores, the acc32 tile prefetched under the last K-tile.
+// blockIdx -> a workgroup index whose consecutive values land on one XCD (tiles sharing A rows share that XCD's L2)
+__device__ __forceinline__ int g4_xcd_remap() {
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+}
+
+// One 128 x 128 output tile (index wgid, N-tiles fastest) of the implicit GEMM, by the calling 256-thread workgroup.
 template <bool CP64, bool PAIR, bool DIRECT>
-__global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage, float inv_cp) {
-  extern __shared__ __align__(16) unsigned char sm4[];
+__device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage,
+                                                float inv_cp, int wgid, unsigned char* sm4) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
   const int tile_n = wgid % a.ntiles_n, tile_m = wgid / a.ntiles_n;
   const int m0 = tile_m * G4_BM, n0 = tile_n * G4_BN;
   const int M = a.B * a.T_out;
@@ -287,6 +292,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
       for (int r = 0; r < 4; ++r) Cs[(wm * 64 + i * 16 + fk * 4 + r) * G4_LDC + wn * 64 + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
   epilogue_pass<G4_BM, G4_BN, G4_LDC, G4_NT, PAIR>(Cs, m0, n0, M, a, e, tid);
+}
+
+template <bool CP64, bool PAIR, bool DIRECT>
+__global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage, float inv_cp) {
+  extern __shared__ __align__(16) unsigned char sm4[];
+  conv_gemm4_tile<CP64, PAIR, DIRECT>(a, e, zpage, inv_cp, g4_xcd_remap(), sm4);
 }
 
 // the direct residual epilogue covers exactly the DiffSVC output projection's form
