@@ -253,9 +253,10 @@ def _wn(sd, name):
     return torch._weight_norm(_t(sd, name + ".weight_v"), _t(sd, name + ".weight_g"), 0)
 
 
-def activation1d(x, alpha_log, beta_log, filt):
-    """modules/bigvgan.py:234-307 (Activation1d = UpSample1d(2,12) -> SnakeBeta(logscale) -> DownSample1d(2,12))
-    with SnakeBeta :146-159. x f32[B,C,T]."""
+def activation1d(x, alpha_log, beta_log, filt, logscale=True):
+    """modules/bigvgan.py:234-307 (Activation1d = UpSample1d(2,12) -> SnakeBeta -> DownSample1d(2,12)) with SnakeBeta
+    :146-159; Snake (:42-92) is the same with beta = alpha. logscale=False: the parameters are alpha / beta themselves
+    (`alpha_logscale=False`). x f32[B,C,T]."""
     C = x.shape[1]
     f = filt.view(1, 1, -1)
     # UpSample1d :277-287  (ratio 2, kernel 12: pad 5, pad_left 15, pad_right 15)
@@ -263,21 +264,26 @@ def activation1d(x, alpha_log, beta_log, filt):
     xu = 2 * F.conv_transpose1d(xu, f.expand(C, -1, -1), stride=2, groups=C)
     xu = xu[..., 15:-15]
     # SnakeBeta :146-159
-    alpha = torch.exp(alpha_log).view(1, -1, 1)
-    beta = torch.exp(beta_log).view(1, -1, 1)
+    alpha = (torch.exp(alpha_log) if logscale else alpha_log).view(1, -1, 1)
+    beta = (torch.exp(beta_log) if logscale else beta_log).view(1, -1, 1)
     xu = xu + (1.0 / (beta + 0.000000001)) * torch.pow(torch.sin(xu * alpha), 2)
     # DownSample1d -> LowPassFilter1d :224-231 (pad_left 5, pad_right 6, stride 2)
     xd = F.pad(xu, (5, 6), mode="replicate")
     return F.conv1d(xd, f.expand(C, -1, -1), stride=2, groups=C)
 
 
-def _act(sd, name, x):
-    return activation1d(x, _t(sd, name + ".act.alpha"), _t(sd, name + ".act.beta"), _t(sd, name + ".upsample.filter"))
+def _act(sd, name, x, logscale=True):
+    """SnakeBeta when the state has `.act.beta`, else Snake (x + 1/(alpha+1e-9) sin^2(alpha x), :84-92)."""
+    alpha = _t(sd, name + ".act.alpha")
+    beta = _t(sd, name + ".act.beta") if name + ".act.beta" in sd else alpha
+    return activation1d(x, alpha, beta, _t(sd, name + ".upsample.filter"), logscale)
 
 
 def bigvgan_forward(sd, vcfg, mel):
-    """modules/bigvgan.py:600-622 (Generator.forward) with AMPBlock1.forward :424-433.
-    mel f32[B,100,T] -> f32[B,1,256T]."""
+    """modules/bigvgan.py:600-622 (Generator.forward) with AMPBlock1.forward :424-433 or AMPBlock2.forward :506-512
+    (`resblock` "2": x = x + conv_d(act(x)) per dilation, one conv each). mel f32[B,100,T] -> f32[B,1,256T]."""
+    ls = bool(getattr(vcfg, "snake_logscale", True))
+    rb2 = str(getattr(vcfg, "resblock", "1")) == "2"
     x = F.conv1d(mel, _wn(sd, "conv_pre"), _t(sd, "conv_pre.bias"), padding=3)
     nk = len(vcfg.resblock_kernel_sizes)
     for i, (u, k) in enumerate(zip(vcfg.upsample_rates, vcfg.upsample_kernel_sizes)):
@@ -287,14 +293,20 @@ def bigvgan_forward(sd, vcfg, mel):
             rb = f"resblocks.{i * nk + j}."
             xr = x
             for l, d in enumerate(dd):
-                xt = _act(sd, rb + f"activations.{2 * l}", xr)
+                if rb2:
+                    xt = _act(sd, rb + f"activations.{l}", xr, ls)
+                    xt = F.conv1d(xt, _wn(sd, rb + f"convs.{l}"), _t(sd, rb + f"convs.{l}.bias"), dilation=d,
+                                  padding=(kk * d - d) // 2)
+                    xr = xt + xr
+                    continue
+                xt = _act(sd, rb + f"activations.{2 * l}", xr, ls)
                 xt = F.conv1d(xt, _wn(sd, rb + f"convs1.{l}"), _t(sd, rb + f"convs1.{l}.bias"), dilation=d, padding=(kk * d - d) // 2)
-                xt = _act(sd, rb + f"activations.{2 * l + 1}", xt)
+                xt = _act(sd, rb + f"activations.{2 * l + 1}", xt, ls)
                 xt = F.conv1d(xt, _wn(sd, rb + f"convs2.{l}"), _t(sd, rb + f"convs2.{l}.bias"), padding=(kk - 1) // 2)
                 xr = xt + xr
             xs = xr if xs is None else xs + xr
         x = xs / nk
-    x = _act(sd, "activation_post", x)
+    x = _act(sd, "activation_post", x, ls)
     x = F.conv1d(x, _wn(sd, "conv_post"), _t(sd, "conv_post.bias"), padding=3)
     return torch.tanh(x)
 

@@ -305,6 +305,7 @@ struct svc_ctx {
   // vocoder
   bool has_vocoder = false;
   int v_in = 100, v_c0 = 1536;
+  bool v_rb2 = false;  // vocoder resblocks are AMPBlock2 (config resblock "2")
   PackedGemm vpre;
   std::vector<VStage> vstages;
   ActP vact_post;
@@ -987,9 +988,18 @@ int build_mapper(svc_ctx* c) {
 }
 
 // ---------------------------------------------------------------------------- finalize: vocoder
+// Activation1d parameters (modules/bigvgan.py:234-307). The kernels take log-scale SnakeBeta parameters: the
+// magnitude term is 1 / (exp(beta) + 1e-9) and the frequency exp(alpha). Snake (:42-92) is SnakeBeta with beta = alpha;
+// linear-scale parameters (snake_logscale = false) are passed as their logarithms, which needs them positive.
 int get_act(svc_ctx* c, const std::string& name, int ch, ActP& a) {
+  const bool snake = cfgv(c, "vocoder.snake", 0) != 0;
+  const bool logscale = cfgv(c, "vocoder.snake_logscale", 1) != 0;
   GETP(al, name + ".act.alpha", ch);
-  GETP(be, name + ".act.beta", ch);
+  const Param* be = al;
+  if (!snake) {
+    GETP(b, name + ".act.beta", ch);
+    be = b;
+  }
   GETP(fu, name + ".upsample.filter", 1, 1, 12);
   GETP(fd, name + ".downsample.lowpass.filter", 1, 1, 12);
   for (int i = 0; i < 12; ++i)
@@ -997,8 +1007,20 @@ int get_act(svc_ctx* c, const std::string& name, int ch, ActP& a) {
       set_error("%s: up/down filters differ (unsupported)", name.c_str());
       return SVC_ERR_INVALID;
     }
+  std::vector<float> av(al->host, al->host + ch), bv(be->host, be->host + ch);
+  if (!logscale) {
+    for (int i = 0; i < ch; ++i) {
+      if (!(av[i] > 0.f) || !(bv[i] > 0.f)) {
+        set_error("%s: snake_logscale=false needs positive alpha/beta (channel %d: %g, %g)", name.c_str(), i, av[i],
+                  bv[i]);
+        return SVC_ERR_INVALID;
+      }
+      av[i] = logf(av[i]);
+      bv[i] = logf(bv[i]);
+    }
+  }
   int st;
-  if ((st = upload_param(c, al, &a.alpha)) || (st = upload_param(c, be, &a.beta)) || (st = upload_param(c, fu, &a.filt)))
+  if ((st = upload_vec(c, av, &a.alpha)) || (st = upload_vec(c, bv, &a.beta)) || (st = upload_param(c, fu, &a.filt)))
     return st;
   return SVC_OK;
 }
@@ -1010,6 +1032,7 @@ int build_vocoder(svc_ctx* c) {
   const int vin = (int)cfgv(c, "vocoder.input_dim", 100);
   c->v_c0 = C0;
   c->v_in = vin;
+  c->v_rb2 = cfgv(c, "vocoder.resblock", 1) == 2;
   int st;
   GETP(pv, "vocoder.conv_pre.weight_v", C0, vin, 7);
   GETP(pg, "vocoder.conv_pre.weight_g", C0, 1, 1);
@@ -1051,6 +1074,17 @@ int build_vocoder(svc_ctx* c) {
         const int d =
             (int)cfgv(c, ("vocoder.resblock_dilation_sizes." + std::to_string(j) + "." + std::to_string(l)).c_str(), 1);
         S.rd[j][l] = d;
+        if (c->v_rb2) {  // AMPBlock2 (modules/bigvgan.py:442-512): x = x + convs[l](activations[l](x)), dilation d
+          std::string n = rb + "convs." + std::to_string(l) + ".";
+          GETP(v, n + "weight_v", ch, ch, kk);
+          GETP(g, n + "weight_g", ch, 1, 1);
+          GETP(bb, n + "bias", ch);
+          if ((st = pack_conv1d(c, S.c2[j][l], v->host, bb->host, ch, ch, kk, ch, d, (kk * d - d) / 2, 1, nullptr,
+                                g->host)))
+            return st;
+          if ((st = get_act(c, rb + "activations." + std::to_string(l), ch, S.acts[j][2 * l + 1]))) return st;
+          continue;
+        }
         std::string n1 = rb + "convs1." + std::to_string(l) + ".", n2 = rb + "convs2." + std::to_string(l) + ".";
         GETP(v1, n1 + "weight_v", ch, ch, kk);
         GETP(g1, n1 + "weight_g", ch, 1, 1);
@@ -2085,29 +2119,38 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
       for (int j = 0; j < nk; ++j) {
         const int nd = (int)S.c1[j].size();
         for (int l = 0; l < nd; ++l) {
-          const float* src = (l == 0) ? Xh : Xjh;
+          // AMPBlock2 reads its activation halo from the x it updates, so its x ping-pongs between Xj and tmp
+          // (AMPBlock1 updates x in place: its second activation reads tmp)
+          const float* src = (l == 0) ? Xh : ((c->v_rb2 && l % 2 == 0) ? tmph : Xjh);
+          float* xnext = (c->v_rb2 && l % 2 == 1) ? tmph : Xjh;
           const ActP& a1 = S.acts[j][2 * l];
           const ActP& a2 = S.acts[j][2 * l + 1];
+          // AMPBlock1: tmp = c1(a1(x)), x' = x + c2(a2(tmp)); AMPBlock2: x' = x + c(a(x)) with c = c2[l] (dilation d)
+          const bool rb2 = c->v_rb2;
+          const int d2 = rb2 ? S.rd[j][l] : 1;
+          const float* act_in = rb2 ? src : tmph;  // input of the activation before the second (or only) conv
           // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
           const bool fuse = use_amp && ch <= amp_maxc && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
-          EpiArgs e1 = epi();
-          e1.out32 = tmph;
-          e1.ld32 = ch;
-          if (fuse) {
-            const PackedGemm& g1 = S.c1[j][l];
-            const AmpConvArgs p1{src, Bh, L, S.rk[j], S.rd[j][l], a1.alpha, a1.beta, a1.filt, g1.W, g1.Kpad, g1.bias};
-            prof_site("bigvgan.amp_c1");
-            if ((st = amp_conv(p1, ch, e1, sh))) return st;
-          } else {
-            if ((st = activation1d(src, a16h, Bh, L, ch, ch, a1.alpha, a1.beta, a1.filt, sh))) return st;
-            if ((st = run_gemm(S.c1[j][l], a16h, ch, ch, Bh, L, L, e1, sh, "bigvgan.amp_c1"))) return st;
-            if ((st = activation1d(tmph, a16h, Bh, L, ch, ch, a2.alpha, a2.beta, a2.filt, sh))) return st;
+          if (!rb2) {
+            EpiArgs e1 = epi();
+            e1.out32 = tmph;
+            e1.ld32 = ch;
+            if (fuse) {
+              const PackedGemm& g1 = S.c1[j][l];
+              const AmpConvArgs p1{src, Bh, L, S.rk[j], S.rd[j][l], a1.alpha, a1.beta, a1.filt, g1.W, g1.Kpad, g1.bias};
+              prof_site("bigvgan.amp_c1");
+              if ((st = amp_conv(p1, ch, e1, sh))) return st;
+            } else {
+              if ((st = activation1d(src, a16h, Bh, L, ch, ch, a1.alpha, a1.beta, a1.filt, sh))) return st;
+              if ((st = run_gemm(S.c1[j][l], a16h, ch, ch, Bh, L, L, e1, sh, "bigvgan.amp_c1"))) return st;
+            }
           }
+          if (!fuse && (st = activation1d(act_in, a16h, Bh, L, ch, ch, a2.alpha, a2.beta, a2.filt, sh))) return st;
           EpiArgs e2 = epi();
           e2.add_row = src;
           e2.ld_add_row = ch;
           if (l + 1 < nd) {
-            e2.out32 = Xjh;
+            e2.out32 = xnext;
             e2.ld32 = ch;
           } else if (j == 0) {
             e2.out32 = XSh;
@@ -2131,7 +2174,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
           }
           if (fuse) {
             const PackedGemm& g2 = S.c2[j][l];
-            const AmpConvArgs p2{tmph, Bh, L, S.rk[j], 1, a2.alpha, a2.beta, a2.filt, g2.W, g2.Kpad, g2.bias};
+            const AmpConvArgs p2{act_in, Bh, L, S.rk[j], d2, a2.alpha, a2.beta, a2.filt, g2.W, g2.Kpad, g2.bias};
             prof_site("bigvgan.amp_c2");
             if ((st = amp_conv(p2, ch, e2, sh))) return st;
           } else if ((st = run_gemm(S.c2[j][l], a16h, ch, ch, Bh, L, L, e2, sh, "bigvgan.amp_c2"))) {

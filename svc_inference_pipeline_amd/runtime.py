@@ -82,6 +82,12 @@ class SVCEngine:
         kv["vocoder.n_kernels"] = len(v.resblock_kernel_sizes)
         kv["vocoder.upsample_initial_channel"] = v.upsample_initial_channel
         kv["vocoder.input_dim"] = v.input_dim
+        # modules/bigvgan.py:536 (AMPBlock1 if resblock == "1" else AMPBlock2), :392-421 snake / snakebeta
+        kv["vocoder.resblock"] = 2 if str(v.resblock) == "2" else 1
+        if v.activation not in ("snake", "snakebeta"):
+            raise ValueError(f"vocoder.activation {v.activation!r}: snake or snakebeta (modules/bigvgan.py:392-421)")
+        kv["vocoder.snake"] = 1 if v.activation == "snake" else 0
+        kv["vocoder.snake_logscale"] = 1 if v.snake_logscale else 0
         for i, (u, k) in enumerate(zip(v.upsample_rates, v.upsample_kernel_sizes)):
             kv[f"vocoder.upsample_rates.{i}"] = u
             kv[f"vocoder.upsample_kernel_sizes.{i}"] = k

@@ -160,17 +160,45 @@ def _wn_conv(sd, seed, name, w_shape, fan_in, bias_n):
     sd[name + ".bias"] = _normal(seed, name + ".bias", (bias_n,), 0.02)
 
 
-def _act(sd, seed, name, ch):
+def _act(sd, seed, name, ch, kind="snakebeta", logscale=True):
+    """Activation1d params (modules/bigvgan.py:234-307): SnakeBeta has alpha and beta, Snake (:42-92) alpha only;
+    log-scale parameters are drawn around 0, linear-scale ones around 1 (the reference's initialisations)."""
     f = kaiser_sinc_filter1d(0.25, 0.3, 12).numpy()
-    sd[name + ".act.alpha"] = _normal(seed, name + ".act.alpha", (ch,), 0.3)
-    sd[name + ".act.beta"] = _normal(seed, name + ".act.beta", (ch,), 0.3)
+    mean = 0.0 if logscale else 1.0
+    sd[name + ".act.alpha"] = _normal(seed, name + ".act.alpha", (ch,), 0.3 if logscale else 0.1, mean=mean)
+    if kind == "snakebeta":
+        sd[name + ".act.beta"] = _normal(seed, name + ".act.beta", (ch,), 0.3 if logscale else 0.1, mean=mean)
     sd[name + ".upsample.filter"] = f.copy()
     sd[name + ".downsample.lowpass.filter"] = f.copy()
 
 
+# BigVGAN configurations infer.py does not use but the config can select (SURVEY.md §8(f) F4): AMPBlock2
+# (modules/bigvgan.py:442-516, dilations (1, 3)) and Snake (:42-92) in log or linear scale
+VOCODER_VARIANTS = {
+    "amp2_snake_log": dict(resblock="2", activation="snake", snake_logscale=True, dil=[[1, 3], [1, 3], [1, 3]]),
+    "amp2_snake_lin": dict(resblock="2", activation="snake", snake_logscale=False, dil=[[1, 3], [1, 3], [1, 3]]),
+    "amp1_snake_log": dict(resblock="1", activation="snake", snake_logscale=True, dil=None),
+}
+
+
+def vocoder_variant_cfg(vcfg, name):
+    """A copy of the vocoder config with one of VOCODER_VARIANTS applied."""
+    import copy
+    v = VOCODER_VARIANTS[name]
+    c = copy.deepcopy(vcfg)
+    c.resblock = v["resblock"]
+    c.activation = v["activation"]
+    c.snake_logscale = v["snake_logscale"]
+    if v["dil"] is not None:
+        c.resblock_dilation_sizes = [list(d) for d in v["dil"]]
+    return c
+
+
 def make_vocoder_state(vcfg, seed=0):
-    """State dict of bigvgan.Generator (modules/bigvgan.py:519-598), AMPBlock1 + SnakeBeta."""
-    assert vcfg.resblock == "1" and vcfg.activation == "snakebeta"
+    """State dict of bigvgan.Generator (modules/bigvgan.py:519-598): AMPBlock1 (convs1 / convs2, :336-440) or
+    AMPBlock2 (convs, :442-516), SnakeBeta or Snake activations (log or linear scale)."""
+    assert vcfg.resblock in ("1", "2") and vcfg.activation in ("snake", "snakebeta")
+    kind, logscale = vcfg.activation, bool(vcfg.snake_logscale)
     sd = {}
     C0 = vcfg.upsample_initial_channel
     _wn_conv(sd, seed, "conv_pre", (C0, vcfg.input_dim, 7), vcfg.input_dim * 7, C0)
@@ -182,13 +210,19 @@ def make_vocoder_state(vcfg, seed=0):
         ch = C0 // (2 ** (i + 1))
         for j, (k, d) in enumerate(zip(vcfg.resblock_kernel_sizes, vcfg.resblock_dilation_sizes)):
             rb = f"resblocks.{i * nk + j}."
-            for l in range(len(d)):
-                _wn_conv(sd, seed, rb + f"convs1.{l}", (ch, ch, k), ch * k, ch)
-                _wn_conv(sd, seed, rb + f"convs2.{l}", (ch, ch, k), ch * k, ch)
-            for a in range(2 * len(d)):
-                _act(sd, seed, rb + f"activations.{a}", ch)
+            if vcfg.resblock == "1":
+                for l in range(len(d)):
+                    _wn_conv(sd, seed, rb + f"convs1.{l}", (ch, ch, k), ch * k, ch)
+                    _wn_conv(sd, seed, rb + f"convs2.{l}", (ch, ch, k), ch * k, ch)
+                n_act = 2 * len(d)
+            else:
+                for l in range(len(d)):
+                    _wn_conv(sd, seed, rb + f"convs.{l}", (ch, ch, k), ch * k, ch)
+                n_act = len(d)
+            for a in range(n_act):
+                _act(sd, seed, rb + f"activations.{a}", ch, kind, logscale)
     ch = C0 // (2 ** len(vcfg.upsample_rates))
-    _act(sd, seed, "activation_post", ch)
+    _act(sd, seed, "activation_post", ch, kind, logscale)
     _wn_conv(sd, seed, "conv_post", (1, ch, 7), ch * 7, 1)
     return sd
 

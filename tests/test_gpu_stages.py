@@ -189,6 +189,35 @@ def test_bigvgan(engine, cfg, states, golden):
     assert rel_l2(wav[0].cpu().numpy(), g["synth"]) < budget
 
 
+@pytest.mark.parametrize("variant", list(W.VOCODER_VARIANTS))
+def test_bigvgan_variants(cfg, states, golden, variant, monkeypatch):
+    """F4: AMPBlock2 / Snake (log and linear scale) generators against the oracle, which
+    tests/test_oracle_golden.py::test_bigvgan_variants pins to the reference's own Generator. Both the fused
+    small-channel path (amp_conv, C <= 48) and the unfused activation1d + GEMM path (SVC_AMP_MAXC=0) are checked,
+    with test_bigvgan's tolerance (1.5 x the fp16-operand emulation's distance + 1e-3)."""
+    import copy
+    g = golden("bigvgan_variants")
+    c2 = copy.deepcopy(cfg)
+    c2.vocoder = W.vocoder_variant_cfg(cfg.vocoder, variant)
+    vsd = W.make_vocoder_state(c2.vocoder, 0)
+    stats = C.load_stats(c2)
+    mel = g["mel"]
+    T = mel.shape[-1]
+    x_norm = (mel - stats["mel_min"][:, None]) / (stats["mel_max"] - stats["mel_min"] + 1e-12)[:, None] * 2 - 1
+    ref = OF.synthesis_fade(torch.from_numpy(g[variant][0, 0]), T).numpy()
+    with OM.Fp16Operands():
+        emu = OM.bigvgan_forward(vsd, c2.vocoder, torch.from_numpy(mel)[None])
+    budget = 1.5 * rel_l2(OF.synthesis_fade(emu[0, 0], T).numpy(), ref) + 1e-3
+    e = SVCEngine(c2, 0, mapper_state=states["mapper"], vocoder_state=vsd)
+    try:
+        for maxc in ("48", "0"):
+            monkeypatch.setenv("SVC_AMP_MAXC", maxc)
+            wav = e.bigvgan(dev(x_norm.T[None].astype(np.float32)))[0].cpu().numpy()
+            assert rel_l2(wav, ref) < budget, (maxc, rel_l2(wav, ref), budget)
+    finally:
+        e.close()
+
+
 def test_vocoder_sub_streams_bit_identical(engine, monkeypatch):
     """BigVGAN with utterance-aligned sub-batches on 1, 2 or 3 streams: identical waveforms."""
     rng = np.random.default_rng(1)

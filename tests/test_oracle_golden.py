@@ -143,6 +143,17 @@ def test_bigvgan_and_synthesis(golden):
     np.testing.assert_allclose(syn.numpy(), g["synth"], rtol=0, atol=2e-5)
 
 
+@pytest.mark.parametrize("variant", ["amp2_snake_log", "amp2_snake_lin", "amp1_snake_log"])
+def test_bigvgan_variants(golden, variant):
+    """F4: AMPBlock2 and Snake (log and linear scale), pinned to the reference's own Generator
+    (tools/make_goldens_amp2.py)."""
+    g = golden("bigvgan_variants")
+    vcfg = W.vocoder_variant_cfg(C.load_config().vocoder, variant)
+    vsd = W.make_vocoder_state(vcfg, seed=0)
+    wav = OM.bigvgan_forward(vsd, vcfg, torch.from_numpy(g["mel"]).unsqueeze(0))
+    np.testing.assert_allclose(wav.numpy(), g[variant], rtol=0, atol=2e-5)
+
+
 def test_format_golden(golden):
     """Config 1 format (gen/1100000814_svcc_CDF1.wav): 24 kHz, 1200 + 379*256 + 1200 samples,
     peak -29491 = round(-0.9*32768), silent padding (utils/util.py:20-37)."""
