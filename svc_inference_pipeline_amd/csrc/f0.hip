@@ -22,6 +22,7 @@ constexpr int F0_MAXC = 16;  // >= max candidates (15 for the parselmouth defaul
 
 struct F0Params {
   int nsp, hnsp, nw, hnw, maxlag, nf, bmax, maxc;
+  int dbg;  // diagnostics (SVC_F0_DBG): 1 = stop after the autocorrelation, 2 = skip the Brent refinement
   double dx, t1, x1, ts, floor_hz, ceiling, voicing, silence, octave_cost, octave_jump, vuv_cost;
 };
 
@@ -101,12 +102,57 @@ __device__ double sinc_interp(const double* y, int n, double x, int depth) {
   return result;
 }
 
-// NUMminimize_brent on f(x) = -sinc_interp(y, x, depth) over [a, b]; returns x, *fx = f(x)
-__device__ double brent_neg_sinc(const double* y, int n, int depth, double a, double b, double tol, double* fxo) {
+// sinc_interp evaluated by a whole wave (x and depth wave-uniform; every lane returns the same value): the 2 * depth
+// terms are spread over the lanes, each lane computing its terms' angles directly (cos(aa + q * daa)) instead of by
+// the serial rotation recurrence, then a wave sum. Equal to sinc_interp up to rounding (~1e-16 relative).
+__device__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ double sinc_interp_wave(const double* y, int n, double x, int depth, int lane) {
+  const int midleft = (int)floor(x), midright = midleft + 1;
+  if (x > n) return y[n - 1];
+  if (x < 1) return y[0];
+  if (x == (double)midleft) return y[midleft - 1];
+  if (depth > midright - 1) depth = midright - 1;
+  if (depth > n - midleft) depth = n - midleft;
+  if (depth <= 2) return sinc_interp(y, n, x, depth);
+  const int left = midright - depth, right = midleft + depth;
+  double part = 0.0;
+  {  // left terms ix = midleft - q, q < depth
+    const double a0 = M_PI * (x - midleft);
+    const double hs = 0.5 * sin(a0);
+    const double aa = a0 / (x - left + 1.0), daa = M_PI / (x - left + 1.0);
+    for (int q = lane; q < depth; q += 64) {
+      const double a = a0 + q * M_PI;
+      const double d = ((q & 1) ? -hs : hs) / a * (1.0 + cos(aa + q * daa));
+      part += y[midleft - q - 1] * d;
+    }
+  }
+  {  // right terms ix = midright + q
+    const double a0 = M_PI * (midright - x);
+    const double hs = 0.5 * sin(a0);
+    const double aa = a0 / (right - x + 1.0), daa = M_PI / (right - x + 1.0);
+    for (int q = lane; q < depth; q += 64) {
+      const double a = a0 + q * M_PI;
+      const double d = ((q & 1) ? -hs : hs) / a * (1.0 + cos(aa + q * daa));
+      part += y[midright + q - 1] * d;
+    }
+  }
+  return wave_sum(part);
+}
+
+// NUMminimize_brent on f(x) = -sinc(y, x, depth) over [a, b]; returns x, *fx = f(x). SINC is sinc_interp (one lane)
+// or sinc_interp_wave (a whole wave, uniform control flow).
+template <typename SINC>
+__device__ double brent_neg_sinc(SINC sinc, const double* y, int n, int depth, double a, double b, double tol,
+                                 double* fxo) {
   const double golden = 1.0 - 0.6180339887498949;
   const double sqrt_eps = 1.4901161193847656e-08;  // sqrt(DBL_EPSILON)
   double v = a + golden * (b - a);
-  double fv = -sinc_interp(y, n, v, depth);
+  double fv = -sinc(y, n, v, depth);
   double x = v, w = v, fx = fv, fw = fv;
   for (int it = 0; it < 60; ++it) {
     const double range = b - a, middle = (a + b) / 2;
@@ -124,7 +170,7 @@ __device__ double brent_neg_sinc(const double* y, int n, int depth, double a, do
     }
     if (fabs(new_step) < tol_act) new_step = new_step > 0 ? tol_act : -tol_act;
     const double t = x + new_step;
-    const double ft = -sinc_interp(y, n, t, depth);
+    const double ft = -sinc(y, n, t, depth);
     if (ft <= fx) {
       if (t < x) b = x; else a = x;
       v = w; w = x; x = t;
@@ -226,6 +272,8 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
   double* frame = sm;               // [nw]
   double* r = frame + P.nw;         // [2*bmax+1], lag L at r[L + bmax]
   double* red = r + 2 * P.bmax + 1; // [8]
+  double* pkf = red + 8;             // [bmax + 1] first pass: peak frequency at lag i (0 = not a candidate peak)
+  double* pks = pkf + P.bmax + 1;    // [bmax + 1] ... and its sinc(30) strength
   __shared__ double cf[F0_MAXC], cs[F0_MAXC];
   __shared__ int cim[F0_MAXC];
   __shared__ int ncs;
@@ -276,20 +324,32 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
   }
   if (threadIdx.x == 0) r[P.bmax] = 1.0;
   __syncthreads();
+  if (P.dbg == 1) return;
   const int rn = 2 * P.bmax + 1;
-  if (threadIdx.x == 0) {
+  const int iend = P.maxlag < P.bmax ? P.maxlag : P.bmax;
+  // first pass, in parallel over lags: local maxima above half the voicing threshold and their sinc(30) strengths
+  for (int i = 2 + threadIdx.x; i < iend; i += blockDim.x) {
+    const double ri = r[P.bmax + i], rm = r[P.bmax + i - 1], rp = r[P.bmax + i + 1];
+    double freq = 0.0, strength = 0.0;
+    if (ri > 0.5 * P.voicing && ri > rm && ri >= rp) {
+      const double dr = 0.5 * (rp - rm), d2r = 2.0 * ri - rm - rp;
+      freq = 1.0 / P.dx / (i + dr / d2r);
+      strength = sinc_interp(r, rn, 1.0 / P.dx / freq + P.bmax + 1, 30);
+      if (strength > 1.0) strength = 1.0 / strength;
+    }
+    pkf[i] = freq;
+    pks[i] = strength;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // ... then the candidate list in lag order (Praat's replacement rule is sequential)
     int nc = 1;
     cf[0] = 0.0;
     cs[0] = 0.0;
     cim[0] = 0;
-    const int iend = P.maxlag < P.bmax ? P.maxlag : P.bmax;
     for (int i = 2; i < iend; ++i) {
-      const double ri = r[P.bmax + i], rm = r[P.bmax + i - 1], rp = r[P.bmax + i + 1];
-      if (ri > 0.5 * P.voicing && ri > rm && ri >= rp) {
-        const double dr = 0.5 * (rp - rm), d2r = 2.0 * ri - rm - rp;
-        const double freq = 1.0 / P.dx / (i + dr / d2r);
-        double strength = sinc_interp(r, rn, 1.0 / P.dx / freq + P.bmax + 1, 30);
-        if (strength > 1.0) strength = 1.0 / strength;
+      if (pkf[i] != 0.0) {
+        const double freq = pkf[i];
+        const double strength = pks[i];
         int place = 0;
         if (nc < P.maxc) {
           place = nc++;
@@ -316,8 +376,10 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
   __syncthreads();
   const int nc = ncs;
   const int k = threadIdx.x;
-  if (k >= 1 && k < nc) {  // second pass: sinc(70) maximum by Brent, one lane per candidate
-    const int ixmid = cim[k] + P.bmax + 1;
+  // second pass: sinc(70) maximum by Brent, one WAVE per candidate (the sinc sums spread over its lanes)
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int kc = 1 + wave; kc < nc && P.dbg != 2; kc += (int)(blockDim.x >> 6)) {
+    const int ixmid = cim[kc] + P.bmax + 1;
     double xmid, ymid;
     if (ixmid <= 1) {
       xmid = 1.0;
@@ -327,14 +389,17 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
       ymid = r[rn - 1];
     } else {
       double fx;
-      xmid = brent_neg_sinc(r, rn, 70, ixmid - 1, ixmid + 1, 1e-10, &fx);
+      auto sw = [lane](const double* y, int n, double x, int depth) { return sinc_interp_wave(y, n, x, depth, lane); };
+      xmid = brent_neg_sinc(sw, r, rn, 70, ixmid - 1, ixmid + 1, 1e-10, &fx);
       ymid = -fx;
     }
     xmid -= P.bmax + 1;
     double freq = 1.0 / P.dx / xmid;
     if (ymid > 1.0) ymid = 1.0 / ymid;
-    cf[k] = freq;
-    cs[k] = ymid;
+    if (lane == 0) {
+      cf[kc] = freq;
+      cs[kc] = ymid;
+    }
   }
   __syncthreads();
   if (k < nc) {
@@ -345,54 +410,91 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
 }
 
 // Pitch_pathFinder + padding to T (one wave per utterance)
-__global__ void f0_path_kernel(F0Params P, F0Out o, int* __restrict__ psi, int T, int pad, double* __restrict__ f0out) {
+// ps_lds: the back-pointers of all frames fit in dynamic LDS as bytes (nf * F0_MAXC bytes), so the final serial
+// backtrack chases LDS instead of global memory; otherwise they go to psi (global).
+__global__ void f0_path_kernel(F0Params P, F0Out o, int* __restrict__ psi, int T, int pad, double* __restrict__ f0out,
+                               int ps_lds) {
+  extern __shared__ unsigned char psl[];
   const int b = blockIdx.x;
   const int j = threadIdx.x;
-  __shared__ double dprev[F0_MAXC], dcur[F0_MAXC];
+  const int jc = threadIdx.x >> 4, kk = threadIdx.x & 15;  // blockDim = 16 * F0_MAXC... at least F0_MAXC x 16
+  // The Viterbi recursion is serial over frames, so each step must not wait on global memory: the candidates of
+  // F0_PCH frames at a time are staged in LDS by the whole block (one load latency per chunk instead of several per
+  // frame), and the previous frame's frequencies stay in LDS. Same arithmetic as before, value for value.
+  constexpr int F0_PCH = 64;
+  __shared__ double dprev[F0_MAXC], dcur[F0_MAXC], pfr[F0_MAXC], dlv[F0_MAXC];
+  __shared__ double vals[F0_MAXC][16];
+  __shared__ double cfr[F0_PCH][F0_MAXC], cst[F0_PCH][F0_MAXC], cin[F0_PCH];
+  __shared__ int cnc[F0_PCH];
+  __shared__ int pnc;
   const double tsc = 0.01 / P.ts;
   const double ojc = P.octave_jump * tsc, vuv = P.vuv_cost * tsc;
   const double ceil2 = P.ceiling;
   int* ps = psi + (int64_t)b * P.nf * F0_MAXC;
   for (int i = 0; i < P.nf; ++i) {
     const int gf = b * P.nf + i;
-    const int nc = o.ncand[gf];
-    double dl = 0;
-    double f2 = 0;
-    if (j < nc) {
-      const double inten = o.inten[gf];
+    const int li = i % F0_PCH;
+    if (li == 0) {
+      __syncthreads();
+      const int nch = min(F0_PCH, P.nf - i);
+      for (int q = j; q < nch * F0_MAXC; q += blockDim.x) {
+        const int fi = q / F0_MAXC, c = q - fi * F0_MAXC;
+        cfr[fi][c] = o.freq[(int64_t)(gf + fi) * F0_MAXC + c];
+        cst[fi][c] = o.str[(int64_t)(gf + fi) * F0_MAXC + c];
+      }
+      for (int q = j; q < nch; q += blockDim.x) {
+        cnc[q] = o.ncand[gf + q];
+        cin[q] = o.inten[gf + q];
+      }
+      __syncthreads();
+    }
+    const int nc = cnc[li];
+    // thread (jc, kk): jc = candidate of this frame, kk = candidate of the previous frame; the kk == 0 threads own jc
+    if (kk == 0 && jc < nc) {
+      const double inten = cin[li];
       double us = P.silence <= 0 ? 0 : 2.0 - inten / (P.silence / (1.0 + P.voicing));
       us = P.voicing + (us > 0 ? us : 0.0);
-      f2 = o.freq[(int64_t)gf * F0_MAXC + j];
+      const double f2 = cfr[li][jc];
       const bool voiced = f2 > 0.0 && f2 < ceil2;
-      dl = voiced ? o.str[(int64_t)gf * F0_MAXC + j] - P.octave_cost * log2(P.ceiling / f2) : us;
+      dlv[jc] = voiced ? cst[li][jc] - P.octave_cost * log2(P.ceiling / f2) : us;
     }
+    __syncthreads();
     if (i == 0) {
-      if (j < nc) dcur[j] = dl;
+      if (kk == 0 && jc < nc) dcur[jc] = dlv[jc];
     } else {
-      const int gp = gf - 1;
-      const int np = o.ncand[gp];
-      if (j < nc) {
+      const int np = pnc;
+      if (jc < nc && kk < np) {  // every transition of the step at once (the log2s were the serial chain)
+        const double f2 = cfr[li][jc];
+        const bool v2 = f2 > 0.0 && f2 < ceil2;
+        const double f1 = pfr[kk];
+        const bool v1 = f1 > 0.0 && f1 < ceil2;
+        double tc;
+        if (!v2) tc = v1 ? vuv : 0.0;
+        else tc = v1 ? ojc * fabs(log2(f1 / f2)) : vuv;
+        vals[jc][kk] = dprev[kk] - tc + dlv[jc];
+      }
+      __syncthreads();
+      if (kk == 0 && jc < nc) {  // best predecessor in kk order, first maximum wins (as the serial loop)
         double best = -1e30;
         int place = 0;
-        const bool v2 = f2 > 0.0 && f2 < ceil2;
-        for (int kk = 0; kk < np; ++kk) {
-          const double f1 = o.freq[(int64_t)gp * F0_MAXC + kk];
-          const bool v1 = f1 > 0.0 && f1 < ceil2;
-          double tc;
-          if (!v2) tc = v1 ? vuv : 0.0;
-          else tc = v1 ? ojc * fabs(log2(f1 / f2)) : vuv;
-          const double val = dprev[kk] - tc + dl;
-          if (val > best) {
-            best = val;
-            place = kk;
+        for (int q = 0; q < np; ++q)
+          if (vals[jc][q] > best) {
+            best = vals[jc][q];
+            place = q;
           }
-        }
-        dcur[j] = best;
-        ps[(int64_t)i * F0_MAXC + j] = place;
+        dcur[jc] = best;
+        if (ps_lds)
+          psl[i * F0_MAXC + jc] = (unsigned char)place;
+        else
+          ps[(int64_t)i * F0_MAXC + jc] = place;
       }
     }
     __syncthreads();
-    if (j < nc) dprev[j] = dcur[j];
+    if (kk == 0 && jc < nc) {
+      dprev[jc] = dcur[jc];
+      pfr[jc] = cfr[li][jc];
+    }
+    if (threadIdx.x == 0) pnc = nc;
     __syncthreads();
   }
   if (j == 0) {
@@ -410,7 +512,7 @@ __global__ void f0_path_kernel(F0Params P, F0Out o, int* __restrict__ psi, int T
       const int gf = b * P.nf + i;
       const int t = pad + i;
       if (t >= 0 && t < T) out[t] = o.freq[(int64_t)gf * F0_MAXC + place];
-      place = i > 0 ? ps[(int64_t)i * F0_MAXC + place] : 0;
+      place = i > 0 ? (ps_lds ? (int)psl[i * F0_MAXC + place] : ps[(int64_t)i * F0_MAXC + place]) : 0;
     }
   }
 }
@@ -428,6 +530,7 @@ int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double
   SVC_REQUIRE(P.nf >= 1, "f0: sound (%lld samples) shorter than the 3-period window", (long long)n);
   SVC_REQUIRE(P.nw <= 2048 && P.maxc <= F0_MAXC, "f0: window %d / candidates %d too large", P.nw, P.maxc);
   P.voicing = voicing;
+  if (const char* dbg = getenv("SVC_F0_DBG")) P.dbg = atoi(dbg);
   P.silence = 0.03;
   P.octave_cost = 0.01;
   P.octave_jump = 0.35;
@@ -453,14 +556,16 @@ int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double
   SVC_LAUNCH_CHECK();
   hipLaunchKernelGGL(f0_window_kernel, dim3(1), dim3(256), 0, s, P.nw, P.bmax, win, winR);
   SVC_LAUNCH_CHECK();
-  const size_t lds = (size_t)(P.nw + 2 * P.bmax + 1 + 8) * sizeof(double);
+  const size_t lds = (size_t)(P.nw + 2 * P.bmax + 1 + 8 + 2 * (P.bmax + 1)) * sizeof(double);
   hipLaunchKernelGGL(f0_frame_kernel, dim3(P.nf, B), dim3(256), lds, s, wav, n, P, win, winR, gpeak, o);
   SVC_LAUNCH_CHECK();
   // utils/f0.py:156-157: pad = (len(audio)//hop - len(f0) + 1)//2 (python floor division)
   const int hop = (int)llround(ts * fs);
   const int64_t num = n / hop - P.nf + 1;
   const int pad = (int)(num >= 0 ? num / 2 : -((-num + 1) / 2));
-  hipLaunchKernelGGL(f0_path_kernel, dim3(B), dim3(64), 0, s, P, o, psi, T, pad, f0_out);
+  const int ps_lds = (size_t)P.nf * F0_MAXC <= 32768 ? 1 : 0;  // 10 s: 934 frames -> 15 KB
+  hipLaunchKernelGGL(f0_path_kernel, dim3(B), dim3(16 * F0_MAXC), ps_lds ? (size_t)P.nf * F0_MAXC : 0, s, P, o, psi, T,
+                     pad, f0_out, ps_lds);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
