@@ -17,7 +17,9 @@
  * Conventions
  *   - Tensors are caller-owned DEVICE buffers, time-major: row = b*T + t, channels contiguous.
  *   - Every call is asynchronous and ordered on `stream` (a hipStream_t; NULL = default stream).
- *   - One context per device; a context is not thread-safe.
+ *   - One context per device; a context is not thread-safe. Calls that share the context's workspace must be
+ *     ordered on one stream; svc_f0_ac and svc_pitch_shift are the exception (own workspace / none) and may run on
+ *     a second stream beside the content encoders (the host pipeline overlaps F0 with Whisper that way).
  *   - Parameters are given in the reference's own state_dict naming with a model prefix
  *     ("mapper.", "vocoder.", "whisper.") as host float32 arrays; they are folded (weight_norm),
  *     packed into MFMA layouts and uploaded by svc_ctx_finalize. Host arrays must stay valid until
@@ -50,6 +52,9 @@ svc_status svc_ctx_add_param(svc_ctx* ctx, const char* name, const float* host, 
 svc_status svc_ctx_finalize(svc_ctx* ctx);
 /* bytes of device memory held by packed weights / by the workspace arena */
 svc_status svc_ctx_memory(svc_ctx* ctx, int64_t* weight_bytes, int64_t* workspace_bytes);
+/* the context's sub-stream `index` (< 8; created on first use, owned by the context): lets a caller overlap
+   svc_f0_ac with the content encoder without creating a stream of its own */
+svc_status svc_ctx_stream(svc_ctx* ctx, int index, void** stream);
 
 /* A2/A3-energy: wav24k [B][n_samples] f32 -> mel [B*T][n_mels] f32 (log-mel, time-major), energy [B*T] f32.
    T = (n_samples + n_fft - hop - n_fft)/hop + 1 (bit-exact frame count, utils/mel.py:148-167). */
@@ -57,7 +62,8 @@ svc_status svc_mel_energy(svc_ctx* ctx, const float* wav24k, int B, int64_t n_sa
                           void* stream);
 
 /* A3-F0: Praat autocorrelation pitch (to_pitch_ac, voicing 0.6, floor f0_min, ceiling f0_max, time step hop/fs),
-   padded to T frames as utils/f0.py:156-157; unvoiced = 0. f0 [B*T] float64. */
+   padded to T frames as utils/f0.py:156-157; unvoiced = 0. f0 [B*T] float64. Uses its own workspace: may run on
+   another stream concurrently with the other stage calls of the same context (not with another svc_f0_ac). */
 svc_status svc_f0_ac(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, int T, double* f0, void* stream);
 
 /* A4: in place, f0 [B*T] float64 *= target_median / median(voiced f0 of that utterance)

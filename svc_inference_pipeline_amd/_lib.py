@@ -19,6 +19,7 @@ PROTOTYPES = {
     "svc_ctx_add_param": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int, ctypes.POINTER(c_int64)]),
     "svc_ctx_finalize": (c_int, [c_void_p]),
     "svc_ctx_memory": (c_int, [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)]),
+    "svc_ctx_stream": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),
     "svc_mel_energy": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p]),
     "svc_f0_ac": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p, c_void_p]),
     "svc_pitch_shift": (c_int, [c_void_p, c_void_p, c_int, c_int, c_double, c_void_p]),

@@ -23,6 +23,8 @@ overlap-add seams.
 """
 from dataclasses import dataclass
 
+import os
+
 import torch
 
 from .runtime import SVCEngine
@@ -91,15 +93,28 @@ class SVCPipeline:
         out.copy_(full.view(B, n_win * WINDOW_MEL_FRAMES, D))
         return out[:, :T].contiguous()
 
+    def _side_stream(self, device):
+        if getattr(self, "_side", None) is None:
+            self._side = self.engine.aux_stream(2)  # the context's own stream: no extra hardware-queue pressure
+        return self._side
+
     def convert(self, wav24, wav16, singer, fast_inference=True, speedup=10, seed=0, utt_ids=None, x_T=None,
                 noise=None, f0=None, wav16_float=None):
         e = self.engine
         mel, energy = e.mel_energy(wav24)
         T = mel.shape[1]
-        if f0 is None:
-            f0 = e.f0(wav24, T)
-        e.pitch_shift(f0)
+        # F0 (Praat AC + pitch shift) is latency-bound serial work on few CUs: it runs on a side stream beside the
+        # content encoder (svc_f0_ac has its own workspace), joined before the conditioner needs it
+        main = torch.cuda.current_stream(wav24.device)
+        side = self._side_stream(wav24.device) if os.environ.get("SVC_F0_SIDE", "1") != "0" else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            if f0 is None:
+                f0 = e.f0(wav24, T)
+            e.pitch_shift(f0)
         content = self.content(wav16, T, wav16_float)
+        main.wait_stream(side)
+        f0.record_stream(main)
         cond = e.condition(content, f0, energy, singer)
         if utt_ids is None and x_T is None:
             utt_ids = torch.arange(wav24.shape[0], device=wav24.device, dtype=torch.int32)

@@ -120,6 +120,13 @@ class SVCEngine:
         except Exception:
             pass
 
+    def aux_stream(self, index=2):
+        """The context's sub-stream `index` as a torch stream (svc_ctx_stream); index 2 is idle while the Whisper
+        encoder runs its two sub-batches on 0 and 1."""
+        ptr = ctypes.c_void_p()
+        _lib.call("svc_ctx_stream", self._ctx, index, ctypes.byref(ptr))
+        return torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", self.device))
+
     def memory(self):
         wb, wsb = ctypes.c_int64(), ctypes.c_int64()
         _lib.call("svc_ctx_memory", self._ctx, ctypes.byref(wb), ctypes.byref(wsb))
