@@ -1233,9 +1233,8 @@ svc_status svc_ctx_finalize(svc_ctx* c) {
 }
 
 // One of the context's own sub-streams (created on first use, the same ones the sampler / vocoder / Whisper
-// sub-batches run on), so a host pipeline can overlap stage calls without adding a stream: an extra stream
-// changes how the context's streams map onto the 4 hardware queues (measured: 737 -> 644 audio-s/s when the
-// F0 stage got a stream of its own).
+// sub-batches run on), so a host pipeline can overlap stage calls without adding a stream (measured: 737 -> 644
+// audio-s/s when the F0 stage got a stream of its own, presumably from sharing the 4 hardware queues).
 svc_status svc_ctx_stream(svc_ctx* c, int index, void** stream) {
   SVC_REQUIRE(c && stream && index >= 0 && index < kMaxSubStreams, "ctx_stream: bad args");
   SVC_HIP_CHECK(hipSetDevice(c->device));
