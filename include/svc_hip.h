@@ -18,8 +18,9 @@
  *   - Tensors are caller-owned DEVICE buffers, time-major: row = b*T + t, channels contiguous.
  *   - Every call is asynchronous and ordered on `stream` (a hipStream_t; NULL = default stream).
  *   - One context per device; a context is not thread-safe. Calls that share the context's workspace must be
- *     ordered on one stream; svc_f0_ac and svc_pitch_shift are the exception (own workspace / none) and may run on
- *     a second stream beside the content encoders (the host pipeline overlaps F0 with Whisper that way).
+ *     ordered on one stream; svc_mel_energy, svc_f0_ac and svc_pitch_shift are the exception (their own workspace /
+ *     none) and may run, ordered among themselves, on a second stream beside the content encoders (the host
+ *     pipeline overlaps them with Whisper that way, on svc_ctx_stream(ctx, 2)).
  *   - Parameters are given in the reference's own state_dict naming with a model prefix
  *     ("mapper.", "vocoder.", "whisper.") as host float32 arrays; they are folded (weight_norm),
  *     packed into MFMA layouts and uploaded by svc_ctx_finalize. Host arrays must stay valid until
@@ -62,8 +63,8 @@ svc_status svc_mel_energy(svc_ctx* ctx, const float* wav24k, int B, int64_t n_sa
                           void* stream);
 
 /* A3-F0: Praat autocorrelation pitch (to_pitch_ac, voicing 0.6, floor f0_min, ceiling f0_max, time step hop/fs),
-   padded to T frames as utils/f0.py:156-157; unvoiced = 0. f0 [B*T] float64. Uses its own workspace: may run on
-   another stream concurrently with the other stage calls of the same context (not with another svc_f0_ac). */
+   padded to T frames as utils/f0.py:156-157; unvoiced = 0. f0 [B*T] float64. Uses the feature-stage workspace
+   (shared with svc_mel_energy only): may run on another stream beside the content-encoder calls. */
 svc_status svc_f0_ac(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, int T, double* f0, void* stream);
 
 /* A4: in place, f0 [B*T] float64 *= target_median / median(voiced f0 of that utterance)

@@ -265,7 +265,8 @@ struct svc_ctx {
   std::vector<void*> allocs;
   int64_t weight_bytes = 0;
   Arena ws;
-  Arena f0ws;  // the F0 stage's own workspace: svc_f0_ac may run on a side stream beside the content encoder
+  Arena auxws;  // workspace of the 24 kHz feature stages (mel / energy, F0): they may run on a side stream beside
+               // the content encoder, which uses ws
 
   // features
   float *fb24 = nullptr, *fb16 = nullptr, *win_mel = nullptr, *win16 = nullptr;
@@ -1173,7 +1174,7 @@ svc_status svc_ctx_destroy(svc_ctx* c) {
   (void)hipDeviceSynchronize();
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->ws.base) (void)hipFree(c->ws.base);
-  if (c->f0ws.base) (void)hipFree(c->f0ws.base);
+  if (c->auxws.base) (void)hipFree(c->auxws.base);
   for (int i = 0; i < c->n_sub_streams; ++i) {
     (void)hipStreamDestroy(c->sub_streams[i]);
     (void)hipEventDestroy(c->ev_join[i]);
@@ -1329,9 +1330,10 @@ svc_status svc_mel_energy(svc_ctx* c, const float* wav, int B, int64_t n, float*
   const int T = (int)T64, nb = c->n_fft / 2 + 1;
   size_t need = (size_t)B * T * nb * 4 + 4096;
   int st;
-  if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
-  c->ws.reset();
-  WS_GET(float, spec, (size_t)B * T * nb);
+  if ((st = c->auxws.reserve(std::max(need, c->auxws.cap)))) return st;
+  c->auxws.reset();
+  float* spec = c->auxws.get<float>((size_t)B * T * nb);
+  SVC_REQUIRE(spec, "mel_energy: workspace");
   DftArgs a{};
   a.wav = wav;
   a.wav_stride = n;
@@ -1356,8 +1358,8 @@ svc_status svc_f0_ac(svc_ctx* c, const float* wav, int B, int64_t n, int T, doub
   const double ts = (double)c->hop / c->fs;
   size_t need = f0_workspace_bytes(B, n, c->fs, ts, c->f0_min);
   int st;
-  if ((st = c->f0ws.reserve(std::max(need + 4096, c->f0ws.cap)))) return st;
-  return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->f0ws.base, c->f0ws.cap,
+  if ((st = c->auxws.reserve(std::max(need + 4096, c->auxws.cap)))) return st;
+  return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->auxws.base, c->auxws.cap,
                      (hipStream_t)stream);
 }
 

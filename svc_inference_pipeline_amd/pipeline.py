@@ -27,7 +27,7 @@ import os
 
 import torch
 
-from .runtime import SVCEngine
+from .runtime import SVCEngine, mel_frames
 
 WHISPER_WINDOW = 478720       # 16 kHz samples per long-input window (29.92 s)
 WINDOW_MEL_FRAMES = 2805      # = 1496 encoder frames * 15 / 8
@@ -101,20 +101,23 @@ class SVCPipeline:
     def convert(self, wav24, wav16, singer, fast_inference=True, speedup=10, seed=0, utt_ids=None, x_T=None,
                 noise=None, f0=None, wav16_float=None):
         e = self.engine
-        mel, energy = e.mel_energy(wav24)
-        T = mel.shape[1]
-        # F0 (Praat AC + pitch shift) is latency-bound serial work on few CUs: it runs on a side stream beside the
-        # content encoder (svc_f0_ac has its own workspace), joined before the conditioner needs it
+        T = mel_frames(wav24.shape[1], e.cfg.n_fft, e.cfg.hop_length)  # utils/mel.py:130-174 frame count
+        # The 24 kHz features (mel / energy, and F0: Praat AC + pitch shift, latency-bound serial work on few CUs)
+        # run on the context's sub-stream 2 beside the content encoder (they use their own workspace), joined before
+        # the conditioner needs them
         main = torch.cuda.current_stream(wav24.device)
         side = self._side_stream(wav24.device) if os.environ.get("SVC_F0_SIDE", "1") != "0" else main
         side.wait_stream(main)
         with torch.cuda.stream(side):
+            mel, energy = e.mel_energy(wav24)
             if f0 is None:
                 f0 = e.f0(wav24, T)
             e.pitch_shift(f0)
+        assert mel.shape[1] == T
         content = self.content(wav16, T, wav16_float)
         main.wait_stream(side)
-        f0.record_stream(main)
+        for t in (mel, energy, f0):
+            t.record_stream(main)
         cond = e.condition(content, f0, energy, singer)
         if utt_ids is None and x_T is None:
             utt_ids = torch.arange(wav24.shape[0], device=wav24.device, dtype=torch.int32)
