@@ -1683,11 +1683,12 @@ struct DenoiseBufs {
   f16* cpF;      // fused path: [NL][rows_pad][2C] fragment-major cp + dilated bias (diff_layer.hip)
   int rows_pad;  // rows of this (sub-)batch rounded up to 64
   f16* y16b;     // [rows][C] ping-pong partner of y16 (the fused layer reads one and writes the other)
-  float* h32;    // [rows][C] residual stream
+  float* h32;    // [rows][C] residual stream (f32: the fused path and SVC_DIFF_RES32=1)
   f16* y16;      // [rows][C] next layer input x + diffusion_projection
   f16* g16;      // [rows][NL*C] gate outputs of every layer (A operand of the skip GEMM)
   f16* s16;      // [rows][C] sum(skip) / sqrt(NL)
   f16* u16;      // [rows][C] relu(skip_projection)
+  f16* lo16;     // [rows][C] low half of the split residual stream: x + dproj = y16 + lo16 (default path)
   size_t cp_ls;  // elements between layers of cp16, which is LAYER-major [NL][rows_total][2C]: each layer's gate
                  // epilogue reads one contiguous block (row-major over all layers put 30 KB between its rows)
   size_t g_ls;   // elements between layers of g16, also layer-major [NL][rows_total][C]: the gate GEMM writes and the
@@ -1709,10 +1710,19 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   const int ldx16 = (int)round_up(c->n_mel, 8);
   const float* dp = c->dproj + (size_t)t * NL * C;
   int st;
+  // Residual stream x: by default split-fp16 storage (x + dproj_l = y16 + lo16, ~22 significand bits in 4 bytes):
+  // the layer's GEMM operand y16 is its high half, so each residual update moves 10 instead of 12 bytes per element.
+  // SVC_DIFF_RES32=1 (and the fused path) keep x in f32 (h32).
+  const char* r32env = getenv("SVC_DIFF_RES32");
+  const bool res32 = fused_layers(c) || (r32env && atoi(r32env) == 1);
   EpiArgs e = epi();
   e.act = ACT_RELU;
-  e.out32 = bb.h32;
-  e.ld32 = C;
+  if (res32) {
+    e.out32 = bb.h32;
+    e.ld32 = C;
+  } else {
+    e.lo16 = bb.lo16;
+  }
   e.out16 = bb.y16;
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
@@ -1752,11 +1762,18 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
     // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step)
     EpiArgs r = epi();
-    r.acc32 = bb.h32;
     r.ld_acc = C;
     r.acc_div = 1.41421356237309515f;
-    r.out32 = bb.h32;
-    r.ld32 = C;
+    if (res32) {
+      r.acc32 = bb.h32;
+      r.out32 = bb.h32;
+      r.ld32 = C;
+    } else {  // x_i = (y16 + lo16) - dproj_i, and x_{i+1} + dproj_{i+1} goes back split into y16 / lo16
+      r.acc16_hi = bb.y16;
+      r.acc16_lo = bb.lo16;
+      r.acc_sub = dp + (size_t)i * C;
+      r.lo16 = bb.lo16;
+    }
     r.out16 = bb.y16;
     r.ld16 = C;
     r.add16 = dp + (size_t)(i + 1) * C;
@@ -1801,14 +1818,16 @@ static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   WS_GET(f16, g16, rows * c->n_layers * C);
   WS_GET(f16, s16, rows * C);
   WS_GET(f16, u16, rows * C);
-  bb = DenoiseBufs{cp16, cpF, (int)round_up((int64_t)rows, 64), y16b, h32, y16, g16, s16, u16, rows * 2 * C, rows * C};
+  WS_GET(f16, lo16, rows * C);
+  bb = DenoiseBufs{cp16, cpF, (int)round_up((int64_t)rows, 64), y16b, h32, y16, g16, s16, u16, lo16, rows * 2 * C,
+                   rows * C};
   return SVC_OK;
 }
 
 static size_t denoise_bytes(svc_ctx* c, int B, int T) {
   const size_t rows = (size_t)B * T, C = c->C;
   return rows * c->n_layers * 2 * C * 2 + (fused_layers(c) ? rows + 64 * kMaxSubStreams : 0) * c->n_layers * 2 * C * 2 +
-         rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 4) + 20 * 4096;
+         rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 5) + 22 * 4096;
 }
 
 // fused path: the hoisted conditioner projection of one (sub-)batch -> fragment-major records with the dilated
@@ -1930,7 +1949,7 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
     const int rp = (int)round_up((int64_t)u.B * T, 64);
     return DenoiseBufs{bb.cp16 + r * 2 * C, bb.cpF + fm_off[h] * NL * 2 * C, rp, bb.y16b + r * C,
                        bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * C, bb.u16 + r * C,
-                       bb.cp_ls, bb.g_ls};
+                       bb.lo16 + r * C, bb.cp_ls, bb.g_ls};
   };
   for (int h = 0; h < S; ++h)
     if ((st = fragment_cp(c, sub_bufs(sub[h]), sub[h].B * T, s))) return st;

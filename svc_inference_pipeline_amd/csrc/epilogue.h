@@ -49,8 +49,18 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
           const float4 ar = *reinterpret_cast<const float4*>(e.add_row + orow * e.ld_add_row + n);
           v.x += ar.x; v.y += ar.y; v.z += ar.z; v.w += ar.w;
         }
-        if (e.acc32) {
-          const float4 ac = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
+        if (e.acc32 || e.acc16_hi) {
+          float4 ac;
+          if (e.acc32) {
+            ac = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
+          } else {  // split residual: (hi + lo) - the add16 it was stored with
+            union { uint2 u; f16 h[4]; } hi, lo;
+            hi.u = *reinterpret_cast<const uint2*>(e.acc16_hi + orow * e.ld_acc + n);
+            lo.u = *reinterpret_cast<const uint2*>(e.acc16_lo + orow * e.ld_acc + n);
+            const float4 sb = *reinterpret_cast<const float4*>(e.acc_sub + n);
+            ac.x = ((float)hi.h[0] + (float)lo.h[0]) - sb.x; ac.y = ((float)hi.h[1] + (float)lo.h[1]) - sb.y;
+            ac.z = ((float)hi.h[2] + (float)lo.h[2]) - sb.z; ac.w = ((float)hi.h[3] + (float)lo.h[3]) - sb.w;
+          }
           v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
           if (e.acc_div != 1.0f) {
             v.x = v.x / e.acc_div; v.y = v.y / e.acc_div; v.z = v.z / e.acc_div; v.w = v.w / e.acc_div;
@@ -67,6 +77,12 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
         union { uint2 u; f16 h[4]; } pk;
         pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
         *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
+        if (e.lo16) {
+          union { uint2 u; f16 h[4]; } lo;
+          lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);
+          lo.h[2] = (f16)(w.z - (float)pk.h[2]); lo.h[3] = (f16)(w.w - (float)pk.h[3]);
+          *reinterpret_cast<uint2*>(e.lo16 + orow * e.ld16 + n) = lo.u;
+        }
         if (e.split16) {
           union { uint2 u; f16 h[4]; } lo;
           lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);

@@ -188,8 +188,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
         if (n < e.scale_cols) v *= e.col_scale;
         if (e.add_t) v += e.add_t[(int64_t)t * e.ld_add_t + n];
         if (e.add_row) v += e.add_row[orow * e.ld_add_row + n];
-        if (e.acc32) {
-          v = e.acc32[orow * e.ld_acc + n] + v;
+        if (e.acc32 || e.acc16_hi) {
+          const float ac = e.acc32 ? e.acc32[orow * e.ld_acc + n]
+                                   : ((float)e.acc16_hi[orow * e.ld_acc + n] + (float)e.acc16_lo[orow * e.ld_acc + n]) -
+                                         e.acc_sub[n];
+          v = ac + v;
           if (e.acc_div != 1.0f) v = v / e.acc_div;
         }
         if (e.out32) e.out32[orow * e.ld32 + n] = v;
@@ -197,6 +200,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
           const float w = e.add16 ? v + e.add16[n] : v;
           const f16 hi = f16_sat(w);
           e.out16[orow * e.ld16 + n] = hi;
+          if (e.lo16) e.lo16[orow * e.ld16 + n] = (f16)(w - (float)hi);
           if (e.split16) {
             e.out16[orow * e.ld16 + e.split16 + n] = (f16)(w - (float)hi);
             e.out16[orow * e.ld16 + 2 * e.split16 + n] = hi;
