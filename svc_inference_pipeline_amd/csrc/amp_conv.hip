@@ -10,8 +10,9 @@
 //      f16 into an LDS image. Rows outside [0, L) are zeros: the conv's own zero padding.
 //   2. conv: v_mfma_f32_16x16x32_f16 with A fragments read from the LDS image at row r + tap*d (row stride
 //      padded so 16-row fragment reads are conflict-free) and B = the packed weights [Npad][Kpad] (L1/L2).
-//   3. epilogue: C staged through LDS, then streamed as float4 over the contiguous block: bias, residual add
-//      (add_row), resblock mean accumulation (acc32 / acc_div), f32 and/or f16 stores.
+//   3. epilogue in registers (the MFMAs run with A and B swapped, so a lane holds 4 consecutive channels of a row):
+//      bias, residual add (add_row), resblock mean accumulation (acc32 / acc_div), f32 and/or f16 stores as 16-B /
+//      8-B vectors. No C staging, so LDS holds only the activation image and more workgroups share a CU.
 // The activation never round-trips through HBM, and every HBM access is a coalesced 16-byte stream.
 #include "common.h"
 #include "snake.h"
@@ -27,8 +28,9 @@ struct AmpCfg {
   static constexpr int ROWS = BT + 2 * MAXP;
   static constexpr int FN = (C + 15) / 16;          // 16-column fragments
   static constexpr int A_BYTES = ROWS * LDA * 2;
-  static constexpr int C_BYTES = BT * C * 4;
-  static constexpr int LDS = A_BYTES > C_BYTES ? A_BYTES : C_BYTES;
+  // the epilogue works in registers (operand-swapped MFMAs, see below), so LDS holds only the activation image:
+  // C = 48: 34 KiB -> 4 workgroups per CU (3 with the former 48 KiB C staging), C = 24: 15 KiB
+  static constexpr int LDS = A_BYTES;
   // activation tasks: VEC channels x RUN rows per thread (VEC 2 / RUN 32 for C = 48 measured 18 % slower: 137 VGPRs)
   static constexpr int VEC = 1;
   static constexpr int RUN = C == 24 ? 32 : 16;  // C = 24: 24 x 10 runs = 240 tasks (611 -> 562-585 us / launch)
@@ -204,57 +206,36 @@ __global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs
 #pragma unroll
     for (int i = 0; i < MW; ++i)
 #pragma unroll
-      for (int j = 0; j < CF::FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < CF::FN; ++j)  // C^T fragment: acc[i][j][r] = C[row fr of block i][channel j*16 + fk*4 + r]
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
   }
-  __syncthreads();  // the activation image is dead: reuse LDS for the C tile
-
-  // ------------------------------------------------------------------ 3. epilogue over the [BT][C] block
-  float* Cs = reinterpret_cast<float*>(amp_sm);
-#pragma unroll
-  for (int i = 0; i < MW; ++i)
-#pragma unroll
-    for (int j = 0; j < CF::FN; ++j) {
-      const int col = j * 16 + fr;
-      if (col < C)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) Cs[((wave * MW + i) * 16 + fk * 4 + r) * C + col] = acc[i][j][r];
-    }
-  __syncthreads();
+  // ------------------------------------------------------------------ 3. epilogue in registers: each lane owns 4
+  // consecutive channels of one row, so bias / residual / accumulator / outputs move as 16-byte vectors
   const int nvalid = min(CF::BT, L - t0);
   const int64_t base = ((int64_t)b * L + t0) * C;
-  const int n4 = nvalid * C / 4;
-  constexpr int U = 4;  // loads of a group are issued before its stores (out32 may alias add_row / acc32)
-  for (int g0 = 0; g0 < n4; g0 += AMP_NT * U) {
-    float4 v[U], ar[U], ac[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i4 = g0 + u * AMP_NT + tid;
-      v[u] = ar[u] = ac[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (i4 >= n4) continue;
-      const int64_t g = base + (int64_t)i4 * 4;
-      v[u] = reinterpret_cast<const float4*>(Cs)[i4];
-      if (e.add_row) ar[u] = *reinterpret_cast<const float4*>(e.add_row + g);
-      if (e.acc32) ac[u] = *reinterpret_cast<const float4*>(e.acc32 + g);
-    }
+  for (int j = 0; j < CF::FN; ++j) {
+    const int c0 = j * 16 + fk * 4;
+    if (c0 >= C) continue;
+    const float4 bi = *reinterpret_cast<const float4*>(p.bias + c0);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int i4 = g0 + u * AMP_NT + tid;
-      if (i4 >= n4) continue;
-      const int col = (i4 * 4) % C;
-      const int64_t g = base + (int64_t)i4 * 4;
-      float4 w = v[u];
-      const float4 bi = *reinterpret_cast<const float4*>(p.bias + col);
-      w.x += bi.x; w.y += bi.y; w.z += bi.z; w.w += bi.w;
+    for (int i = 0; i < MW; ++i) {
+      const int row = (wave * MW + i) * 16 + fr;
+      if (row >= nvalid) continue;
+      const int64_t g = base + (int64_t)row * C + c0;
+      float4 w = make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w);
       if (e.add_row) {
-        w.x += ar[u].x; w.y += ar[u].y; w.z += ar[u].z; w.w += ar[u].w;
+        const float4 ar = *reinterpret_cast<const float4*>(e.add_row + g);
+        w.x += ar.x; w.y += ar.y; w.z += ar.z; w.w += ar.w;
       }
       if (e.acc32) {
-        w.x = ac[u].x + w.x; w.y = ac[u].y + w.y; w.z = ac[u].z + w.z; w.w = ac[u].w + w.w;
+        const float4 ac = *reinterpret_cast<const float4*>(e.acc32 + g);
+        w.x = ac.x + w.x; w.y = ac.y + w.y; w.z = ac.z + w.z; w.w = ac.w + w.w;
         if (e.acc_div != 1.0f) {
           w.x = w.x / e.acc_div; w.y = w.y / e.acc_div; w.z = w.z / e.acc_div; w.w = w.w / e.acc_div;
         }
       }
-      if (e.out32) *reinterpret_cast<float4*>(e.out32 + g) = w;
+      if (e.out32) *reinterpret_cast<float4*>(e.out32 + g) = w;  // may alias add_row / acc32: same lane, same element
       if (e.out16) {
         union { uint2 u2; f16 h[4]; } pk;
         pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
