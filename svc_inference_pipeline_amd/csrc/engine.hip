@@ -2409,11 +2409,12 @@ __global__ void fill_f16_kernel(f16* p, int64_t n, uint32_t seed) {
 
 extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_kind, int variant, int iters, double* ms_out) {
   SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters >= 1, "gemm_bench: bad args");
-  SVC_REQUIRE(epi_kind < 3 || variant == 24, "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
+  SVC_REQUIRE(epi_kind < 3 || epi_kind == 6 || variant == 24,
+              "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float *bias, *R = nullptr;
-  if (epi_kind == 2) {  // DiffSVC residual epilogue: x32 read-modify-write + next f16 input
+  if (epi_kind == 2 || epi_kind == 6) {  // DiffSVC residual epilogue: x32 (6: split-fp16 lo half) read-modify-write
     SVC_HIP_CHECK(hipMalloc(&R, (size_t)M * N * 4));
     SVC_HIP_CHECK(hipMemset(R, 0, (size_t)M * N * 4));
   }
@@ -2439,6 +2440,9 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
     e.out16 = Y; e.ld16 = N;
     if (epi_kind == 2) {
       e.acc32 = R; e.ld_acc = N; e.acc_div = 1.41421356237309515f; e.out32 = R; e.ld32 = N; e.add16 = bias;
+    } else if (epi_kind == 6) {  // split residual in place, as diffsvc.outproj: (Y + lo) - sub -> Y / lo
+      e.acc16_hi = Y; e.acc16_lo = reinterpret_cast<f16*>(R); e.acc_sub = bias; e.lo16 = reinterpret_cast<f16*>(R);
+      e.ld_acc = N; e.acc_div = 1.41421356237309515f; e.add16 = bias;
     }
   }
   hipEvent_t e0, e1;

@@ -153,7 +153,14 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int n = min(nw + j * 16 + fk * 4, a.N - 4);  // clamped columns are loaded but never stored
-        res[i][j] = *reinterpret_cast<const float4*>(e.acc32 + (int64_t)m * e.ld_acc + n);
+        if (e.acc16_hi) {  // split residual: the raw hi / lo halves, combined in the epilogue
+          const uint2 h = *reinterpret_cast<const uint2*>(e.acc16_hi + (int64_t)m * e.ld_acc + n);
+          const uint2 l = *reinterpret_cast<const uint2*>(e.acc16_lo + (int64_t)m * e.ld_acc + n);
+          res[i][j] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x),
+                                  __uint_as_float(l.y));
+        } else {
+          res[i][j] = *reinterpret_cast<const float4*>(e.acc32 + (int64_t)m * e.ld_acc + n);
+        }
       }
       return;
     }
@@ -225,20 +232,36 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
       if (n >= a.N) continue;
       const float4 bi = *reinterpret_cast<const float4*>(e.bias + n);
       const float4 ad = *reinterpret_cast<const float4*>(e.add16 + n);
+      const bool split = e.acc16_hi != nullptr;
+      const float4 sb = split ? *reinterpret_cast<const float4*>(e.acc_sub + n) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + fr;
         if (m >= M) continue;
         float4 v = make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w);
-        v.x = (res[i][j].x + v.x) / e.acc_div;  // the order and IEEE division of epilogue_pass
-        v.y = (res[i][j].y + v.y) / e.acc_div;
-        v.z = (res[i][j].z + v.z) / e.acc_div;
-        v.w = (res[i][j].w + v.w) / e.acc_div;
-        *reinterpret_cast<float4*>(e.out32 + (int64_t)m * e.ld32 + n) = v;
-        union { uint2 u; f16 h[4]; } pk;
-        pk.h[0] = f16_sat(v.x + ad.x); pk.h[1] = f16_sat(v.y + ad.y);
-        pk.h[2] = f16_sat(v.z + ad.z); pk.h[3] = f16_sat(v.w + ad.w);
+        float4 ac = res[i][j];
+        if (split) {  // (hi + lo) - the add16 it was stored with, as epilogue_pass
+          H4 hi, lo;
+          hi.u = make_uint2(__float_as_uint(ac.x), __float_as_uint(ac.y));
+          lo.u = make_uint2(__float_as_uint(ac.z), __float_as_uint(ac.w));
+          ac.x = ((float)hi.h[0] + (float)lo.h[0]) - sb.x; ac.y = ((float)hi.h[1] + (float)lo.h[1]) - sb.y;
+          ac.z = ((float)hi.h[2] + (float)lo.h[2]) - sb.z; ac.w = ((float)hi.h[3] + (float)lo.h[3]) - sb.w;
+        }
+        v.x = (ac.x + v.x) / e.acc_div;  // the order and IEEE division of epilogue_pass
+        v.y = (ac.y + v.y) / e.acc_div;
+        v.z = (ac.z + v.z) / e.acc_div;
+        v.w = (ac.w + v.w) / e.acc_div;
+        if (!split) *reinterpret_cast<float4*>(e.out32 + (int64_t)m * e.ld32 + n) = v;
+        const float4 w = make_float4(v.x + ad.x, v.y + ad.y, v.z + ad.z, v.w + ad.w);
+        H4 pk;
+        pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
         *reinterpret_cast<uint2*>(e.out16 + (int64_t)m * e.ld16 + n) = pk.u;
+        if (split) {
+          H4 lo;
+          lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);
+          lo.h[2] = (f16)(w.z - (float)pk.h[2]); lo.h[3] = (f16)(w.w - (float)pk.h[3]);
+          *reinterpret_cast<uint2*>(e.lo16 + (int64_t)m * e.ld16 + n) = lo.u;
+        }
       }
     }
     return;
@@ -302,9 +325,12 @@ __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiA
 
 // the direct residual epilogue covers exactly the DiffSVC output projection's form
 bool conv_gemm4_rmw_form(const ConvGemmArgs& a, const EpiArgs& e) {
-  return e.kind == EPI_GENERIC && e.act == ACT_NONE && e.acc32 && e.out32 && e.out16 && e.add16 && !e.add_t &&
+  // f32 residual (acc32 -> out32) or the split-fp16 one (acc16_hi / acc16_lo - acc_sub -> out16 / lo16)
+  const bool f32 = e.acc32 && e.out32 && !e.acc16_hi && !e.lo16 && e.ld32 % 4 == 0;
+  const bool split = !e.acc32 && !e.out32 && e.acc16_hi && e.acc16_lo && e.acc_sub && e.lo16;
+  return e.kind == EPI_GENERIC && e.act == ACT_NONE && (f32 || split) && e.out16 && e.add16 && !e.add_t &&
          !e.add_row && e.scale_cols == 0 && e.split16 == 0 && e.T_ostore == a.T_out && e.ostride == 1 &&
-         e.ophase == 0 && a.N % 4 == 0 && e.ld_acc % 4 == 0 && e.ld32 % 4 == 0 && e.ld16 % 4 == 0;
+         e.ophase == 0 && a.N % 4 == 0 && e.ld_acc % 4 == 0 && e.ld16 % 4 == 0;
 }
 
 // direct: the register epilogue (DIRECT: gate, or the residual read-modify-write) where the epilogue has that form,

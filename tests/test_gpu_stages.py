@@ -115,15 +115,20 @@ def test_fused_layer_vs_oracle(engine, states, cfg, fused, B, T, monkeypatch):
         assert rel_l2(eps, other) < 2e-3
 
 
-@pytest.mark.parametrize("variant", ["20", "24", "21"])
+@pytest.mark.parametrize("variant", ["20", "24", "21", "rmw", "rmw32"])
 @pytest.mark.parametrize("B,T", [(3, 50), (2, 700), (5, 937)])
 def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, monkeypatch):
-    """The DiffSVC gate GEMM kernels (LDS-staged and in-register gate epilogues, deep-ring variant) on ragged row
-    counts (B*T not a multiple of the 128-row tile, utterance boundaries inside tiles) against the oracle's eps."""
+    """The DiffSVC gate GEMM kernels (LDS-staged and in-register gate epilogues, deep-ring variant) and the register
+    residual epilogue of the output projection (rmw: split-fp16 residual, rmw32: f32 residual) on ragged row counts
+    (B*T not a multiple of the 128-row tile, utterance boundaries inside tiles) against the oracle's eps."""
     rng = np.random.default_rng(B * 7 + T)
     cond = rng.standard_normal((B, T, 384)).astype(np.float32)
     x = rng.standard_normal((B, T, 100)).astype(np.float32)
     table = W.step_embedding_table(1000)
+    if variant.startswith("rmw"):
+        monkeypatch.setenv("SVC_GEMM4_RMW", "1")
+        monkeypatch.setenv("SVC_DIFF_RES32", "1" if variant == "rmw32" else "0")
+        variant = "15"
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
     monkeypatch.setenv("SVC_DIFF_FUSED", "0")
     eps = engine.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()

@@ -13,6 +13,8 @@ SHAPES = [  # name, M, N, Cin, taps, epi
     ("diffsvc.outproj(res)", 29984, 384, 384, 1, 0),
     ("diffsvc.outproj(rmw)", 29984, 384, 384, 1, 2),   # with the real epilogue: f32 residual RMW + next f16 input
     ("diffsvc.outproj(rmw,sub)", 9995, 384, 384, 1, 2),
+    ("diffsvc.outproj(split)", 29984, 384, 384, 1, 6),  # the default split-fp16 residual RMW (hi / lo halves)
+    ("diffsvc.outproj(split,sub)", 9995, 384, 384, 1, 6),
     ("diffsvc.skipsum", 29984, 384, 7680, 1, 0),
     ("bigvgan.s2 k11", 32 * 14992, 384, 384, 11, 0),
     ("whisper.fc1", 48000, 4096, 1024, 1, 0),
