@@ -131,6 +131,8 @@ struct EpiArgs {
   // as acc = (hi + lo) - acc_sub (the add16 it was stored with), in place of acc32; lo16: also write the lo half
   const f16* acc16_hi; const f16* acc16_lo; const float* acc_sub;
   f16* lo16;
+  // host-side launch hint: keep conv_gemm3's LDS-staged epilogue for this call (set by run_gemm, see gemm3.hip)
+  int no_reg_epi;
 };
 
 int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);

@@ -542,6 +542,11 @@ static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cv
 int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
              hipStream_t s, const char* site = "") {
   prof_site(site);
+  // conv_gemm3's register epilogues (SVC_GEMM3_DIRECT mask, gemm3.hip) stay off inside the DiffSVC sampler unless
+  // bit 8 is set: there its sub-batch GEMMs run beside the gate GEMMs of the other streams, which then ran slower
+  const char* denv = getenv("SVC_GEMM3_DIRECT");
+  const int dmask = denv ? atoi(denv) : 3;
+  if (!(dmask & 8) && site && strncmp(site, "diffsvc.", 8) == 0) e.no_reg_epi = 1;
   const ConvGemmArgs a = gemm_args(g, X, ldx, Cvalid, B, T_in, T_out, e);
   const bool pair = e.kind == EPI_GATE;
   // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..14 = conv_gemm3 tile,

@@ -78,10 +78,19 @@ __device__ __forceinline__ void g3_dma(const void* src, unsigned char* lds) {
 // every W rows: rows w*W + h*Q + [0, Q)
 __device__ __forceinline__ int half_row(int i, int h, int Q, int W) { return (i / Q) * W + h * Q + (i % Q); }
 
-template <int BM, int BN, bool CP64, bool PAIR, bool HALO>
+// Register epilogue forms (FORM > 0, !PAIR, !HALO): the MFMAs run with A and B swapped, so a lane's accumulator holds
+// 4 consecutive columns of one output row and the epilogue reads and writes HBM straight from registers (no C tile
+// through LDS, no extra barriers). Each form is the epilogue_pass arithmetic, in the same order, for one family:
+//   G3_F16  : act(acc + bias) (* col_scale for n < scale_cols) -> out16 (+ split16 lo / hi copies)
+//   G3_RES32: acc + bias (+ add_row) ((acc32 + v) / acc_div) -> out32 and / or out16 (+ add16)
+//   G3_SPLIT: acc + bias, ((acc16_hi + acc16_lo) - acc_sub + v) / acc_div -> out16 = hi(v + add16), lo16 = lo
+enum { G3_LDS = 0, G3_F16 = 1, G3_RES32 = 2, G3_SPLIT = 3 };
+
+template <int BM, int BN, bool CP64, bool PAIR, bool HALO, int FORM = G3_LDS>
 __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage,
                                                            float inv_cp) {
   static_assert(!HALO || CP64, "tap reuse needs whole-tap K-tiles");
+  static_assert(FORM == G3_LDS || (!PAIR && !HALO), "register epilogues: generic, per-tap schedule only");
   using CF = G3<BM, BN, HALO>;
   extern __shared__ __align__(16) unsigned char sm3[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -308,7 +317,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
       for (int i = 0; i < CF::FQM; ++i)
 #pragma unroll
         for (int j = 0; j < CF::FQN; ++j)
-          acc[QMI][QNI][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][s], bf[j][s], acc[QMI][QNI][i][j], 0, 0, 0);
+          if constexpr (FORM != G3_LDS)  // C^T fragment: acc[..][i][j][r] = C[row fr of block i][col fk*4 + r of j]
+            acc[QMI][QNI][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][s], af[i][s], acc[QMI][QNI][i][j], 0, 0, 0);
+          else
+            acc[QMI][QNI][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][s], bf[j][s], acc[QMI][QNI][i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     g3_barrier();
   };
@@ -347,7 +359,108 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
     kj = nj;
   }
   if (wm == 0) g3_barrier();
-  vm_wait<0>();  // trailing dummy DMAs land before the ring is reused for C staging
+  vm_wait<0>();  // trailing dummy DMAs land before the ring is reused for C staging (or the workgroup ends)
+  if constexpr (FORM != G3_LDS) {
+    union H4 { uint2 u; f16 h[4]; };
+    // column groups (y, j): packed columns nq .. nq + 3; their bias (and per-column vectors) loaded once
+    float4 cb[2][CF::FQN], cs[2][CF::FQN], ca[2][CF::FQN];
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int j = 0; j < CF::FQN; ++j) {
+        const int n = min(n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4, a.N - 4);
+        cb[y][j] = *reinterpret_cast<const float4*>(e.bias + n);
+        if constexpr (FORM == G3_SPLIT) cs[y][j] = *reinterpret_cast<const float4*>(e.acc_sub + n);
+        if constexpr (FORM != G3_F16) {
+          if (e.add16) ca[y][j] = *reinterpret_cast<const float4*>(e.add16 + n);
+        }
+      }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int i = 0; i < CF::FQM; ++i) {
+        const int m = m0 + wm * CF::WTM + x * CF::QM + i * 16 + fr;
+        if (m >= M) continue;
+        const int b = m / a.T_out, t = m - b * a.T_out;
+        const int64_t orow = (int64_t)b * e.T_ostore + (int64_t)t * e.ostride + e.ophase;
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int j = 0; j < CF::FQN; ++j) {
+            const int n = n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4;
+            if (n >= a.N) continue;
+            const floatx4& c = acc[x][y][i][j];
+            float4 v = make_float4(c[0] + cb[y][j].x, c[1] + cb[y][j].y, c[2] + cb[y][j].z, c[3] + cb[y][j].w);
+            if constexpr (FORM == G3_F16) {
+              if (e.act == ACT_GELU) {
+                v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+              } else if (e.act == ACT_RELU) {
+                v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+              }
+              if (n < e.scale_cols) {
+                v.x *= e.col_scale; v.y *= e.col_scale; v.z *= e.col_scale; v.w *= e.col_scale;
+              }
+              H4 pk;
+              pk.h[0] = f16_sat(v.x); pk.h[1] = f16_sat(v.y); pk.h[2] = f16_sat(v.z); pk.h[3] = f16_sat(v.w);
+              f16* o = e.out16 + orow * e.ld16 + n;
+              *reinterpret_cast<uint2*>(o) = pk.u;
+              if (e.split16) {
+                H4 lo;
+                lo.h[0] = (f16)(v.x - (float)pk.h[0]); lo.h[1] = (f16)(v.y - (float)pk.h[1]);
+                lo.h[2] = (f16)(v.z - (float)pk.h[2]); lo.h[3] = (f16)(v.w - (float)pk.h[3]);
+                *reinterpret_cast<uint2*>(o + e.split16) = lo.u;
+                *reinterpret_cast<uint2*>(o + 2 * e.split16) = pk.u;
+              }
+            } else {
+              if constexpr (FORM == G3_RES32) {
+                if (e.add_row) {
+                  const float4 ar = *reinterpret_cast<const float4*>(e.add_row + orow * e.ld_add_row + n);
+                  v.x += ar.x; v.y += ar.y; v.z += ar.z; v.w += ar.w;
+                }
+              }
+              float4 ac;
+              bool has_acc = true;
+              if constexpr (FORM == G3_SPLIT) {
+                H4 hi, lo;
+                hi.u = *reinterpret_cast<const uint2*>(e.acc16_hi + orow * e.ld_acc + n);
+                lo.u = *reinterpret_cast<const uint2*>(e.acc16_lo + orow * e.ld_acc + n);
+                ac.x = ((float)hi.h[0] + (float)lo.h[0]) - cs[y][j].x;
+                ac.y = ((float)hi.h[1] + (float)lo.h[1]) - cs[y][j].y;
+                ac.z = ((float)hi.h[2] + (float)lo.h[2]) - cs[y][j].z;
+                ac.w = ((float)hi.h[3] + (float)lo.h[3]) - cs[y][j].w;
+              } else {
+                has_acc = e.acc32 != nullptr;
+                if (has_acc) ac = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
+              }
+              if (has_acc) {
+                v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
+                if (e.acc_div != 1.0f) {
+                  v.x = v.x / e.acc_div; v.y = v.y / e.acc_div; v.z = v.z / e.acc_div; v.w = v.w / e.acc_div;
+                }
+              }
+              if constexpr (FORM == G3_RES32) {
+                if (e.out32) *reinterpret_cast<float4*>(e.out32 + orow * e.ld32 + n) = v;  // may alias add_row / acc32
+              }
+              if (e.out16) {
+                float4 w = v;
+                if (e.add16) {
+                  w.x += ca[y][j].x; w.y += ca[y][j].y; w.z += ca[y][j].z; w.w += ca[y][j].w;
+                }
+                H4 pk;
+                pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
+                *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
+                if constexpr (FORM == G3_SPLIT) {
+                  H4 lo;
+                  lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);
+                  lo.h[2] = (f16)(w.z - (float)pk.h[2]); lo.h[3] = (f16)(w.w - (float)pk.h[3]);
+                  *reinterpret_cast<uint2*>(e.lo16 + orow * e.ld16 + n) = lo.u;
+                }
+              }
+            }
+          }
+      }
+    return;
+  }
   __syncthreads();
 
   // ---- epilogue: stage C through LDS in EP column passes, then the shared vector epilogue
@@ -389,6 +502,23 @@ static int halo_of(const ConvGemmArgs& a) {
   return h >= 1 && h <= 32 ? h : 0;
 }
 
+// Register epilogue form of a generic epilogue (G3_LDS when it has none). SVC_GEMM3_DIRECT is a mask of the forms in
+// use: 1 = G3_F16, 2 = G3_RES32, 4 = G3_SPLIT, 8 = also inside the DiffSVC sampler (run_gemm sets no_reg_epi there
+// otherwise); default 3, 0 = the LDS epilogue everywhere. Alone every form is as fast or faster (Whisper fc1 12 %,
+// the DiffSVC 3-tap store 12 %, skip sum 3 %); inside the 3-stream sampler the gate GEMMs beside them ran slower.
+static int direct_form3(const ConvGemmArgs& a, const EpiArgs& e) {
+  const char* v = getenv("SVC_GEMM3_DIRECT");  // read per call (A/B runs and tests switch it)
+  const int mask = v ? atoi(v) : 3;
+  if (e.no_reg_epi || e.kind != EPI_GENERIC || e.add_t) return G3_LDS;
+  const bool acc16 = e.acc16_hi || e.acc16_lo || e.acc_sub || e.lo16;
+  if (e.out16 && !e.out32 && !e.add_row && !e.acc32 && !acc16 && !e.add16) return (mask & 1) ? G3_F16 : G3_LDS;
+  if (e.act != ACT_NONE || e.scale_cols > 0 || e.split16) return G3_LDS;
+  if (!acc16 && (e.out32 || e.out16)) return (mask & 2) ? G3_RES32 : G3_LDS;
+  if (e.acc16_hi && e.acc16_lo && e.acc_sub && e.lo16 && e.out16 && !e.out32 && !e.add_row && !e.acc32)
+    return (mask & 4) ? G3_SPLIT : G3_LDS;
+  return G3_LDS;
+}
+
 template <int BM, int BN, bool PAIR>
 static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipStream_t s, const char* tag) {
   ConvGemmArgs a = a0;
@@ -419,27 +549,35 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
   }
   using CF = G3<BM, BN>;
   const int M = a.B * a.T_out;
+  const int form = PAIR ? G3_LDS : direct_form3(a, e);
   a.ntiles_n = cdiv(a.N, BN);
   const int64_t grid = (int64_t)cdiv(M, BM) * a.ntiles_n;
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm3: bad grid");
   SVC_REQUIRE((int64_t)a.ntiles_n * BN <= std::max(round_up(a.N, 256), round_up(a.N, 384)),
               "conv_gemm3: weights not padded for BN=%d", BN);
   const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
-  static bool attr[2] = {false, false};
-  if (!attr[cp64]) {
-    const void* fn = cp64 ? (const void*)conv_gemm3_kernel<BM, BN, true, PAIR, false>
-                          : (const void*)conv_gemm3_kernel<BM, BN, false, PAIR, false>;
-    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS));
-    attr[cp64] = true;
+  const void* fns[2][4] = {
+      {(const void*)conv_gemm3_kernel<BM, BN, false, PAIR, false, G3_LDS>,
+       (const void*)conv_gemm3_kernel<BM, BN, false, false, false, G3_F16>,
+       (const void*)conv_gemm3_kernel<BM, BN, false, false, false, G3_RES32>,
+       (const void*)conv_gemm3_kernel<BM, BN, false, false, false, G3_SPLIT>},
+      {(const void*)conv_gemm3_kernel<BM, BN, true, PAIR, false, G3_LDS>,
+       (const void*)conv_gemm3_kernel<BM, BN, true, false, false, G3_F16>,
+       (const void*)conv_gemm3_kernel<BM, BN, true, false, false, G3_RES32>,
+       (const void*)conv_gemm3_kernel<BM, BN, true, false, false, G3_SPLIT>}};
+  const void* fn = fns[cp64][form];
+  // the register forms need only the operand ring (no C staging)
+  const int lds = form == G3_LDS ? CF::LDS : CF::RING;
+  static bool attr[2][4] = {};
+  if (!attr[cp64][form]) {
+    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr[cp64][form] = true;
   }
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
   const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);
-  if (cp64)
-    hipLaunchKernelGGL((conv_gemm3_kernel<BM, BN, true, PAIR, false>), dim3((unsigned)grid), dim3(CF::NT), CF::LDS, s,
-                       a, e, zpage, 1.0f / (float)a.Cp);
-  else
-    hipLaunchKernelGGL((conv_gemm3_kernel<BM, BN, false, PAIR, false>), dim3((unsigned)grid), dim3(CF::NT), CF::LDS, s,
-                       a, e, zpage, 1.0f / (float)a.Cp);
+  const float inv = 1.0f / (float)a.Cp;
+  void* args[] = {&a, const_cast<EpiArgs*>(&e), const_cast<const f16**>(&zpage), const_cast<float*>(&inv)};
+  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(CF::NT), args, lds, s));
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;

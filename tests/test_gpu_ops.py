@@ -40,11 +40,15 @@ def _tm(x):  # [B, C, T] -> time-major [B*T, C]
 ])
 @pytest.mark.parametrize("variant", ["0", "1", "-1", "10", "11", "12", "13", "14", "15", "20", "21", "22", "24"])
 @pytest.mark.parametrize("halo", ["1", "0"])
-def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, halo, monkeypatch):
+@pytest.mark.parametrize("direct", ["15", "0"])
+def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, halo, direct, monkeypatch):
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)  # -1: v1, 0..4: conv_gemm2 tiles, 10..14: conv_gemm3 tiles, 15: auto
     monkeypatch.setenv("SVC_GEMM_HALO", halo)        # conv_gemm3 tap reuse (multi-tap, Cin % 64 == 0, |shift| <= 32)
+    monkeypatch.setenv("SVC_GEMM3_DIRECT", direct)   # conv_gemm3 register epilogues (all forms) or LDS-staged C tile
     if halo == "0" and variant not in ("10", "14", "15"):
         pytest.skip("the halo switch only affects conv_gemm3")
+    if direct == "0" and not (halo == "0" and variant in ("10", "11", "12", "13", "14", "15")):
+        pytest.skip("the epilogue switch only affects conv_gemm3's per-tap schedule")
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, Cin, T, generator=g)
     w = torch.randn(Cout, Cin, k, generator=g) / np.sqrt(Cin * k)

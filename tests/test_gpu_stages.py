@@ -56,7 +56,11 @@ def test_mel_energy(engine, cfg, golden):
         np.testing.assert_allclose(en[0].cpu().numpy(), ref_en, rtol=2e-5, atol=1e-7)
 
 
-def test_whisper_encoder_tiny(engine, golden):
+@pytest.mark.parametrize("direct", ["15", "0"])
+def test_whisper_encoder_tiny(engine, golden, direct, monkeypatch):
+    """Whisper encoder against the reference-pinned golden, with conv_gemm3's register epilogues (qkv / fc1: f16
+    outputs, out / fc2: f32 residual) and with the LDS-staged epilogue (SVC_GEMM3_DIRECT=0)."""
+    monkeypatch.setenv("SVC_GEMM3_DIRECT", direct)
     g = golden("whisper_logmel")
     wav16 = g["wav16"]
     feats = engine.whisper_encode(dev(wav16[None]))
@@ -138,9 +142,13 @@ def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, monkeypatch):
     assert rel_l2(eps, ref) < 5e-3
 
 
-@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15", "20", "21", "22", "24"])
+@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "21", "22", "24"])
 def test_eps_gemm_variants(engine, golden, variant, monkeypatch):
-    """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path)."""
+    """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path); 15lds:
+    conv_gemm3 with the LDS-staged epilogue everywhere; 15reg: with every register form, in the sampler too."""
+    if variant in ("15lds", "15reg"):
+        monkeypatch.setenv("SVC_GEMM3_DIRECT", "0" if variant == "15lds" else "15")
+        variant = "15"
     monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
     monkeypatch.setenv("SVC_DIFF_FUSED", "0")
     g = golden("conditioner_diffsvc")
@@ -177,7 +185,9 @@ def test_sampler_sub_streams_bit_identical(engine, golden, monkeypatch):
         assert np.array_equal(outs[ns][0], outs["1"][0]) and np.array_equal(outs[ns][1], outs["1"][1]), ns
 
 
-def test_bigvgan(engine, cfg, states, golden):
+@pytest.mark.parametrize("direct", ["15", "0"])
+def test_bigvgan(engine, cfg, states, golden, direct, monkeypatch):
+    monkeypatch.setenv("SVC_GEMM3_DIRECT", direct)  # conv_gemm3 register epilogues (default) or the LDS-staged one
     g = golden("bigvgan")
     stats = C.load_stats(cfg)
     mel = g["mel"]  # de-normalised mel [100, T]
