@@ -561,6 +561,15 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   // (703 vs 713 audio-s/s, same box), so it is opt-in.
   const char* renv = getenv("SVC_GEMM4_RMW");
   const char* genv = getenv("SVC_GEMM4_GATE");  // 0: the gate GEMM on conv_gemm4's LDS-staged epilogue (variant 20)
+  // SVC_SITE_VARIANT="site=variant,...": per-call-site override (tile / kernel A/B runs, e.g. diffsvc.outproj=20)
+  if (const char* senv = getenv("SVC_SITE_VARIANT")) {
+    const size_t sl = site ? strlen(site) : 0;
+    for (const char* p = senv; sl && (p = strstr(p, site)) != nullptr; p += sl)
+      if ((p == senv || p[-1] == ',') && p[sl] == '=') {
+        variant = atoi(p + sl + 1);
+        break;
+      }
+  }
   if (variant == 15 && pair) variant = (genv && !atoi(genv)) ? 20 : 24;
   if (variant == 15 && renv && atoi(renv) && conv_gemm4_rmw_form(a, e)) variant = 24;
   if (pair || g.N > 64) {
