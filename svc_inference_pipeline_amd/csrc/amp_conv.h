@@ -14,6 +14,7 @@ struct AmpConvArgs {
   int Kpad;
   const float* bias;
   int dbg;  // diagnostics (tools/amp_bench.py, SVC_AMP_DBG): 1 = skip the activation phase, 2 = skip the conv phase
+  int run_adapt = 0;  // activation runs sized for one task per thread (SVC_AMP_RUN, default on)
 };
 
 bool amp_conv_supported(int C, int k, int d);

@@ -55,12 +55,16 @@ __global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs
   if (p.dbg == 1) {
     for (int i = tid; i < rows * CF::LDA; i += AMP_NT) As[i] = (f16)0.0f;
   } else {
-    constexpr int VEC = CF::VEC, BLK = 8, RUN = CF::RUN;
+    constexpr int VEC = CF::VEC, BLK = 8;
     using V = ActVec<VEC>;
     float f[12];
 #pragma unroll
     for (int q = 0; q < 12; ++q) f[q] = p.filt[q];
     const int ngrp = C / VEC;
+    // run length: with p.run_adapt, the shortest multiple of BLK that gives every (channel, run) task to its own
+    // thread (one exposed load latency per thread: a run's sliding window prefetches its next block), else CF::RUN
+    const int nr_fit = max(1, AMP_NT / ngrp);
+    const int RUN = p.run_adapt ? ((rows + nr_fit - 1) / nr_fit + BLK - 1) / BLK * BLK : CF::RUN;
     const int nruns = (rows + RUN - 1) / RUN;
     const float* xb = p.x + (int64_t)b * L * C;
     for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
@@ -279,6 +283,15 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
                   (!e.acc32 || e.ld_acc == C) && !e.add16 && e.act == ACT_NONE && e.kind == EPI_GENERIC,
               "amp_conv: epilogue must be contiguous rows of C channels (bias / add_row / acc32 / out32 / out16)");
   SVC_REQUIRE(((uintptr_t)p.x & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "amp_conv: alignment");
+  static const int run_adapt = [] {
+    const char* v = getenv("SVC_AMP_RUN");  // "0": the fixed run length (A/B runs)
+    return v && v[0] == '0' ? 0 : 1;
+  }();
+  if (run_adapt && !p.run_adapt) {
+    AmpConvArgs q = p;
+    q.run_adapt = 1;
+    return amp_conv(q, C, e, s);
+  }
   if (const char* dbg = getenv("SVC_AMP_DBG")) {
     AmpConvArgs q = p;
     q.dbg = atoi(dbg);
