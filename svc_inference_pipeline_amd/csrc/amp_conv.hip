@@ -31,7 +31,8 @@ struct AmpCfg {
   // the epilogue works in registers (operand-swapped MFMAs, see below), so LDS holds only the activation image:
   // C = 48: 34 KiB -> 4 workgroups per CU (3 with the former 48 KiB C staging), C = 24: 15 KiB
   static constexpr int LDS = A_BYTES;
-  // activation tasks: VEC channels x RUN rows per thread (VEC 2 / RUN 32 for C = 48 measured 18 % slower: 137 VGPRs)
+  // activation tasks: VEC channels x RUN rows per thread for MODE 0 / 1 (MODE 2 / 3 use channel pairs in 4-row blocks;
+  // the earlier VEC 2 / RUN 32 / 8-row-block form for C = 48 measured 18 % slower: 137 VGPRs + AGPRs, 3 waves)
   static constexpr int VEC = 1;
   static constexpr int RUN = C == 24 ? 32 : 16;  // C = 24: 24 x 10 runs = 240 tasks (611 -> 562-585 us / launch)
   static_assert(C % 8 == 0 && LDA % 8 == 0, "16-B fragment rows");
@@ -39,8 +40,14 @@ struct AmpCfg {
 
 constexpr int AMP_NT = 256;
 
-template <int C>
-__global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
+// MODE 0: launch bounds with no occupancy target (the compiler then splits the register file into 64-119 VGPRs +
+// 32-48 AGPRs); MODE 1: a 4-waves-per-SIMD target, under which it keeps the accumulators in the unified VGPR file
+// (C = 24: 67 registers, 7 waves per SIMD instead of 5; C = 48: LDS-limited to 4 either way); MODE 2: as 1, with
+// C = 48's activation on channel pairs (packed f32 FMAs, 4-row blocks to fit the same registers); MODE 3 (default):
+// as 2 for C = 24 too (79 registers, 6 waves per SIMD). Per launch, B = 32 x 10 s (tools/amp_bench.py): C = 48
+// 7-20 % and C = 24 7-12 % faster than MODE 0; end to end +0.5 % (2 -> 0) and +0.3 % (3 -> 2)
+template <int C, int MODE>
+__global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
   using CF = AmpCfg<C>;
   extern __shared__ __align__(16) unsigned char amp_sm[];
   f16* As = reinterpret_cast<f16*>(amp_sm);
@@ -55,7 +62,8 @@ __global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs
   if (p.dbg == 1) {
     for (int i = tid; i < rows * CF::LDA; i += AMP_NT) As[i] = (f16)0.0f;
   } else {
-    constexpr int VEC = CF::VEC, BLK = 8;
+    constexpr bool PK = (MODE == 2 && C == 48) || (MODE == 3 && C <= 48);
+    constexpr int VEC = PK ? 2 : CF::VEC, BLK = PK ? 4 : 8;
     using V = ActVec<VEC>;
     float f[12];
 #pragma unroll
@@ -249,12 +257,12 @@ __global__ __launch_bounds__(AMP_NT) void amp_conv_kernel(AmpConvArgs p, EpiArgs
   }
 }
 
-template <int C>
-static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
+template <int C, int MODE>
+static int launch_amp_mode(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   using CF = AmpCfg<C>;
   static bool attr = false;
   if (!attr) {
-    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)amp_conv_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)amp_conv_kernel<C, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       CF::LDS));
     attr = true;
   }
@@ -265,10 +273,22 @@ static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   const double bytes = elems * (4.0 + (e.out32 ? 4 : 0) + (e.out16 ? 2 : 0) + (e.add_row ? 4 : 0) + (e.acc32 ? 4 : 0));
   const char* tag = C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>");
   const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
-  hipLaunchKernelGGL(amp_conv_kernel<C>, dim3((unsigned)grid), dim3(AMP_NT), CF::LDS, s, p, e);
+  hipLaunchKernelGGL((amp_conv_kernel<C, MODE>), dim3((unsigned)grid), dim3(AMP_NT), CF::LDS, s, p, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
+}
+
+template <int C>
+static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
+  static const int mode = [] {
+    const char* v = getenv("SVC_AMP_MODE");  // A/B runs of the register / packed-activation forms
+    return v ? atoi(v) : 3;
+  }();
+  if (mode == 0) return launch_amp_mode<C, 0>(p, e, s);
+  if (mode == 1) return launch_amp_mode<C, 1>(p, e, s);
+  if (mode == 2) return launch_amp_mode<C, 2>(p, e, s);
+  return launch_amp_mode<C, 3>(p, e, s);
 }
 
 bool amp_conv_supported(int C, int k, int d) {
