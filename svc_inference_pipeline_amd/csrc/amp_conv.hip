@@ -281,10 +281,8 @@ static int launch_amp_mode(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s
 
 template <int C>
 static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
-  static const int mode = [] {
-    const char* v = getenv("SVC_AMP_MODE");  // A/B runs of the register / packed-activation forms
-    return v ? atoi(v) : 3;
-  }();
+  const char* mv = getenv("SVC_AMP_MODE");  // A/B runs of the register / packed-activation forms (read per call)
+  const int mode = mv ? atoi(mv) : 3;
   if (mode == 0) return launch_amp_mode<C, 0>(p, e, s);
   if (mode == 1) return launch_amp_mode<C, 1>(p, e, s);
   if (mode == 2) return launch_amp_mode<C, 2>(p, e, s);

@@ -104,11 +104,15 @@ def test_activation1d(B, L, C, variant, monkeypatch):
     assert np.max(np.abs(out - ref.numpy()) / (np.abs(ref.numpy()) + 1e-2)) < 5e-3
 
 
+@pytest.mark.parametrize("mode", ["3", "2", "1", "0"])
 @pytest.mark.parametrize("C", [24, 48, 96])
 @pytest.mark.parametrize("B,L,k,d", [(2, 37, 3, 1), (1, 1, 11, 5), (1, 5, 7, 3), (2, 130, 11, 5), (1, 300, 7, 3),
                                      (3, 257, 11, 1)])
-def test_amp_conv(B, L, k, d, C):
-    """Fused SnakeBeta Activation1d -> dilated conv -> bias + residual (BigVGAN C <= 96 stages)."""
+def test_amp_conv(B, L, k, d, C, mode, monkeypatch):
+    """Fused SnakeBeta Activation1d -> dilated conv -> bias + residual (BigVGAN C <= 96 stages), in every kernel form
+    (SVC_AMP_MODE: 3 = default packed channel-pair activation, 2 = packed for C = 48 only, 1 / 0 = scalar activation
+    with / without the occupancy launch bound)."""
+    monkeypatch.setenv("SVC_AMP_MODE", mode)
     from svc_inference_pipeline_amd import weights as W
     g = torch.Generator().manual_seed(5)
     x = torch.randn(B, C, L, generator=g) * 2
