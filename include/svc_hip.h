@@ -125,7 +125,6 @@ svc_status svc_op_conv1d(const float* x, int B, int T_in, int Cin, const float* 
 /* ConvTranspose1d, w [Cin][Cout][k]; T_out = (T_in-1)*stride - 2*pad + k */
 svc_status svc_op_conv_transpose1d(const float* x, int B, int T_in, int Cin, const float* w, const float* bias,
                                    int Cout, int k, int stride, int pad, float* y, void* stream);
-/* Activation1d(SnakeBeta, logscale): x f32 [B*L][C] -> y f32 [B*L][C] */
 /* Rational-ratio resampler (F1; replaces librosa.resample in utils/audio.py:49-53 and ffmpeg's 16 kHz decode in
  * utils/whisper_extractor/audio.py:41-49). x f32 [B][n_in] -> y f32 [B][svc_resample_len(n_in, sr_in, sr_out)],
  * scipy.signal.resample_poly's Kaiser(5) polyphase FIR; quantize16 = 1 rounds to int16 / 32768 (s16le decode). */
@@ -141,6 +140,7 @@ svc_status svc_resample_filter(int sr_in, int sr_out, double* h, int cap, int* n
 svc_status svc_op_amp_conv(const float* x, int B, int L, int C, const float* alpha_log, const float* beta_log,
                            const float* filt, const float* w, const float* bias, int k, int d, const float* add_row,
                            float* y, void* stream);
+/* Activation1d(SnakeBeta, logscale): x f32 [B*L][C] -> y f32 [B*L][C] */
 svc_status svc_op_activation1d(const float* x, int B, int L, int C, const float* alpha_log, const float* beta_log,
                                const float* filt12, float* y, void* stream);
 /* attention on f32 q,k,v [B*L][D] (already projected; scaled inside by dh^-1/4 each) -> out f32 [B*L][D] */
@@ -157,7 +157,9 @@ svc_status svc_profile_filter(const char* kernel_prefix);
 svc_status svc_profile_read(int idx, char* name, int name_len, double* total_ms, int64_t* launches, double* flops,
                             double* bytes, int* n_kernels);
 /* GEMM microbenchmark on synthetic operands: average ms per launch of one implicit-GEMM configuration
-   (variant -1 = first-generation kernel, >= 0 = conv_gemm2 tile variants); epi 0 = f16 store, 1 = paired gate */
+   (variant -1 = first-generation kernel, 0-9 = conv_gemm2 tiles, 10-14 = conv_gemm3 tiles, 15 = the production
+   choice, 20 / 24 = conv_gemm4 with the LDS-staged / register epilogue, 21 / 22 = conv_gemm5; see run_gemm in
+   engine.hip); epi 0 = f16 store, 1 = paired gate, 2 / 6 = f32 / split-fp16 residual read-modify-write */
 svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi, int variant, int iters, double* ms_out);
 /* slaney mel filterbank (librosa.filters.mel, htk=False, norm='slaney') computed natively, host output */
 svc_status svc_mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double fmax, float* out_host);
