@@ -273,7 +273,12 @@ static int launch_amp_mode(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s
   const double bytes = elems * (4.0 + (e.out32 ? 4 : 0) + (e.out16 ? 2 : 0) + (e.add_row ? 4 : 0) + (e.acc32 ? 4 : 0));
   const char* tag = C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>");
   const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
-  hipLaunchKernelGGL((amp_conv_kernel<C, MODE>), dim3((unsigned)grid), dim3(AMP_NT), CF::LDS, s, p, e);
+  // the activation image needs BT + 2P rows, not BT + 2 MAXP: sized per launch, C = 48 fits 5 workgroups per CU
+  // (instead of 4) for every conv with P <= 15 (SVC_AMP_LDS=max keeps the worst-case size, A/B runs)
+  const char* lenv = getenv("SVC_AMP_LDS");
+  const int P = (p.k - 1) / 2 * p.d;
+  const int lds = lenv && lenv[0] == 'm' ? CF::LDS : (CF::BT + 2 * P) * CF::LDA * 2;
+  hipLaunchKernelGGL((amp_conv_kernel<C, MODE>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, p, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
