@@ -68,6 +68,21 @@ def test_whisper_encoder_tiny(engine, golden, direct, monkeypatch):
     assert rel_l2(feats[0].cpu().numpy(), ref) < 5e-3
 
 
+def test_whisper_stream_split(engine, golden, monkeypatch):
+    """SVC_WHISPER_STREAMS = 2 / 3 (utterance-aligned sub-batches on concurrent streams) against the default single
+    full-batch stream, on a batch of 3 clips; the sub-batch launches may pick other GEMM tiles, so the bound is fp32
+    rounding, not bit equality."""
+    g = golden("whisper_logmel")
+    w = dev(np.stack([g["wav16"], g["wav16"][::-1].copy(), 0.5 * g["wav16"]]))
+    monkeypatch.setenv("SVC_WHISPER_STREAMS", "1")
+    one = engine.whisper_encode(w).cpu().numpy()
+    for ns in ("2", "3"):
+        monkeypatch.setenv("SVC_WHISPER_STREAMS", ns)
+        split = engine.whisper_encode(w).cpu().numpy()
+        for b in range(3):
+            assert rel_l2(split[b], one[b]) < 1e-4, (ns, b)
+
+
 def test_content_map_exact(engine, golden):
     g = golden("content_map")
     raw = torch.from_numpy(g["raw"]).float()
