@@ -6,7 +6,12 @@ whole hot path over one batch already resident in HBM: mel/energy, Praat-AC F0, 
 Whisper log-mel + encoder, content map, conditioner, PLMS-100 sampler, de-normalisation, BigVGAN,
 fade-out, and (N > 1) the RCCL gather of every rank's waveforms to rank 0.
 
-    python bench.py [--gpus N --steps K --warmup W]        (N > 1: launched by torch.distributed.run)
+    python bench.py [--gpus N --steps K --warmup W]
+
+N > 1: either launched by torch.distributed.run (RANK / LOCAL_RANK / WORLD_SIZE set, one process per GPU), or, when
+WORLD_SIZE is unset, this process spawns the N ranks itself (spawn_ranks) BEFORE anything touches the GPU and exits
+with the worst rank's status. `--dry-run` replaces the engine by an identity "conversion" of the synthetic clips on
+the CPU (gloo), so the spawn / sharding / gather path can be tested without a GPU (tests/test_parallel.py).
 
 Weights are seeded random tensors of the reference architectures (no checkpoints offline); inputs
 are synthetic harmonic clips. Rank 0 prints one JSON line.
@@ -14,6 +19,8 @@ are synthetic harmonic clips. Rank 0 prints one JSON line.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -50,20 +57,45 @@ def synth_inputs(uids, seconds, float16k=False):
     return w24, w16
 
 
-def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads, hs=None, fast=True):
+def host_cpus():
+    """CPUs this process may use: the scheduler affinity mask, capped by a cgroup CPU quota when one is set
+    (a GPU box's process sees the whole machine in nproc but gets a share of it). -> (threads, info dict)."""
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    threads = min(affinity, quota) if quota else affinity
+    return threads, {"nproc": affinity, "cgroup_quota_cpus": quota, "cpu_model": model,
+                     "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads, hs=None, fast=True, host=None):
     """The oracle (CPU restatement of the reference path, torch-CPU fp32) on ONE clip of the same
     workload, timed on this host: mel/energy, F0, pitch shift, Whisper-medium, map, conditioner,
     PLMS (speedup 10 = 101 denoiser calls), de-normalisation, BigVGAN, fade."""
     from oracle import pipeline as OP
     torch.set_num_threads(threads)
+    host = dict(host or {})
     w24, w16 = synth_inputs([0], seconds, float16k=hs is not None)
     if fast:
         t0 = time.time()
         OP.convert(cfg, ws, ms, vs, w24[0], w16[0], singer=1, speedup=speedup, seed=0, hs=hs)
         dt = time.time() - t0
-        return {"value": round(seconds / dt, 4), "unit": "audio-s/s", "cores": threads, "kind": "port",
+        return {"value": round(seconds / dt, 4), "unit": "audio-s/s", "cores": threads, "kind": "port", **host,
                 "sample": f"1 x {seconds:g} s clip, full oracle path (PLMS speedup {speedup}), torch-CPU fp32, "
-                          f"{threads} threads, {dt:.1f} s"}
+                          f"{threads} threads (all CPUs available to the process), {dt:.1f} s"}
     # DDPM-1000 on the CPU is ~2 min per clip: time the path once with PLMS speedup 250 (5 denoiser calls) and
     # 10 more denoiser calls alone, then extrapolate the sampler to 1000 calls.
     from oracle import models as OM
@@ -79,7 +111,7 @@ def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads, hs=None, fast=True)
         OM.diffsvc_forward(ms, cfg.mapper, x, cond, torch.tensor([999 - i]), table)
     t_call = (time.time() - t0) / 10
     dt = t_path + (1000 - 5) * t_call
-    return {"value": round(seconds / dt, 4), "unit": "audio-s/s", "cores": threads, "kind": "port",
+    return {"value": round(seconds / dt, 4), "unit": "audio-s/s", "cores": threads, "kind": "port", **host,
             "sample": f"1 x {seconds:g} s clip, oracle path with 5 denoiser calls ({t_path:.1f} s) + 995 x "
                       f"{t_call * 1e3:.0f} ms timed denoiser calls (DDPM-1000 extrapolated), torch-CPU fp32, {threads} threads"}
 
@@ -94,16 +126,79 @@ def family(prof):
     return out
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n, argv):
+    """Run `bench.py argv` as n rank processes (RANK = LOCAL_RANK = 0..n-1, WORLD_SIZE = n, rendezvous on
+    127.0.0.1) and return the worst exit status. The caller has not touched the GPU (no torch.cuda call, no
+    libsvc_hip load): every rank is a fresh child process, nothing is exec'ed from a GPU-initialised process."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    for p in procs:
+        code = p.wait()
+        if code != 0 and rc == 0:
+            rc = code if code > 0 else 128 - code
+    if rc:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def dry_run(args, dist):
+    """CPU stand-in for the engine (gloo): each rank "converts" its shard of synthetic clips by the identity
+    (the 24 kHz clip trimmed to T*hop samples, as the vocoder output is), keyed by global utterance id exactly as
+    the GPU run is, then runs the same gather. Rank 0 prints the bench line's distributed fields and, with
+    --dump, saves the gathered waveforms, so world 1 and world N outputs can be compared (tests/test_parallel.py)."""
+    B = args.batch
+    uids = np.arange(dist.rank * B, (dist.rank + 1) * B)
+    w24, _ = synth_inputs(uids, args.seconds)
+    T = (w24.shape[1] + 768 - 1024) // 256 + 1
+    wav = torch.from_numpy(np.ascontiguousarray(w24[:, :T * 256]))
+    dist.barrier()
+    t0 = time.time()
+    out = None
+    for _ in range(args.steps):
+        out, lens = dist.gather_waveforms(wav, return_lengths=True)
+    dist.barrier()
+    per_rank = [r[0] for r in dist.all_gather_floats([time.time() - t0])]
+    elapsed = max(per_rank)
+    if dist.rank == 0:
+        assert out.shape[0] == dist.world * B and bool(torch.isfinite(out).all())
+        if args.dump:
+            np.save(args.dump, out.numpy())
+        print(json.dumps({"metric": "dry-run gather (identity conversion, CPU)", "n_gpus": args.gpus,
+                          "dist_world": dist.world, "backend": dist.backend or "none", "steps": args.steps,
+                          "per_rank_s": [round(t, 4) for t in per_rank], "elapsed_s": round(elapsed, 4),
+                          "gathered": list(out.shape), "lengths": lens.tolist()}), flush=True)
+    dist.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo identity conversion: exercises the rank spawn, sharding and gather only")
+    ap.add_argument("--dump", default=None, help="(--dry-run) save rank 0's gathered waveforms to this .npy")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--speedup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads for the CPU baseline (default: every CPU available to the process)")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--content", choices=["whisper", "contentvec"], default="whisper",
                     help="content encoder (BASELINE config 5: contentvec = the HuBERT/ContentVec variant)")
@@ -113,6 +208,14 @@ def main():
                     help="content encoder GEMMs on split-fp16 operands (the precision mode that meets the 1e-3 mel-L1 "
                          "target in tools/precision_sweep.py)")
     args = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    if args.dry_run:
+        return dry_run(args, DistContext.from_env(backend="gloo"))
 
     dist = DistContext.from_env()
     torch.cuda.set_device(dist.local_rank)
@@ -203,7 +306,8 @@ def main():
         log(f"step {i + 1}/{args.steps} {time.time() - t0:.2f}s")
     torch.cuda.synchronize()
     dist.barrier()
-    elapsed = dist.max_over_ranks(time.time() - t0)
+    per_rank = [r[0] for r in dist.all_gather_floats([time.time() - t0])]
+    elapsed = max(per_rank)
     prof = _lib.profile_read()
     _lib.profile_enable(False)
     _lib.profile_filter("")
@@ -266,11 +370,15 @@ def main():
     cpu = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, 1 clip)...")
-        cpu = cpu_baseline(cfg, ws, ms, vs, args.seconds, args.speedup, args.cpu_threads, hs=hs, fast=fast)
+        threads, host = host_cpus()
+        cpu = cpu_baseline(cfg, ws, ms, vs, args.seconds, args.speedup, args.cpu_threads or threads, hs=hs,
+                           fast=fast, host=host)
     if dist.rank == 0:
         line = {
             "metric": "converted audio sec/sec (RTF^-1) end-to-end, 10 s clips",
             "value": round(value, 2), "unit": "audio-s/s", "n_gpus": dist.world, "steps": args.steps,
+            "dist_world": dist.world, "backend": dist.backend or "none",
+            "per_rank_ms_per_step": [round(1000.0 * t / args.steps, 2) for t in per_rank],
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
             "config": {"workload": f"batch={B}/GPU x {args.seconds:g} s synthetic clips, "

@@ -106,7 +106,9 @@ svc_status svc_condition(svc_ctx* ctx, const void* content_f16, const double* f0
 /* A11+A12: cond f32 [B*T][384] -> x_0 f32 [B*T][n_mel] (normalised mel, time-major).
    mode SVC_MODE_DDPM: `interval` ignored, 1000 steps; SVC_MODE_PLMS: reference speedup (e.g. 10).
    x_T f32 [B*T][n_mel] or NULL (then drawn on device from `seed` and `utt_ids`).
-   noise (DDPM only) f32 [steps][B*T][n_mel] (already in time-major order) or NULL (device Philox noise). */
+   noise (DDPM only) f32 [steps][B*T][n_mel] (already in time-major order) or NULL (device Philox noise keyed by
+   `seed` and `utt_ids`). utt_ids int32 [B] may be NULL only when nothing is drawn on the device: x_T given and,
+   for DDPM, `noise` given; otherwise a NULL utt_ids is SVC_ERR_INVALID. */
 svc_status svc_diffsvc_sample(svc_ctx* ctx, const float* cond, int B, int T, int mode, int interval, const float* x_T,
                               const float* noise, uint64_t seed, const int32_t* utt_ids, float* x0, void* stream);
 

@@ -1905,6 +1905,8 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
   SVC_REQUIRE(mode == SVC_MODE_DDPM || (mode == SVC_MODE_PLMS && interval >= 1), "sample: mode %d interval %d", mode,
               interval);
   SVC_REQUIRE(x_T || utt_ids, "sample: need x_T or utt_ids for device noise");
+  // DDPM draws step noise on the device unless `noise` is given; that noise is keyed by utterance id
+  SVC_REQUIRE(mode != SVC_MODE_DDPM || noise || utt_ids, "sample: DDPM without `noise` needs utt_ids");
   hipStream_t s = (hipStream_t)stream;
   const int rows = B * T, nm = c->n_mel, ld16 = (int)round_up(nm, 8);
   int st;

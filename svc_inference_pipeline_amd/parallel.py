@@ -50,24 +50,50 @@ class DistContext:
         torchdist.all_reduce(t, op=torchdist.ReduceOp.MAX)
         return float(t.item())
 
-    def gather_waveforms(self, wav):
-        """Gather every rank's [B_r, S] waveforms to rank 0 -> [sum B_r, S] on rank 0, None elsewhere.
-        Shards of unequal size are padded to the largest B (lengths exchanged first)."""
+    def all_gather_floats(self, values):
+        """Every rank's list of floats (same length on every rank) -> [world][len] on every rank."""
         if self.world == 1:
-            return wav
-        n = torch.tensor([wav.shape[0]], dtype=torch.int64, device=wav.device)
-        sizes = [torch.zeros_like(n) for _ in range(self.world)]
-        torchdist.all_gather(sizes, n)
-        sizes = [int(s.item()) for s in sizes]
-        bmax = max(sizes)
-        if wav.shape[0] < bmax:
-            pad = torch.zeros(bmax - wav.shape[0], *wav.shape[1:], dtype=wav.dtype, device=wav.device)
-            wav = torch.cat([wav, pad])
-        bufs = [torch.empty_like(wav) for _ in range(self.world)] if self.rank == 0 else None
-        torchdist.gather(wav.contiguous(), gather_list=bufs, dst=0)
+            return [list(map(float, values))]
+        dev = "cuda" if self.backend == "nccl" else "cpu"
+        t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=dev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        torchdist.all_gather(out, t)
+        return [o.cpu().tolist() for o in out]
+
+    def gather_waveforms(self, wav, lengths=None, return_lengths=False):
+        """Gather every rank's [B_r, S_r] waveforms to rank 0 -> [sum B_r, max S_r] on rank 0, None elsewhere.
+
+        The (B_r, S_r) shapes are all-gathered first (one int64 pair per rank); each shard is zero-padded to the
+        largest B and S, so ranks may hold different numbers of utterances and different clip lengths.
+        `lengths` (int [B_r], default S_r for every row) are the per-utterance valid sample counts; with
+        `return_lengths` rank 0 also gets them for the whole gathered batch (int64 [sum B_r], None elsewhere)."""
+        if lengths is None:
+            lengths = torch.full((wav.shape[0],), wav.shape[1] if wav.dim() > 1 else 0, dtype=torch.int64)
+        lengths = torch.as_tensor(lengths, dtype=torch.int64)
+        if self.world == 1:
+            return (wav, lengths) if return_lengths else wav
+        dev = wav.device
+        shape = torch.tensor([wav.shape[0], wav.shape[1] if wav.dim() > 1 else 0], dtype=torch.int64, device=dev)
+        shapes = [torch.zeros_like(shape) for _ in range(self.world)]
+        torchdist.all_gather(shapes, shape)
+        shapes = [(int(s[0].item()), int(s[1].item())) for s in shapes]
+        bmax = max(b for b, _ in shapes)
+        smax = max(s for _, s in shapes)
+        buf = torch.zeros(bmax, smax, dtype=wav.dtype, device=dev)
+        if wav.numel():
+            buf[:wav.shape[0], :wav.shape[1]] = wav
+        lbuf = torch.zeros(bmax, dtype=torch.int64, device=dev)
+        lbuf[:lengths.numel()] = lengths.to(dev)
+        bufs = [torch.empty_like(buf) for _ in range(self.world)] if self.rank == 0 else None
+        lbufs = [torch.empty_like(lbuf) for _ in range(self.world)] if self.rank == 0 else None
+        torchdist.gather(buf, gather_list=bufs, dst=0)
+        torchdist.gather(lbuf, gather_list=lbufs, dst=0)
         if self.rank != 0:
-            return None
-        return torch.cat([b[:s] for b, s in zip(bufs, sizes)])
+            return (None, None) if return_lengths else None
+        out = torch.cat([b[:n] for b, (n, _) in zip(bufs, shapes)])
+        if return_lengths:
+            return out, torch.cat([l[:n] for l, (n, _) in zip(lbufs, shapes)]).cpu()
+        return out
 
     def close(self):
         if self.world > 1 and torchdist.is_initialized():

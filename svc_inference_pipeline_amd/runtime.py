@@ -30,6 +30,18 @@ def mel_frames(n_samples, n_fft=1024, hop=256):
     return (n_samples + (n_fft - hop) - n_fft) // hop + 1
 
 
+def check_supported(cfg):
+    """Reject configurations the native path does not implement, before any device work (raise ValueError)."""
+    merge = getattr(cfg.mapper, "merge_mode", "add")
+    if merge != "add":
+        # modules/encoder.py:193-199: "add" sums the sub-encoder outputs, "concat" widens cond to their summed
+        # widths. The native conditioner implements "add" only; anything else must not silently mis-condition.
+        raise ValueError(f"mapper.merge_mode {merge!r}: only 'add' is supported (modules/encoder.py:195-199)")
+    if cfg.vocoder.activation not in ("snake", "snakebeta"):
+        raise ValueError(f"vocoder.activation {cfg.vocoder.activation!r}: snake or snakebeta "
+                         "(modules/bigvgan.py:392-421)")
+
+
 class SVCEngine:
     """Stages of infer.py on one GPU. `whisper_state`, `mapper_state`, `vocoder_state`, `hubert_state` are dicts
     in the reference's state_dict naming (svc_inference_pipeline_amd.weights; fairseq's for HuBERT); any subset
@@ -39,6 +51,7 @@ class SVCEngine:
 
     def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None, hubert_state=None,
                  hubert_output_layer=9, content_split=False):
+        check_supported(cfg)
         _lib.load()
         self.cfg = cfg
         self.device = device
@@ -208,7 +221,8 @@ class SVCEngine:
         """svc_model_inference (modules/diffsvcrepo_inference.py:154-240) -> normalised mel x_0 f32 [B, T, n_mel]."""
         B, T, _ = cond.shape
         x0 = torch.empty(B, T, self.cfg.mapper.n_mel, device=cond.device, dtype=torch.float32)
-        if x_T is None and utt_ids is None:
+        if utt_ids is None and (x_T is None or (noise is None and not fast_inference)):
+            # device noise (x_T, and DDPM's per-step z) is keyed by utterance id: default to batch positions
             utt_ids = torch.arange(B, device=cond.device, dtype=torch.int32)
         uid = utt_ids.to(torch.int32).contiguous() if utt_ids is not None else None
         mode = MODE_PLMS if fast_inference else MODE_DDPM

@@ -35,3 +35,13 @@ def test_convert_many_rejects_mismatched_lists():
     pipe = SVCPipeline.__new__(SVCPipeline)
     with pytest.raises(ValueError):
         pipe.convert_many([torch.zeros(10)], [], [0])
+
+
+def test_check_supported_rejects_concat_merge_mode():
+    from svc_inference_pipeline_amd import config as C
+    from svc_inference_pipeline_amd.runtime import check_supported
+    cfg = C.load_config()
+    check_supported(cfg)  # the reference config ("add") is accepted
+    cfg.mapper.merge_mode = "concat"
+    with pytest.raises(ValueError, match="merge_mode"):
+        check_supported(cfg)
