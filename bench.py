@@ -144,15 +144,21 @@ def spawn_ranks(n, argv):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    # poll all ranks: the first failure ends the others (a peer blocked in a collective would never return)
     rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0] if bad[0] > 0 else 128 - bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+            break
+        time.sleep(0.2)
     for p in procs:
         code = p.wait()
         if code != 0 and rc == 0:
             rc = code if code > 0 else 128 - code
-    if rc:
-        for p in procs:
-            if p.poll() is None:
-                p.kill()
     return rc
 
 
@@ -204,9 +210,10 @@ def main():
                     help="content encoder (BASELINE config 5: contentvec = the HuBERT/ContentVec variant)")
     ap.add_argument("--sampler", choices=["plms", "ddpm"], default="plms",
                     help="plms = the reference's fast_inference PLMS (speedup --speedup); ddpm = 1000-step DDPM")
-    ap.add_argument("--content-split", action="store_true",
-                    help="content encoder GEMMs on split-fp16 operands (the precision mode that meets the 1e-3 mel-L1 "
-                         "target in tools/precision_sweep.py)")
+    ap.add_argument("--precision", choices=["wsplit", "split", "fp16"], default="wsplit",
+                    help="wsplit (default): weight-split Whisper linears, split-fp16 conv stem / HuBERT / DiffSVC head, "
+                         "the mode that meets the 1e-3 mel-L1 target (tests/test_gpu_headline.py); split: every "
+                         "content GEMM on split-fp16 operands; fp16: plain fp16 operands (faster, fails the target)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -231,7 +238,8 @@ def main():
     ms = W.make_mapper_state(cfg.mapper, seed=0)
     vs = W.make_vocoder_state(cfg.vocoder, seed=0)
     eng = SVCEngine(cfg, dist.local_rank, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs,
-                    content_split=args.content_split)
+                    content_split={"split": 1, "wsplit": 2, "fp16": 0}[args.precision],
+                    head_split=args.precision != "fp16")
     fast = args.sampler == "plms"
     pipe = SVCPipeline(eng)
     B = args.batch
@@ -385,7 +393,9 @@ def main():
                                    + ("Whisper-medium" if hs is None else "HuBERT/ContentVec (layer 9)")
                                    + (f" + PLMS-100 DiffSVC (speedup {args.speedup})" if fast else " + DDPM-1000 DiffSVC")
                                    + " + BigVGAN, fp16 MFMA operands / fp32 accumulate"
-                                   + (", split-fp16 content encoder" if args.content_split else ""),
+                                   + {"split": ", split-fp16 content encoder + DiffSVC head (mel-L1 <= 1e-3 mode)",
+                                      "wsplit": ", weight-split Whisper linears + split-fp16 stem / DiffSVC head",
+                                      "fp16": ", plain fp16 operands (mel-L1 target not met)"}[args.precision],
                        "global_batch": dist.world * B, "seq_len_frames": int((d24.shape[1] + 768 - 1024) // 256 + 1),
                        "parallelism": f"dp{dist.world} (per-utterance shards, RCCL gather)"},
             "roofline": roof, "cpu_baseline": cpu,

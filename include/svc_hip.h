@@ -103,6 +103,13 @@ svc_status svc_hubert_dims(svc_ctx* ctx, int* final_dim, int* embed_dim);
 svc_status svc_condition(svc_ctx* ctx, const void* content_f16, const double* f0, const float* energy,
                          const int32_t* singer, int B, int T, float* cond, void* stream);
 
+/* A10's integer half, exported for bit-exact testing: the melody / loudness embedding indices the conditioner uses,
+   torch.bucketize(f0 f64, melody bins f32) and torch.bucketize(energy f32, loudness bins f32) with right=False and
+   torch's NaN placement (past the last bin) — modules/encoder.py:47-57,70 and :93-102,115. Bins are the context's
+   (checkpoint) bins. f0 [n] f64, energy [n] f32 -> melody_idx, loudness_idx [n] int32 in [0, n_bins - 1]. */
+svc_status svc_condition_indices(svc_ctx* ctx, const double* f0, const float* energy, int n, int32_t* melody_idx,
+                                 int32_t* loudness_idx, void* stream);
+
 /* A11+A12: cond f32 [B*T][384] -> x_0 f32 [B*T][n_mel] (normalised mel, time-major).
    mode SVC_MODE_DDPM: `interval` ignored, 1000 steps; SVC_MODE_PLMS: reference speedup (e.g. 10).
    x_T f32 [B*T][n_mel] or NULL (then drawn on device from `seed` and `utt_ids`).
@@ -159,9 +166,9 @@ svc_status svc_profile_filter(const char* kernel_prefix);
 svc_status svc_profile_read(int idx, char* name, int name_len, double* total_ms, int64_t* launches, double* flops,
                             double* bytes, int* n_kernels);
 /* GEMM microbenchmark on synthetic operands: average ms per launch of one implicit-GEMM configuration
-   (variant -1 = first-generation kernel, 0-9 = conv_gemm2 tiles, 10-14 = conv_gemm3 tiles, 15 = the production
-   choice, 20 / 24 = conv_gemm4 with the LDS-staged / register epilogue, 21 / 22 = conv_gemm5; see run_gemm in
-   engine.hip); epi 0 = f16 store, 1 = paired gate, 2 / 6 = f32 / split-fp16 residual read-modify-write */
+   (variant -1 = first-generation kernel, 10-14 = conv_gemm3 tiles, 15 = the production choice, 20 / 24 =
+   conv_gemm4 with the LDS-staged / register epilogue; see run_gemm in engine.hip); epi 0 = f16 store, 1 = paired
+   gate, 2 / 6 = f32 / split-fp16 residual read-modify-write */
 svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi, int variant, int iters, double* ms_out);
 /* slaney mel filterbank (librosa.filters.mel, htk=False, norm='slaney') computed natively, host output */
 svc_status svc_mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double fmax, float* out_host);

@@ -30,6 +30,7 @@ PROTOTYPES = {
     "svc_hubert_frames": (c_int64, [c_int64]),
     "svc_hubert_dims": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "svc_condition": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "svc_condition_indices": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
     "svc_diffsvc_sample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_uint64,
                                    c_void_p, c_void_p, c_void_p]),
     "svc_diffsvc_eps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),

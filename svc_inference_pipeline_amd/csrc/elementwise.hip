@@ -229,6 +229,9 @@ int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T,
 // ============================================================================ bucketize
 // torch.bucketize(x, bins) with right=False = number of bins < x. f0 is float64 and the f32 bins are
 // widened exactly (torch promotes to f64); energy is compared in f32 (modules/encoder.py:70,115).
+// The search step is torch's own `!(bins[mid] >= x)` (ATen Bucketization cus_lower_bound), not `bins[mid] < x`:
+// the two differ for NaN, which torch places past the last bin (index nb). NaN f0 is what pitch_shift gives an
+// utterance with no voiced frame (np.median of an empty array).
 __global__ void bucketize_kernel(const double* __restrict__ f0, const float* __restrict__ en,
                                  const float* __restrict__ mbins, const float* __restrict__ ebins, int nb,
                                  int* __restrict__ im, int* __restrict__ ie, int n) {
@@ -239,13 +242,13 @@ __global__ void bucketize_kernel(const double* __restrict__ f0, const float* __r
   int lo = 0, hi = nb;  // first index with bins[idx] >= x
   while (lo < hi) {
     int mid = (lo + hi) >> 1;
-    if ((double)mbins[mid] < fv) lo = mid + 1; else hi = mid;
+    if (!((double)mbins[mid] >= fv)) lo = mid + 1; else hi = mid;
   }
   im[i] = lo;
   lo = 0; hi = nb;
   while (lo < hi) {
     int mid = (lo + hi) >> 1;
-    if (ebins[mid] < ev) lo = mid + 1; else hi = mid;
+    if (!(ebins[mid] >= ev)) lo = mid + 1; else hi = mid;
   }
   ie[i] = lo;
 }

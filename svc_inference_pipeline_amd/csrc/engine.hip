@@ -113,11 +113,9 @@ int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int 
 int f32_to_f16x3_grouped(const float* x, f16* y, int rows, int C, int Cg, hipStream_t s);
 int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s);
-int conv_gemm2(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
 bool conv_gemm4_rmw_form(const ConvGemmArgs& a, const EpiArgs& e);
-int conv_gemm5(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int ns, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 struct DiffLayerArgs {
   const f16* x16;
@@ -274,7 +272,9 @@ struct svc_ctx {
   double fmin = 0, fmax = 12000, f0_min = 65, f0_max = 800;
   // content encoders in split-fp16 precision ("content.split" = 1 at finalize): every GEMM operand of Whisper /
   // HuBERT except the attention path is [hi | lo | hi] against [W_hi; W_hi; W_lo] weights (3x MFMA work)
-  bool content_split = false;
+  bool content_split = false;  // content_mode == 1
+  int content_mode = 0;         // "content.split": 0 fp16, 1 split-fp16 operands (x3), 2 weight-split (x2, Whisper)
+  bool head_split = true;  // DiffSVC skip_projection / output_projection on split-fp16 operands ("mapper.head_split")
   // whisper
   bool has_whisper = false;
   int wD = 0, wH = 0, wL = 0, wctx = 0, wmels = 80;
@@ -412,6 +412,33 @@ int pack_gemm_split3(svc_ctx* c, PackedGemm& g, int N, int Cin, WG wget, BG bget
       bget);
 }
 
+// Weight-split packing of a 1-tap GEMM (plain f16 operand): W'[n] = [f16(w) | f16(w - f16(w))] as TWO taps with a
+// zero row shift, so the implicit-GEMM A loader reads the same activation row for both and the product carries the
+// weights to ~22 significand bits at 2x the MFMA work, with no extra activation bytes. The weight rounding is the
+// larger share of an fp16 linear's error (precision).
+template <typename WG, typename BG>
+int pack_gemm_wsplit2(svc_ctx* c, PackedGemm& g, int N, int Cin, WG wget, BG bget) {
+  int st = pack_gemm(
+      c, g, N, Cin, Cin, 2,
+      [&](int n, int ci, int t) {
+        const float w = wget(n, ci, 0);
+        const float hi = (float)(f16)w;
+        return t == 0 ? hi : w - hi;
+      },
+      bget);
+  g.tap_mul = 0;
+  g.tap_add = 0;
+  g.istride = 1;
+  return st;
+}
+
+// a content-encoder linear in precision mode `mode` (0 fp16, 1 split-fp16 operands, 2 weight-split)
+template <typename WG, typename BG>
+int pack_linear_mode(svc_ctx* c, PackedGemm& g, int N, int Cin, int mode, WG wget, BG bget) {
+  if (mode == 1) return pack_gemm_split3(c, g, N, Cin, wget, bget);
+  if (mode == 2) return pack_gemm_wsplit2(c, g, N, Cin, wget, bget);
+  return pack_gemm(c, g, N, Cin, Cin, 1, wget, bget);
+}
 
 // Conv1d weight [Cout][Cin][k] (optionally weight-normed along dim 0) into a packed GEMM
 int pack_conv1d(svc_ctx* c, PackedGemm& g, const float* w, const float* bias, int Cout, int Cin, int k, int Cp,
@@ -549,11 +576,11 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   if (!(dmask & 8) && site && strncmp(site, "diffsvc.", 8) == 0) e.no_reg_epi = 1;
   const ConvGemmArgs a = gemm_args(g, X, ldx, Cvalid, B, T_in, T_out, e);
   const bool pair = e.kind == EPI_GATE;
-  // SVC_GEMM_VARIANT: -1 = v1 for plain GEMMs; 0..4 = conv_gemm2 tile; 10..14 = conv_gemm3 tile,
+  // SVC_GEMM_VARIANT: -1 = v1 (gemm.hip) for plain GEMMs; 10..14 = conv_gemm3 tile,
   // 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired epilogue, K = 1152)
   // which runs conv_gemm4 with its register gate epilogue (24; 3-9 % faster than conv_gemm3); 20 = conv_gemm4,
-  // 21 / 22 = conv_gemm5 (conv_gemm4 with a 4- / 5-slot ring of 32-deep K-steps), 24 = conv_gemm4 with its register
-  // epilogues (gate; residual read-modify-write) where the epilogue has that form
+  // 24 = conv_gemm4 with its register epilogues (gate; residual read-modify-write) where the epilogue has that form.
+  // (The round-1 conv_gemm2 tiles and conv_gemm5 ring variants were measured slower and removed.)
   const char* venv = getenv("SVC_GEMM_VARIANT");  // read per call (A/B runs and tests switch it)
   int variant = venv ? atoi(venv) : 15;
   // SVC_GEMM4_RMW=1: the output projection on conv_gemm4's register epilogue too. Alone it is 12 % faster per sampler
@@ -572,11 +599,12 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   }
   if (variant == 15 && pair) variant = (genv && !atoi(genv)) ? 20 : 24;
   if (variant == 15 && renv && atoi(renv) && conv_gemm4_rmw_form(a, e)) variant = 24;
+  SVC_REQUIRE(variant == -1 || (variant >= 10 && variant <= 15) || variant == 20 || variant == 24,
+              "SVC_GEMM_VARIANT %d: -1, 10..15, 20 or 24", variant);
   if (pair || g.N > 64) {
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), s, variant == 24);
-    if (variant == 21 || variant == 22) return conv_gemm5(a, e, zero_page(), variant - 17, s);
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
-    if (pair || variant >= 0) return conv_gemm2(a, e, zero_page(), variant < 0 ? 0 : variant, s);
+    if (pair) return conv_gemm3(a, e, zero_page(), 5, s);  // v1 has no paired epilogue
   }
   return conv_gemm(a, e, s);
 }
@@ -604,7 +632,9 @@ int build_whisper(svc_ctx* c) {
   GETP(c1b, "whisper.encoder.conv1.bias", D);
   GETP(c2w, "whisper.encoder.conv2.weight", D, D, 3);
   GETP(c2b, "whisper.encoder.conv2.bias", D);
-  const bool sp = c->content_split;
+  // precision: the conv stem is split-fp16 in both split modes; the blocks' linears follow content_mode
+  const int mode = c->content_mode;
+  const bool sp = mode != 0;
   SVC_REQUIRE(!sp || nm % 8 == 0, "whisper split precision: n_mels %d", nm);
   int st = pack_conv1d_opt(c, c->wconv1, c1w->host, c1b->host, D, nm, 3, (int)round_up(nm, 8), 1, 1, 1, sp);
   if (st) return st;
@@ -635,12 +665,14 @@ int build_whisper(svc_ctx* c) {
       return w->host[(int64_t)(n % D) * D + ci];
     };
     auto qkv_b = [&](int n) { return n < D ? qb->host[n] : (n < 2 * D ? 0.0f : vb->host[n - 2 * D]); };
-    st = sp ? pack_gemm_split3(c, b.qkv, 3 * D, D, qkv_w, qkv_b) : pack_gemm(c, b.qkv, 3 * D, D, D, 1, qkv_w, qkv_b);
-    if (st) return st;
-    // the attention output (A of `out`) stays fp16: the attention kernel's P.V path is fp16 either way
-    if ((st = pack_conv1d(c, b.out, ow->host, ob->host, D, D, 1, D, 1, 0, 1))) return st;
-    if ((st = pack_conv1d_opt(c, b.fc1, f1w->host, f1b->host, 4 * D, D, 1, D, 1, 0, 1, sp))) return st;
-    if ((st = pack_conv1d_opt(c, b.fc2, f2w->host, f2b->host, D, 4 * D, 1, 4 * D, 1, 0, 1, sp))) return st;
+    auto lin = [&](const Param* w) { return [w](int n, int ci, int) { return w->host[(int64_t)n * (w->shape[1]) + ci]; }; };
+    auto bias = [&](const Param* b0) { return [b0](int n) { return b0->host[n]; }; };
+    if ((st = pack_linear_mode(c, b.qkv, 3 * D, D, mode, qkv_w, qkv_b))) return st;
+    // the attention output (A of `out`) is fp16 (the attention kernel's P.V path is fp16 either way): split3 would
+    // only split the weights, which the weight-split mode does at 2x
+    if ((st = pack_linear_mode(c, b.out, D, D, mode == 2 ? 2 : 0, lin(ow), bias(ob)))) return st;
+    if ((st = pack_linear_mode(c, b.fc1, 4 * D, D, mode, lin(f1w), bias(f1b)))) return st;
+    if ((st = pack_linear_mode(c, b.fc2, D, 4 * D, mode, lin(f2w), bias(f2b)))) return st;
     if ((st = upload_param(c, l1g, &b.ln1_g)) || (st = upload_param(c, l1b, &b.ln1_b)) ||
         (st = upload_param(c, l2g, &b.ln2_g)) || (st = upload_param(c, l2b, &b.ln2_b)))
       return st;
@@ -673,7 +705,7 @@ int build_hubert(svc_ctx* c) {
   c->hconv.assign(7, PackedGemm());
   c->hconv_k = {10, 3, 3, 3, 3, 2, 2};
   c->hconv_s = {5, 2, 2, 2, 2, 2, 2};
-  const bool sp = c->content_split;
+  const bool sp = c->content_mode != 0;  // HuBERT: split-fp16 in both split modes
   if (sp)  // split-fp16 frames rows [hi(5) | lo(5) | hi(5) | 0] against [W_hi | W_hi | W_lo | 0] per tap
     st = pack_gemm(
         c, c->hconv[0], Cc, 16, 16, 2,
@@ -943,8 +975,12 @@ int build_mapper(svc_ctx* c) {
   GETP(spb, q + "skip_projection.bias", C);
   GETP(opw, q + "output_projection.weight", nmel, C, 1);
   GETP(opb, q + "output_projection.bias", nmel);
-  if ((st = pack_conv1d(c, c->skipproj, spw->host, spb->host, C, C, 1, C, 1, 0, 1))) return st;
-  if ((st = pack_conv1d(c, c->outproj, opw->host, opb->host, nmel, C, 1, C, 1, 0, 1))) return st;
+  // The head (skip_projection + output_projection, modules/diffsvc.py:315-319) on split-fp16 operands by default
+  // ("mapper.head_split"): its rounding feeds eps directly and is, after the conditioner projection, the largest
+  // denoiser-side term of the mel-L1 error (precision); 3x the MFMA work of two small K = 384 GEMMs.
+  c->head_split = cfgv(c, "mapper.head_split", 1) != 0;
+  if ((st = pack_conv1d_opt(c, c->skipproj, spw->host, spb->host, C, C, 1, C, 1, 0, 1, c->head_split))) return st;
+  if ((st = pack_conv1d_opt(c, c->outproj, opw->host, opb->host, nmel, C, 1, C, 1, 0, 1, c->head_split))) return st;
 
   // step MLP + per-layer diffusion projections for every step (input-independent: precomputed)
   std::vector<float> dp((size_t)steps * NL * C);
@@ -1237,7 +1273,10 @@ svc_status svc_ctx_finalize(svc_ctx* c) {
     any_m |= kv.first.rfind("mapper.", 0) == 0;
     any_v |= kv.first.rfind("vocoder.", 0) == 0;
   }
-  c->content_split = cfgv(c, "content.split", 0) != 0;
+  c->content_mode = (int)cfgv(c, "content.split", 0);
+  SVC_REQUIRE(c->content_mode >= 0 && c->content_mode <= 2, "content.split %d: 0 fp16, 1 split-fp16, 2 weight-split",
+              c->content_mode);
+  c->content_split = c->content_mode == 1;
   if (any_w && (st = build_whisper(c))) return st;
   if (any_h && (st = build_hubert(c))) return st;
   if (any_m && (st = build_mapper(c))) return st;
@@ -1394,15 +1433,16 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   SVC_REQUIRE(L * 2 == F, "whisper: n_ctx %d != 1500", L);
   const int nb = 201;
   const size_t rows1 = (size_t)B * F, rows2 = (size_t)B * L;
-  const int X3 = c->content_split ? 3 : 1;  // split-fp16 operands are [hi | lo | hi] rows
-  size_t need = rows1 * nb * 4 + rows1 * c->wmels * 4 + rows1 * c->wmels * 2 * X3 + rows1 * D * 2 * X3 /*h1*/ +
+  const int X3 = c->content_split ? 3 : 1;  // split-fp16 block operands are [hi | lo | hi] rows
+  const int XS = c->content_mode != 0 ? 3 : 1;  // the conv stem is split-fp16 in both split modes
+  size_t need = rows1 * nb * 4 + rows1 * c->wmels * 4 + rows1 * c->wmels * 2 * XS + rows1 * D * 2 * XS /*h1*/ +
                 rows2 * D * 4 + rows2 * D * 2 * X3 + rows2 * 3 * D * 2 + rows2 * D * 2 + rows2 * 4 * D * 2 * X3 + 64 * 4096;
   int st;
   if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
   c->ws.reset();
   WS_GET(float, spec, rows1 * nb);
   WS_GET(float, ls, rows1 * c->wmels);
-  WS_GET(f16, lm16, rows1 * c->wmels * X3);
+  WS_GET(f16, lm16, rows1 * c->wmels * XS);
   WS_GET(float, mx, B);
   DftArgs a{};
   a.wav = wav16;
@@ -1419,15 +1459,15 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   a.out = spec;
   if ((st = dft_frames(a, B, s))) return st;
   if ((st = mel_log(spec, nb, c->fb16, c->wmels, ls, (int)rows1, 1, s))) return st;
-  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s, X3 == 3 ? c->wmels : 0))) return st;
+  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s, XS == 3 ? c->wmels : 0))) return st;
   // conv stem
-  WS_GET(f16, h1, rows1 * D * X3);
+  WS_GET(f16, h1, rows1 * D * XS);
   EpiArgs e = epi();
   e.act = ACT_GELU;
   e.out16 = h1;
-  e.ld16 = D * X3;
-  e.split16 = X3 == 3 ? D : 0;
-  if ((st = run_gemm(c->wconv1, lm16, c->wmels * X3, c->wmels * X3, B, F, F, e, s, "whisper.conv1"))) return st;
+  e.ld16 = D * XS;
+  e.split16 = XS == 3 ? D : 0;
+  if ((st = run_gemm(c->wconv1, lm16, c->wmels * XS, c->wmels * XS, B, F, F, e, s, "whisper.conv1"))) return st;
   WS_GET(float, x, rows2 * D);
   e = epi();
   e.act = ACT_GELU;
@@ -1435,7 +1475,7 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   e.ld_add_t = D;
   e.out32 = x;
   e.ld32 = D;
-  if ((st = run_gemm(c->wconv2, h1, D * X3, D * X3, B, F, L, e, s, "whisper.conv2"))) return st;
+  if ((st = run_gemm(c->wconv2, h1, D * XS, D * XS, B, F, L, e, s, "whisper.conv2"))) return st;
   WS_GET(f16, n16, rows2 * D * X3);
   WS_GET(f16, qkv, rows2 * 3 * D);
   WS_GET(f16, o16, rows2 * D);
@@ -1538,7 +1578,7 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
   for (int i = 0; i <= 7; ++i) t[i] = hubert_len(n, i);  // t[0] = n samples, t[7] = frames
   const int Cc = c->hC, D = c->hD, F = (int)F64;
   const int Fd = c->hblocks[0].fc1.N;
-  const bool sp = c->content_split;
+  const bool sp = c->content_mode != 0;  // HuBERT: split-fp16 in both split modes
   const int X3 = sp ? 3 : 1;  // split-fp16 operands are [hi | lo | hi] rows
   const int w5 = sp ? 16 : 8;
   const int64_t R5 = cdiv64(n, 5);
@@ -1682,6 +1722,15 @@ static int condition_impl(svc_ctx* c, const void* content16, const double* f0, c
   return run_gemm(c->content_lin, (const f16*)content16, c->content_dim, c->content_dim, B, T, T, e, s, "cond.content");
 }
 
+svc_status svc_condition_indices(svc_ctx* c, const double* f0, const float* energy, int n, int32_t* melody_idx,
+                                 int32_t* loudness_idx, void* stream) {
+  CTX_READY(c);
+  SVC_REQUIRE(c->has_mapper, "mapper weights not loaded");
+  SVC_REQUIRE(n >= 0 && (n == 0 || (f0 && energy && melody_idx && loudness_idx)), "condition_indices: n %d", n);
+  if (n == 0) return SVC_OK;
+  return bucketize(f0, energy, c->mbins, c->ebins, c->n_bins - 1, melody_idx, loudness_idx, n, (hipStream_t)stream);
+}
+
 svc_status svc_condition(svc_ctx* c, const void* content16, const double* f0, const float* energy,
                          const int32_t* singer, int B, int T, float* cond, void* stream) {
   CTX_READY(c);
@@ -1701,8 +1750,8 @@ struct DenoiseBufs {
   float* h32;    // [rows][C] residual stream (f32: the fused path and SVC_DIFF_RES32=1)
   f16* y16;      // [rows][C] next layer input x + diffusion_projection
   f16* g16;      // [rows][NL*C] gate outputs of every layer (A operand of the skip GEMM)
-  f16* s16;      // [rows][C] sum(skip) / sqrt(NL)
-  f16* u16;      // [rows][C] relu(skip_projection)
+  f16* s16;      // [rows][3C] sum(skip) / sqrt(NL) ([hi | lo | hi] split-fp16 with head_split, else [rows][C])
+  f16* u16;      // [rows][3C] relu(skip_projection), same layout
   f16* lo16;     // [rows][C] low half of the split residual stream: x + dproj = y16 + lo16 (default path)
   size_t cp_ls;  // elements between layers of cp16, which is LAYER-major [NL][rows_total][2C]: each layer's gate
                  // epilogue reads one contiguous block (row-major over all layers put 30 KB between its rows)
@@ -1795,11 +1844,13 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     if ((st = run_gemm(c->outres[i], bb.g16 + (size_t)i * bb.g_ls, C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
   }
   // skip = sum_i skip_i (modules/diffsvc.py:311); x = skip / sqrt(len(layers)) (:315)
+  const int H3 = c->head_split ? 3 : 1;  // split-fp16 head operands are [hi | lo | hi] rows
   e = epi();
   e.scale_cols = C;
   e.col_scale = 1.0f / sqrtf((float)NL);
   e.out16 = bb.s16;
-  e.ld16 = C;
+  e.ld16 = C * H3;
+  e.split16 = H3 == 3 ? C : 0;
   {
     PackedGemm sk = c->skip_all;  // K index l * C + k = "tap" l * Cp + k with Cp = C: same packed weights
     sk.Cp = C;
@@ -1813,13 +1864,14 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e = epi();
   e.act = ACT_RELU;
   e.out16 = bb.u16;
-  e.ld16 = C;
-  if ((st = run_gemm(c->skipproj, bb.s16, C, C, B, T, T, e, s, "diffsvc.skipproj"))) return st;
+  e.ld16 = C * H3;
+  e.split16 = H3 == 3 ? C : 0;
+  if ((st = run_gemm(c->skipproj, bb.s16, C * H3, C * H3, B, T, T, e, s, "diffsvc.skipproj"))) return st;
   e = epi();
   e.out32 = eps;
   e.ld32 = c->n_mel;
   (void)rows;
-  return run_gemm(c->outproj, bb.u16, C, C, B, T, T, e, s, "diffsvc.eps_out");
+  return run_gemm(c->outproj, bb.u16, C * H3, C * H3, B, T, T, e, s, "diffsvc.eps_out");
 }
 
 static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
@@ -1831,8 +1883,8 @@ static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   WS_GET(f16, y16, rows * C);
   WS_GET(f16, y16b, rows * C);
   WS_GET(f16, g16, rows * c->n_layers * C);
-  WS_GET(f16, s16, rows * C);
-  WS_GET(f16, u16, rows * C);
+  WS_GET(f16, s16, rows * C * 3);  // [hi | lo | hi] when head_split
+  WS_GET(f16, u16, rows * C * 3);
   WS_GET(f16, lo16, rows * C);
   bb = DenoiseBufs{cp16, cpF, (int)round_up((int64_t)rows, 64), y16b, h32, y16, g16, s16, u16, lo16, rows * 2 * C,
                    rows * C};
@@ -1842,7 +1894,7 @@ static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
 static size_t denoise_bytes(svc_ctx* c, int B, int T) {
   const size_t rows = (size_t)B * T, C = c->C;
   return rows * c->n_layers * 2 * C * 2 + (fused_layers(c) ? rows + 64 * kMaxSubStreams : 0) * c->n_layers * 2 * C * 2 +
-         rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 5) + 22 * 4096;
+         rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 9) + 22 * 4096;
 }
 
 // fused path: the hoisted conditioner projection of one (sub-)batch -> fragment-major records with the dilated
@@ -1965,7 +2017,7 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
     const int h = (int)(&u - sub);
     const int rp = (int)round_up((int64_t)u.B * T, 64);
     return DenoiseBufs{bb.cp16 + r * 2 * C, bb.cpF + fm_off[h] * NL * 2 * C, rp, bb.y16b + r * C,
-                       bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * C, bb.u16 + r * C,
+                       bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * 3 * C, bb.u16 + r * 3 * C,
                        bb.lo16 + r * C, bb.cp_ls, bb.g_ls};
   };
   for (int h = 0; h < S; ++h)
@@ -2468,9 +2520,8 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   int st = SVC_OK;
   auto run = [&]() {
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
-    if (variant == 21 || variant == 22) return conv_gemm5(a, e, zero_page(), variant - 17, 0);
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, 0);
-    return variant < 0 ? conv_gemm(a, e, 0) : conv_gemm2(a, e, zero_page(), variant, 0);
+    return conv_gemm(a, e, 0);
   };
   for (int w = 0; w < 2 && !st; ++w) st = run();
   SVC_HIP_CHECK(hipEventRecord(e0, 0));

@@ -45,12 +45,16 @@ def check_supported(cfg):
 class SVCEngine:
     """Stages of infer.py on one GPU. `whisper_state`, `mapper_state`, `vocoder_state`, `hubert_state` are dicts
     in the reference's state_dict naming (svc_inference_pipeline_amd.weights; fairseq's for HuBERT); any subset
-    may be given. `hubert_output_layer` is utils/hubert.py:42's output_layer (9). `content_split` runs the
-    Whisper / HuBERT GEMMs on split-fp16 operands ([hi | lo | hi] x [W_hi; W_hi; W_lo], ~19 significand bits, 3x the
-    MFMA work) — the content encoder is the largest term of the mel-L1 error (precision sweep)."""
+    may be given. `hubert_output_layer` is utils/hubert.py:42's output_layer (9). Precision modes (the defaults are
+    the mode the north-star mel-L1 test and bench.py run; DESIGN.md, precision): `content_split` = 0 runs the content
+    encoder on plain fp16 operands; 1 on split-fp16 operands ([hi | lo | hi] x [W_hi; W_hi; W_lo], ~19 significand
+    bits, 3x the MFMA work); 2 (default) splits only the weights of Whisper's block linears ([x | x] x [W_hi; W_lo],
+    2x, no extra activation bytes; the weight rounding is the larger share of their error) with the conv stem and
+    HuBERT as in 1. `head_split` runs the DiffSVC head (skip_projection, output_projection) on split-fp16 operands,
+    the largest denoiser-side term left."""
 
     def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None, hubert_state=None,
-                 hubert_output_layer=9, content_split=False):
+                 hubert_output_layer=9, content_split=2, head_split=True):
         check_supported(cfg)
         _lib.load()
         self.cfg = cfg
@@ -60,7 +64,9 @@ class SVCEngine:
         _lib.call("svc_ctx_create", device, ctypes.byref(self._ctx))
         self._keep = []
         self._set_config()
-        _lib.call("svc_ctx_set_config", self._ctx, b"content.split", 1.0 if content_split else 0.0)
+        # content_split: False / 0 = fp16, True / 1 = split-fp16 operands, 2 = weight-split Whisper linears
+        _lib.call("svc_ctx_set_config", self._ctx, b"content.split", float(int(content_split)))
+        _lib.call("svc_ctx_set_config", self._ctx, b"mapper.head_split", 1.0 if head_split else 0.0)
         if whisper_state is not None:
             self._add_state("whisper.", whisper_state)
             self.whisper_dims = W.whisper_dims_from_state(whisper_state)
@@ -210,6 +216,18 @@ class SVCEngine:
         _lib.call("svc_condition", self._ctx, _ptr(content16), _ptr(f0.contiguous()), _ptr(energy.contiguous()),
                   _ptr(singer), B, T, _ptr(cond), _stream())
         return cond
+
+    def condition_indices(self, f0, energy):
+        """The conditioner's embedding indices (torch.bucketize semantics, modules/encoder.py:70,115):
+        f0 f64 [...], energy f32 [...] -> (melody int32, loudness int32) of the same shape."""
+        f0 = f0.to(torch.float64).contiguous()
+        energy = energy.to(torch.float32).contiguous()
+        assert f0.shape == energy.shape
+        im = torch.empty(f0.shape, dtype=torch.int32, device=f0.device)
+        ie = torch.empty_like(im)
+        _lib.call("svc_condition_indices", self._ctx, _ptr(f0), _ptr(energy), f0.numel(), _ptr(im), _ptr(ie),
+                  _stream())
+        return im, ie
 
     def diffsvc_eps(self, cond, x, t):
         B, T, _ = cond.shape

@@ -1,0 +1,135 @@
+"""GPU parity at the headline configuration (BASELINE.json configs[1]): Whisper-medium content + PLMS-100 DiffSVC +
+BigVGAN, B = 32 x 10 s, in the engine's default precision mode (the one bench.py measures).
+
+- Whisper-medium (1024 wide, 16 heads, 24 layers; utils/whisper_extractor/model.py:132-160) against the oracle.
+- PLMS with speedup 10 (100 iterations, modules/diffsvcrepo_inference.py:216-231) against the reference-generated
+  golden (tests/golden/samplers.npz "plms100").
+- The north-star tolerance: <= 1e-3 mean |delta| of the de-normalised natural-log mel
+  (utils/acoustic_feature_extraction.py:83-97) against the fp32 oracle, on the Whisper-medium path with DDPM-1000 and
+  shared x_T / step noise (PLMS on random weights diverges to |x| ~ 1e2, so its mel is not a meaningful L1 target).
+- The full B = 32 x 10 s conversion: shapes, finiteness, and per-utterance bit-equality with single-clip runs.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from gpu_util import dev, rel_l2  # noqa: E402
+from oracle import features as OF  # noqa: E402
+from oracle import models as OM  # noqa: E402
+from oracle import noise as ON  # noqa: E402
+from oracle import pipeline as OP  # noqa: E402
+from svc_inference_pipeline_amd import config as C  # noqa: E402
+from svc_inference_pipeline_amd import weights as W  # noqa: E402
+from svc_inference_pipeline_amd.pipeline import SVCPipeline  # noqa: E402
+from svc_inference_pipeline_amd.runtime import SVCEngine  # noqa: E402
+
+MEDIUM = W.WHISPER_DIMS["medium"]
+MEL_L1_TARGET = 1e-3   # BASELINE.json north_star: "<= 1e-3 mel-L1 vs the CPU reference"
+
+
+@pytest.fixture(scope="module")
+def cfg():
+    c = C.load_config()
+    c.mapper.input_content_dim["whisper"] = MEDIUM["n_audio_state"]
+    return c
+
+
+@pytest.fixture(scope="module")
+def states(cfg):
+    torch.set_num_threads(16)
+    return dict(whisper=W.make_whisper_state(MEDIUM, 0), mapper=W.make_mapper_state(cfg.mapper, 0),
+                vocoder=W.make_vocoder_state(cfg.vocoder, 0))
+
+
+@pytest.fixture(scope="module")
+def engine(cfg, states):
+    """The production engine, default precision mode (SVCEngine's defaults are bench.py's)."""
+    e = SVCEngine(cfg, 0, whisper_state=states["whisper"], mapper_state=states["mapper"],
+                  vocoder_state=states["vocoder"])
+    yield e
+    e.close()
+
+
+def test_whisper_medium_vs_oracle(engine, states):
+    """A5+A6 at the real dims on a 10 s clip (500 of the 1500 encoder frames carry audio). fp16 MFMA operands with
+    fp32 accumulation over 24 layers: relative L2 <= 2e-3 on the encoder output and on the mapped content."""
+    wav16 = ON.synth_clip_16k_quantised(3, 10.0)
+    feats = engine.whisper_encode(dev(wav16[None]))[0].cpu().numpy()
+    with torch.no_grad():
+        lm = OF.whisper_log_mel(torch.from_numpy(OF.pad_or_trim(wav16))[None])
+        ref = OM.whisper_encoder(states["whisper"], lm, MEDIUM["n_audio_head"])[0].numpy()
+    assert feats.shape == ref.shape == (1500, 1024)
+    assert rel_l2(feats, ref) < 2e-3, rel_l2(feats, ref)
+    T = OF.mel_frames(240000)
+    content = engine.map_content(dev(feats[None]), T)[0].float().cpu().numpy()
+    assert rel_l2(content, OF.map_whisper_features(ref, T)) < 2e-3
+
+
+def test_plms100_vs_golden(engine, golden):
+    """The headline sampler: PLMS speedup 10 = 100 iterations / 101 denoiser calls, against the reference's own
+    svc_model_inference(fast_inference=True, speedup=10) output on the golden conditioning and x_T. Random weights
+    make PLMS diverge (|x| ~ 1e2), so the bound is relative: rel-L2 <= 1e-2 (fp16 operands)."""
+    g = golden("samplers")
+    cond = dev(golden("conditioner_diffsvc")["cond"])
+    x = engine.diffsvc_sample(cond, fast_inference=True, speedup=10, x_T=dev(g["x_T"]))
+    assert rel_l2(x[0].cpu().numpy().T, g["plms100"]) < 1e-2, rel_l2(x[0].cpu().numpy().T, g["plms100"])
+
+
+def _mel_l1(engine, cfg, states, seconds=1.0):
+    """Whisper-medium path, DDPM-1000, shared x_T and step noise: mean |delta| of the de-normalised ln-mel."""
+    stats = C.load_stats(cfg)
+    w24 = ON.synth_clip(7, seconds, 24000).astype(np.float32)
+    w16 = ON.synth_clip_16k_quantised(7, seconds)
+    T = OF.mel_frames(len(w24))
+    f0 = ON.synth_f0(4, T)
+    seed = 17
+    xT = ON.x_T(seed, 1, T)
+    noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
+    res = SVCPipeline(engine).convert(dev(w24[None]), dev(w16[None]), dev(np.array([2]), torch.int32),
+                                      fast_inference=False, x_T=dev(xT), noise=dev(noise),
+                                      f0=dev(f0[None], torch.float64))
+    _, mel_gpu = engine.bigvgan(res.x0, return_mel=True)
+    with torch.no_grad():
+        mel = OF.mel_spectrogram(torch.from_numpy(w24)[None], cfg)
+        en = OF.energy_from_mel(mel)
+        f0s = torch.from_numpy(OF.pitch_shift(f0, stats["target_f0_median"]))[None]
+        content = torch.from_numpy(np.asarray(OP.whisper_content(states["whisper"], w16, T), np.float32))[None]
+        cond = OM.conditioner(states["mapper"], {"whisper": content}, f0s, en, torch.tensor([[2]]))
+        table = W.step_embedding_table(1000)
+        consts = OM.schedule_constants(C.noise_schedule(cfg.mapper))
+        den = lambda x, t: OM.diffsvc_forward(states["mapper"], cfg.mapper, x, cond, t, table)  # noqa: E731
+        x0 = OM.sample_ddpm(den, torch.from_numpy(xT), 1, T, 1000, consts,
+                            lambda i: torch.from_numpy(ON.step_noise(seed, i, 1, T)))
+    ref = OF.denormalize_mel_channel(x0[0].numpy().T, stats["mel_min"], stats["mel_max"])
+    return float(np.mean(np.abs(mel_gpu[0].cpu().numpy().T - ref)))
+
+
+def test_mel_l1_north_star_whisper_medium(engine, cfg, states):
+    """The north-star tolerance on the headline content encoder, in the default precision mode."""
+    l1 = _mel_l1(engine, cfg, states)
+    assert l1 <= MEL_L1_TARGET, l1
+
+
+def test_headline_batch_convert(engine, cfg):
+    """configs[1] through SVCPipeline.convert: B = 32 synthetic 10 s clips, PLMS-100, BigVGAN. Every output is
+    finite and full length, and utterance k is bit-identical to converting clip k alone with the same utterance id
+    (the batch never changes per-utterance arithmetic: sampler sub-batches, GEMM tiles and the vocoder's
+    per-utterance zero padding)."""
+    B = 32
+    uids = np.arange(B)
+    w24 = np.stack([ON.synth_clip(int(u), 10.0, 24000) for u in uids])
+    w16 = np.stack([ON.synth_clip_16k_quantised(int(u), 10.0) for u in uids])
+    singer = dev(uids % 5, torch.int32)
+    pipe = SVCPipeline(engine)
+    res = pipe.convert(dev(w24), dev(w16), singer, fast_inference=True, speedup=10, seed=1234,
+                       utt_ids=dev(uids, torch.int32))
+    T = OF.mel_frames(240000)
+    assert res.wav.shape == (B, T * cfg.hop_length) and res.x0.shape == (B, T, 100)
+    assert bool(torch.isfinite(res.wav).all()) and bool(torch.isfinite(res.x0).all())
+    for k in (0, 13, 31):
+        one = pipe.convert(dev(w24[k:k + 1]), dev(w16[k:k + 1]), singer[k:k + 1], fast_inference=True, speedup=10,
+                           seed=1234, utt_ids=dev(uids[k:k + 1], torch.int32))
+        assert torch.equal(one.x0[0], res.x0[k]), k
+        assert torch.equal(one.wav[0], res.wav[k]), k

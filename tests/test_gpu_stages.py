@@ -134,10 +134,10 @@ def test_fused_layer_vs_oracle(engine, states, cfg, fused, B, T, monkeypatch):
         assert rel_l2(eps, other) < 2e-3
 
 
-@pytest.mark.parametrize("variant", ["20", "24", "21", "rmw", "rmw32"])
+@pytest.mark.parametrize("variant", ["20", "24", "rmw", "rmw32"])
 @pytest.mark.parametrize("B,T", [(3, 50), (2, 700), (5, 937)])
 def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, monkeypatch):
-    """The DiffSVC gate GEMM kernels (LDS-staged and in-register gate epilogues, deep-ring variant) and the register
+    """The DiffSVC gate GEMM kernels (LDS-staged and in-register gate epilogues) and the register
     residual epilogue of the output projection (rmw: split-fp16 residual, rmw32: f32 residual) on ragged row counts
     (B*T not a multiple of the 128-row tile, utterance boundaries inside tiles) against the oracle's eps."""
     rng = np.random.default_rng(B * 7 + T)
@@ -157,7 +157,7 @@ def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, monkeypatch):
     assert rel_l2(eps, ref) < 5e-3
 
 
-@pytest.mark.parametrize("variant", ["1", "3", "10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "21", "22", "24"])
+@pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "24"])
 def test_eps_gemm_variants(engine, golden, variant, monkeypatch):
     """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path); 15lds:
     conv_gemm3 with the LDS-staged epilogue everywhere; 15reg: with every register form, in the sampler too."""
@@ -267,3 +267,76 @@ def test_bigvgan_batch_independence(engine, cfg):
     for b in range(3):
         w1 = engine.bigvgan(dev(x[b:b + 1])).cpu().numpy()[0]
         assert np.array_equal(w1, wb[b])
+
+
+def _adversarial_bucket_inputs(mbins, ebins):
+    """f0 (f64) and energy (f32) values aimed at torch.bucketize's edge cases: every bin edge exactly, one f64 /
+    f32 ulp either side of it, f64 values that round onto an f32 edge, zero and unvoiced f0, energy at and below
+    the 1e-30 first edge and at and above 1.5, subnormals, NaN and infinities, plus random in-range values."""
+    mb = mbins.astype(np.float64)
+    f0 = [mb, np.nextafter(mb, np.inf), np.nextafter(mb, -np.inf),
+          mb + mb * 2.0 ** -30, mb - mb * 2.0 ** -30,  # round onto the f32 edge when narrowed; compare in f64
+          np.array([0.0, -0.0, -1.0, 1e-300, 32.6, 32.603, 2093.005, 2093.0046, 5000.0, 1e300,
+                    np.nan, np.inf, -np.inf])]
+    rng = np.random.default_rng(11)
+    f0.append(np.exp(rng.uniform(np.log(20.0), np.log(3000.0), 4096)))
+    f0 = np.concatenate(f0)
+    eb = ebins.astype(np.float32)
+    en = [eb, np.nextafter(eb, np.float32(np.inf)), np.nextafter(eb, np.float32(-np.inf)),
+          np.array([0.0, -0.0, 1e-30, 9.99e-31, 1e-31, 1e-38, 1e-45, 1.4999999, 1.5, 1.5000001, 2.0, 1e30,
+                    np.nan, np.inf, -np.inf], np.float32)]
+    en.append(np.exp(rng.uniform(np.log(1e-32), np.log(3.0), 4096)).astype(np.float32))
+    en = np.concatenate(en).astype(np.float32)
+    n = max(len(f0), len(en))
+    f0 = np.resize(f0, n)
+    en = np.resize(en, n)
+    return f0, en
+
+
+def test_condition_indices_bit_exact(engine, states):
+    """A10's integer half: the conditioner's melody / loudness indices equal torch.bucketize's (right=False, f64 f0
+    against f32 bins compared in f64, NaN past the last bin) bit for bit on adversarial values
+    (modules/encoder.py:47-57,70 and :93-102,115)."""
+    p = "0.registered_modules_dict."
+    mbins = np.asarray(states["mapper"][p + "melody.melody_bins"], np.float32)
+    ebins = np.asarray(states["mapper"][p + "loudness.energy_bins"], np.float32)
+    f0, en = _adversarial_bucket_inputs(mbins, ebins)
+    im, ie = engine.condition_indices(dev(f0, torch.float64), dev(en))
+    ref_m = torch.bucketize(torch.from_numpy(f0), torch.from_numpy(mbins)).numpy()
+    ref_e = torch.bucketize(torch.from_numpy(en), torch.from_numpy(ebins)).numpy()
+    assert np.array_equal(im.cpu().numpy(), ref_m)
+    assert np.array_equal(ie.cpu().numpy(), ref_e)
+    # the values that sit exactly on an edge land on that edge's index (number of bins < x)
+    assert np.array_equal(ref_m[:len(mbins)], np.arange(len(mbins)))
+    # and the oracle's index rule agrees (it is what the golden-pinned conditioner uses)
+    assert np.array_equal(OM.bucketize_indices(torch.from_numpy(f0), torch.from_numpy(mbins)).numpy(), ref_m)
+
+
+def test_condition_indices_empty_and_shapes(engine):
+    im, ie = engine.condition_indices(dev(np.zeros((0,)), torch.float64), dev(np.zeros((0,))))
+    assert im.numel() == 0 and ie.numel() == 0
+    f0 = np.array([[0.0, 100.0, 440.0], [np.nan, 60.0, 900.0]])
+    en = np.array([[0.0, 0.1, 1.0], [1e-31, 2.0, 0.5]], np.float32)
+    im, ie = engine.condition_indices(dev(f0, torch.float64), dev(en))
+    assert im.shape == (2, 3) and im.dtype == torch.int32
+
+
+def test_ddpm_without_noise_or_utt_ids_is_rejected(engine, golden):
+    """svc_diffsvc_sample in DDPM mode with x_T given but neither step noise nor utterance ids has no key for the
+    device noise: the ABI must return SVC_ERR_INVALID (not read a NULL id table on the device)."""
+    import ctypes
+    from gpu_util import ptr, stream
+    from svc_inference_pipeline_amd import _lib
+    g = golden("samplers")
+    cond = dev(golden("conditioner_diffsvc")["cond"])
+    B, T, _ = cond.shape
+    xT = dev(g["x_T"])
+    x0 = torch.empty(B, T, 100, device="cuda")
+    with pytest.raises(_lib.SVCError, match="utt_ids"):
+        _lib.call("svc_diffsvc_sample", engine._ctx, ptr(cond), B, T, 0, 1, ptr(xT), None, ctypes.c_uint64(0), None,
+                  ptr(x0), stream())
+    # the host wrapper defaults the ids instead, and the run is reproducible
+    a = engine.diffsvc_sample(cond, fast_inference=False, x_T=xT, seed=3).cpu().numpy()
+    b = engine.diffsvc_sample(cond, fast_inference=False, x_T=xT, seed=3,
+                              utt_ids=torch.zeros(B, dtype=torch.int32, device="cuda")).cpu().numpy()
+    assert np.isfinite(a).all() and np.array_equal(a, b)

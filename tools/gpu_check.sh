@@ -11,7 +11,7 @@ if [ -n "$ACT" ]; then
   timeout -k 10 300 python3 tools/act_bench.py > gpurun_out/act_bench.log 2>&1 || exit $?
   grep -v amdgpu.ids gpurun_out/act_bench.log
 fi
-timeout -k 10 300 python3 tools/gemm_bench.py ${VARIANTS:--1 0 1 10 11 12 13 14 15} > gpurun_out/gemm_bench.log 2>&1 || exit $?
+timeout -k 10 300 python3 tools/gemm_bench.py ${VARIANTS:--1 10 11 12 13 14 15 20 24} > gpurun_out/gemm_bench.log 2>&1 || exit $?
 grep -v amdgpu.ids gpurun_out/gemm_bench.log
 if [ -n "$BENCH" ]; then
   # BENCH_ENVS: space-separated "VAR=val,VAR=val" settings, one quick bench each ("-" = defaults)

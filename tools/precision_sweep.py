@@ -1,4 +1,5 @@
-"""BASELINE config 5 tolerance sweep: HuBERT/ContentVec content + DDPM-1000 + BigVGAN, fp16 vs bf16 operands.
+"""mel-L1 tolerance sweep: content encoder (Whisper-medium, the headline, or HuBERT/ContentVec, BASELINE config 5)
++ DDPM-1000 + BigVGAN, fp16 vs bf16 operands, and the HIP path's precision modes.
 
 The reference runs in fp32. The HIP path feeds MFMA with fp16 operands and accumulates in fp32 (DESIGN.md,
 "Dtypes"); bf16 runs at the same gfx950 MFMA rate but keeps 8 instead of 11 significand bits. This tool measures
@@ -13,7 +14,8 @@ per-step noise:
 Metrics, per SURVEY.md §7.3: mel-L1 = mean |delta| of the de-normalised natural-log mel fed to the vocoder (the
 north-star target is <= 1e-3), plus the same in normalised units, the content features' and the waveform's
 relative L2. Random weights (no checkpoints offline) make BigVGAN chaotic, so the waveform figure is
-informational. Usage: python tools/precision_sweep.py [--gpu] [--seconds 1.0] > profiles/<round>_precision_sweep.json
+informational. Usage: python tools/precision_sweep.py [--content whisper|contentvec] [--gpu] [--no-emu] [--no-vocoder]
+[--seconds 1.0] > profiles/<round>_precision_sweep.json
 """
 import argparse
 import json
@@ -39,68 +41,93 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-def oracle_chain(cfg, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats):
+def oracle_chain(cfg, ws, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats, vocoder=True):
+    from oracle import pipeline as OP
     mel = OF.mel_spectrogram(torch.from_numpy(w24)[None], cfg)
     en = OF.energy_from_mel(mel)
     T = mel.shape[-1]
     f0s = torch.from_numpy(OF.pitch_shift(f0, stats["target_f0_median"]))[None]
     with torch.no_grad():
-        hf = OM.hubert_content(hs, torch.from_numpy(w16)[None], 9)[0].numpy()
-        content = torch.from_numpy(OF.map_hubert_features(hf, T).astype(np.float32))[None]
-        cond = OM.conditioner(ms, {"contentvec": content}, f0s, en, torch.tensor([[2]]))
+        if hs is not None:
+            content = OP.hubert_content(hs, w16, T)
+            ctype = "contentvec"
+        else:
+            content = OP.whisper_content(ws, w16, T)
+            ctype = "whisper"
+        content = torch.from_numpy(np.asarray(content, np.float32))[None]
+        cond = OM.conditioner(ms, {ctype: content}, f0s, en, torch.tensor([[2]]))
         table = W.step_embedding_table(1000)
         consts = OM.schedule_constants(C.noise_schedule(cfg.mapper))
         den = lambda x, t: OM.diffsvc_forward(ms, cfg.mapper, x, cond, t, table)  # noqa: E731
         x0 = OM.sample_ddpm(den, torch.from_numpy(xT), 1, T, 1000, consts, noise_fn)
         mel_d = OF.denormalize_mel_channel(x0[0].numpy().T, stats["mel_min"], stats["mel_max"]).astype(np.float32)
-        wav = OM.bigvgan_forward(vs, cfg.vocoder, torch.from_numpy(mel_d)[None])
-        wav = OF.synthesis_fade(wav[0, 0], T).numpy()
+        wav = None
+        if vocoder:
+            wav = OM.bigvgan_forward(vs, cfg.vocoder, torch.from_numpy(mel_d)[None])
+            wav = OF.synthesis_fade(wav[0, 0], T).numpy()
     return dict(content=content[0].numpy(), x0=x0[0].numpy(), mel=mel_d.T, wav=wav)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpu", action="store_true")
+    ap.add_argument("--content", choices=["whisper", "contentvec"], default="contentvec")
+    ap.add_argument("--whisper-dims", default="medium")
+    ap.add_argument("--no-emu", action="store_true", help="skip the fp16 / bf16 operand emulations")
+    ap.add_argument("--no-vocoder", action="store_true", help="mel-L1 only (skip BigVGAN)")
     ap.add_argument("--seconds", type=float, default=1.0)
     ap.add_argument("--threads", type=int, default=16)
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     cfg = C.load_config()
-    cfg.mapper.content_feature = ["contentvec"]
-    cfg.mapper.input_content_dim["contentvec"] = W.HUBERT_DIMS["contentvec"]["final_dim"]
-    hs = W.make_hubert_state(W.HUBERT_DIMS["contentvec"], 0)
+    ws = hs = None
+    if args.content == "contentvec":
+        cfg.mapper.content_feature = ["contentvec"]
+        cfg.mapper.input_content_dim["contentvec"] = W.HUBERT_DIMS["contentvec"]["final_dim"]
+        hs = W.make_hubert_state(W.HUBERT_DIMS["contentvec"], 0)
+        w16 = ON.synth_clip(7, args.seconds, 16000).astype(np.float32)
+    else:
+        dims = W.WHISPER_DIMS[args.whisper_dims]
+        cfg.mapper.input_content_dim["whisper"] = dims["n_audio_state"]
+        ws = W.make_whisper_state(dims, 0)
+        w16 = ON.synth_clip_16k_quantised(7, args.seconds)
     ms = W.make_mapper_state(cfg.mapper, 0)
     vs = W.make_vocoder_state(cfg.vocoder, 0)
     stats = C.load_stats(cfg)
     w24 = ON.synth_clip(7, args.seconds, 24000).astype(np.float32)
-    w16 = ON.synth_clip(7, args.seconds, 16000).astype(np.float32)
     T = OF.mel_frames(len(w24))
     f0 = ON.synth_f0(4, T)
     seed = 17
     xT = ON.x_T(seed, 1, T)
     noise_fn = lambda i: torch.from_numpy(ON.step_noise(seed, i, 1, T))  # noqa: E731
+    voc = not args.no_vocoder
 
     results = {}
     t0 = time.time()
-    ref = oracle_chain(cfg, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats)
+    ref = oracle_chain(cfg, ws, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats, voc)
     timing = {"fp32": round(time.time() - t0, 1)}
     runs = {}
-    for name, dt in (("fp16-emu", torch.float16), ("bf16-emu", torch.bfloat16)):
+    for name, dt in (() if args.no_emu else (("fp16-emu", torch.float16), ("bf16-emu", torch.bfloat16))):
         t0 = time.time()
         with OM.OperandRounding(dt, linear=True):
-            runs[name] = oracle_chain(cfg, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats)
+            runs[name] = oracle_chain(cfg, ws, hs, ms, vs, w24, w16, f0, xT, noise_fn, stats, voc)
         timing[name] = round(time.time() - t0, 1)
     if args.gpu:
         from svc_inference_pipeline_amd.pipeline import SVCPipeline
         from svc_inference_pipeline_amd.runtime import SVCEngine
-        for name, split in (("gpu-fp16", False), ("gpu-fp16, split-fp16 content encoder", True)):
-            e = SVCEngine(cfg, 0, mapper_state=ms, vocoder_state=vs, hubert_state=hs, content_split=split)
+        for name, split, head in (("gpu-fp16", False, False), ("gpu, split-fp16 content encoder", True, False),
+                                  ("gpu, split-fp16 DiffSVC head", False, True),
+                                  ("gpu, split-fp16 content encoder + DiffSVC head (default)", True, True),
+                                  ("gpu, weight-split content linears + split-fp16 DiffSVC head", 2, True)):
+            e = SVCEngine(cfg, 0, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs,
+                          content_split=split, head_split=head)
             d = lambda a, t=torch.float32: torch.as_tensor(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
             noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
             pipe = SVCPipeline(e)
-            content = pipe.content(d(w16[None]), T, d(w16[None])).float().cpu().numpy()[0]
+            w16f = d(w16[None]) if hs is not None else None
+            content = pipe.content(d(w16[None]), T, w16f).float().cpu().numpy()[0]
             res = pipe.convert(d(w24[None]), d(w16[None]), d(np.array([2]), torch.int32), fast_inference=False,
-                               x_T=d(xT), noise=d(noise), f0=d(f0[None], torch.float64), wav16_float=d(w16[None]))
+                               x_T=d(xT), noise=d(noise), f0=d(f0[None], torch.float64), wav16_float=w16f)
             _, mel_d = e.bigvgan(res.x0, return_mel=True)
             runs[name] = dict(content=content, x0=res.x0[0].cpu().numpy(), mel=mel_d[0].cpu().numpy(),
                               wav=res.wav[0].cpu().numpy())
@@ -111,9 +138,10 @@ def main():
             "mel_l1_normalised": float(np.mean(np.abs(r["x0"] - ref["x0"]))),
             "mel_l1_target_1e-3_met": bool(np.mean(np.abs(r["mel"] - ref["mel"])) <= 1e-3),
             "content_rel_l2": rel_l2(r["content"], ref["content"]),
-            "wav_rel_l2": rel_l2(r["wav"], ref["wav"]),
+            "wav_rel_l2": rel_l2(r["wav"], ref["wav"]) if voc else None,
         }
-    print(json.dumps({"config": "BASELINE config 5: ContentVec (layer 9) + DDPM-1000 + BigVGAN, seeded random weights, "
+    enc = ("Whisper-" + args.whisper_dims) if hs is None else "ContentVec (layer 9)"
+    print(json.dumps({"config": f"{enc} + DDPM-1000 + BigVGAN, seeded random weights, "
                                 f"{args.seconds:g} s synthetic clip (T={T}), shared x_T and step noise; reference = "
                                 "fp32 oracle", "cpu_seconds": timing, "results": results}, indent=1))
 
