@@ -1,0 +1,125 @@
+"""GPU parity for BASELINE.json configs[3] and configs[4] at their real dimensions.
+
+configs[3] — one 180 s song (T = 16 875 mel frames) through the headline engine (Whisper-medium). The reference cannot
+run it (utils/whisper.py:52-56 pads / trims to one 30 s window, and the 2812-frame mapped content then fails to
+concatenate in modules/encoder.py:197), so, as in tests/test_gpu_long.py, content parity is per 29.92 s window
+against oracle.pipeline.whisper_content (7 windows), mel / energy / F0 parity is over the whole clip, and the converted
+waveform must be finite and full length.
+
+configs[4] — the HuBERT / ContentVec content encoder (fairseq layer 9 + final_proj, utils/hubert.py:31-47,83-134) at
+the real ContentVec dims with the 1000-step DDPM schedule: the north-star mel-L1 tolerance (<= 1e-3 of the
+de-normalised ln-mel, utils/acoustic_feature_extraction.py:83-97) against the fp32 oracle with shared x_T and step
+noise, in the engine's default precision mode.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from gpu_util import dev, rel_l2  # noqa: E402
+from oracle import features as OF  # noqa: E402
+from oracle import models as OM  # noqa: E402
+from oracle import noise as ON  # noqa: E402
+from oracle import pipeline as OP  # noqa: E402
+from oracle import praat_ac as PA  # noqa: E402
+from svc_inference_pipeline_amd import config as C  # noqa: E402
+from svc_inference_pipeline_amd import weights as W  # noqa: E402
+from svc_inference_pipeline_amd.pipeline import WINDOW_MEL_FRAMES, SVCPipeline  # noqa: E402
+from svc_inference_pipeline_amd.runtime import SVCEngine  # noqa: E402
+
+MEDIUM = W.WHISPER_DIMS["medium"]
+MEL_L1_TARGET = 1e-3
+
+
+@pytest.fixture(scope="module")
+def long_setup():
+    torch.set_num_threads(16)
+    cfg = C.load_config()
+    cfg.mapper.input_content_dim["whisper"] = MEDIUM["n_audio_state"]
+    ws = W.make_whisper_state(MEDIUM, 0)
+    e = SVCEngine(cfg, 0, whisper_state=ws, mapper_state=W.make_mapper_state(cfg.mapper, 0),
+                  vocoder_state=W.make_vocoder_state(cfg.vocoder, 0))
+    wav24 = ON.synth_clip(21, 180.0, 24000)
+    wav16 = ON.synth_clip_16k_quantised(21, 180.0)
+    yield cfg, ws, e, wav24, wav16
+    e.close()
+
+
+def test_config4_180s_content_per_window(long_setup):
+    cfg, ws, e, wav24, wav16 = long_setup
+    T = OF.mel_frames(len(wav24))
+    assert T == 16875
+    n_win = -(-T // WINDOW_MEL_FRAMES)
+    assert n_win == 7
+    content = SVCPipeline(e).content(dev(wav16[None]), T)[0].float().cpu().numpy()
+    with torch.no_grad():
+        ref = OP.whisper_content(ws, wav16, T)
+    assert content.shape == ref.shape == (T, MEDIUM["n_audio_state"])
+    for c in range(n_win):  # the headline encoder's bound (tests/test_gpu_headline.py), per window
+        sl = slice(c * WINDOW_MEL_FRAMES, min(T, (c + 1) * WINDOW_MEL_FRAMES))
+        assert rel_l2(content[sl], ref[sl]) < 2e-3, (c, rel_l2(content[sl], ref[sl]))
+
+
+def test_config4_180s_mel_f0_and_full_length_convert(long_setup):
+    cfg, ws, e, wav24, wav16 = long_setup
+    mel, en = e.mel_energy(dev(wav24[None]))
+    T = mel.shape[1]
+    ref = OF.mel_spectrogram(torch.from_numpy(wav24)[None], cfg)[0].numpy()
+    assert ref.shape[-1] == T  # bit-exact frame count
+    assert np.mean(np.abs(mel[0].cpu().numpy().T - ref)) < 3e-5
+    np.testing.assert_allclose(en[0].cpu().numpy(), OF.energy_from_mel(torch.from_numpy(ref)[None])[0].numpy(),
+                               rtol=2e-5, atol=1e-7)
+    f0 = e.f0(dev(wav24[None]), T)[0].cpu().numpy()
+    f0_ref = PA.f0_features(wav24, T, fs=cfg.fs, hop=cfg.hop_length, floor=cfg.f0_min, ceiling=cfg.f0_max)
+    assert np.array_equal(f0 > 0, f0_ref > 0)
+    rel = np.abs(f0 - f0_ref) / np.maximum(f0_ref, 1.0)
+    assert rel.max() < 1e-5 and np.mean(rel > 2e-7) < 0.01
+    r = SVCPipeline(e).convert(dev(wav24[None]), dev(wav16[None]), dev(np.array([3]), torch.int32), speedup=10,
+                               seed=5)
+    assert r.wav.shape == (1, T * cfg.hop_length) and r.x0.shape == (1, T, 100)
+    assert bool(torch.isfinite(r.wav).all()) and bool(torch.isfinite(r.x0).all())
+
+
+def test_config5_contentvec_ddpm1000_mel_l1():
+    """ContentVec (768 wide, 12 layers used up to output_layer 9, final_proj 256) + DDPM-1000 on a 1 s clip, shared
+    x_T and per-step noise, default precision mode: de-normalised ln-mel L1 <= 1e-3 against the fp32 oracle."""
+    torch.set_num_threads(16)
+    cfg = C.load_config()
+    cfg.mapper.content_feature = ["contentvec"]
+    cfg.mapper.input_content_dim["contentvec"] = W.HUBERT_DIMS["contentvec"]["final_dim"]
+    hs = W.make_hubert_state(W.HUBERT_DIMS["contentvec"], 0)
+    ms = W.make_mapper_state(cfg.mapper, 0)
+    vs = W.make_vocoder_state(cfg.vocoder, 0)
+    stats = C.load_stats(cfg)
+    w24 = ON.synth_clip(7, 1.0, 24000).astype(np.float32)
+    w16 = ON.synth_clip(7, 1.0, 16000).astype(np.float32)
+    T = OF.mel_frames(len(w24))
+    f0 = ON.synth_f0(4, T)
+    seed = 17
+    xT = ON.x_T(seed, 1, T)
+    noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
+    e = SVCEngine(cfg, 0, mapper_state=ms, vocoder_state=vs, hubert_state=hs)
+    try:
+        res = SVCPipeline(e).convert(dev(w24[None]), dev(w16[None]), dev(np.array([2]), torch.int32),
+                                     fast_inference=False, x_T=dev(xT), noise=dev(noise),
+                                     f0=dev(f0[None], torch.float64), wav16_float=dev(w16[None]))
+        _, mel_gpu = e.bigvgan(res.x0, return_mel=True)
+        mel_gpu = mel_gpu[0].cpu().numpy().T
+        assert bool(torch.isfinite(res.wav).all())
+    finally:
+        e.close()
+    with torch.no_grad():
+        mel = OF.mel_spectrogram(torch.from_numpy(w24)[None], cfg)
+        en = OF.energy_from_mel(mel)
+        f0s = torch.from_numpy(OF.pitch_shift(f0, stats["target_f0_median"]))[None]
+        content = torch.from_numpy(np.asarray(OP.hubert_content(hs, w16, T), np.float32))[None]
+        cond = OM.conditioner(ms, {"contentvec": content}, f0s, en, torch.tensor([[2]]))
+        table = W.step_embedding_table(1000)
+        consts = OM.schedule_constants(C.noise_schedule(cfg.mapper))
+        den = lambda x, t: OM.diffsvc_forward(ms, cfg.mapper, x, cond, t, table)  # noqa: E731
+        x0 = OM.sample_ddpm(den, torch.from_numpy(xT), 1, T, 1000, consts,
+                            lambda i: torch.from_numpy(ON.step_noise(seed, i, 1, T)))
+    ref = OF.denormalize_mel_channel(x0[0].numpy().T, stats["mel_min"], stats["mel_max"])
+    l1 = float(np.mean(np.abs(mel_gpu - ref)))
+    assert l1 <= MEL_L1_TARGET, l1
