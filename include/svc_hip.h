@@ -27,6 +27,14 @@
  *     svc_ctx_finalize returns. A missing or mis-shaped parameter makes finalize fail (the reference
  *     silently keeps random init, utils/load_models.py:34-43).
  *   - Status codes instead of exceptions; svc_last_error() describes the last failure of this thread.
+ *   - Ragged batches: a batch holds B utterances of different lengths padded to the longest (rows keep the batch
+ *     stride). The per-utterance lengths are HOST arrays — n_samples (int64 [B], samples) for the 24 kHz feature
+ *     stages, frames (int32 [B], mel frames) for the sampler and the vocoder; NULL means every utterance has the
+ *     batch length. Each utterance is then computed exactly as a clip of its own length (its own reflect / zero /
+ *     replicate padding, STFT frames, Praat frame grid, fade-out): outputs are bit-identical to converting it alone,
+ *     and the rows past its end are written as zeros. Whisper needs no lengths: pad its 16 kHz input with zeros (as
+ *     pad_or_trim does). The tables are staged to the device stream-ordered (a ring of 8 slots per stage group), so
+ *     calls of one entry point must be ordered on one stream.
  */
 #ifndef SVC_HIP_H
 #define SVC_HIP_H
@@ -58,14 +66,16 @@ svc_status svc_ctx_memory(svc_ctx* ctx, int64_t* weight_bytes, int64_t* workspac
 svc_status svc_ctx_stream(svc_ctx* ctx, int index, void** stream);
 
 /* A2/A3-energy: wav24k [B][n_samples] f32 -> mel [B*T][n_mels] f32 (log-mel, time-major), energy [B*T] f32.
-   T = (n_samples + n_fft - hop - n_fft)/hop + 1 (bit-exact frame count, utils/mel.py:148-167). */
-svc_status svc_mel_energy(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, float* mel, float* energy,
-                          void* stream);
+   T = (n_samples + n_fft - hop - n_fft)/hop + 1 (bit-exact frame count, utils/mel.py:148-167).
+   utt_samples (host int64 [B] or NULL): ragged batch, utterance b's samples (<= n_samples); its T_b frames as above. */
+svc_status svc_mel_energy(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, const int64_t* utt_samples,
+                          float* mel, float* energy, void* stream);
 
 /* A3-F0: Praat autocorrelation pitch (to_pitch_ac, voicing 0.6, floor f0_min, ceiling f0_max, time step hop/fs),
    padded to T frames as utils/f0.py:156-157; unvoiced = 0. f0 [B*T] float64. Uses the feature-stage workspace
    (shared with svc_mel_energy only): may run on another stream beside the content-encoder calls. */
-svc_status svc_f0_ac(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, int T, double* f0, void* stream);
+svc_status svc_f0_ac(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, const int64_t* utt_samples, int T,
+                     double* f0, void* stream);
 
 /* A4: in place, f0 [B*T] float64 *= target_median / median(voiced f0 of that utterance)
    (utils/acoustic_feature_extraction.py:33-52; np.median semantics, NaN when no frame is voiced). */
@@ -110,22 +120,26 @@ svc_status svc_condition(svc_ctx* ctx, const void* content_f16, const double* f0
 svc_status svc_condition_indices(svc_ctx* ctx, const double* f0, const float* energy, int n, int32_t* melody_idx,
                                  int32_t* loudness_idx, void* stream);
 
-/* A11+A12: cond f32 [B*T][384] -> x_0 f32 [B*T][n_mel] (normalised mel, time-major).
+/* A11+A12: cond f32 [B*T][384] -> x_0 f32 [B*T][n_mel] (normalised mel, time-major). frames: see Ragged batches.
    mode SVC_MODE_DDPM: `interval` ignored, 1000 steps; SVC_MODE_PLMS: reference speedup (e.g. 10).
    x_T f32 [B*T][n_mel] or NULL (then drawn on device from `seed` and `utt_ids`).
    noise (DDPM only) f32 [steps][B*T][n_mel] (already in time-major order) or NULL (device Philox noise keyed by
    `seed` and `utt_ids`). utt_ids int32 [B] may be NULL only when nothing is drawn on the device: x_T given and,
    for DDPM, `noise` given; otherwise a NULL utt_ids is SVC_ERR_INVALID. */
-svc_status svc_diffsvc_sample(svc_ctx* ctx, const float* cond, int B, int T, int mode, int interval, const float* x_T,
-                              const float* noise, uint64_t seed, const int32_t* utt_ids, float* x0, void* stream);
+svc_status svc_diffsvc_sample(svc_ctx* ctx, const float* cond, int B, int T, const int32_t* frames, int mode,
+                              int interval, const float* x_T, const float* noise, uint64_t seed,
+                              const int32_t* utt_ids, float* x0, void* stream);
 
 /* single epsilon prediction (DiffSVC.forward, modules/diffsvc.py:284-321) for testing: x f32 [B*T][n_mel], step t */
-svc_status svc_diffsvc_eps(svc_ctx* ctx, const float* cond, const float* x, int B, int T, int t, float* eps,
-                           void* stream);
+svc_status svc_diffsvc_eps(svc_ctx* ctx, const float* cond, const float* x, int B, int T, const int32_t* frames, int t,
+                           float* eps, void* stream);
 
 /* A13+A14+A15: x0 f32 [B*T][n_mel] (normalised) -> wav [B][T*256] f32 (denorm, Generator, tanh, fade-out).
+   frames (host int32 [B] or NULL): ragged batch, utterance b's waveform is frames[b]*256 samples (fade-out at its end,
+   zeros after).
    mel_denorm_out (optional, f32 [B*T][n_mel]) receives the de-normalised mel. */
-svc_status svc_bigvgan(svc_ctx* ctx, const float* x0, int B, int T, float* wav, float* mel_denorm_out, void* stream);
+svc_status svc_bigvgan(svc_ctx* ctx, const float* x0, int B, int T, const int32_t* frames, float* wav,
+                       float* mel_denorm_out, void* stream);
 
 /* ---------------- op-level entry points (used by the parity tests; weights are unpacked f32 device arrays) */
 /* y[B*T_out][Cout] = conv1d(x[B*T_in][Cin]) ; w [Cout][Cin][k] ; act 0 none / 1 gelu / 2 relu */

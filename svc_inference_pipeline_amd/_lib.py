@@ -20,8 +20,8 @@ PROTOTYPES = {
     "svc_ctx_finalize": (c_int, [c_void_p]),
     "svc_ctx_memory": (c_int, [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)]),
     "svc_ctx_stream": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),
-    "svc_mel_energy": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p]),
-    "svc_f0_ac": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_int, c_void_p, c_void_p]),
+    "svc_mel_energy": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "svc_f0_ac": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
     "svc_pitch_shift": (c_int, [c_void_p, c_void_p, c_int, c_int, c_double, c_void_p]),
     "svc_whisper_encode": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p]),
     "svc_map_content": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
@@ -31,10 +31,10 @@ PROTOTYPES = {
     "svc_hubert_dims": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "svc_condition": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "svc_condition_indices": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_void_p]),
-    "svc_diffsvc_sample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_uint64,
-                                   c_void_p, c_void_p, c_void_p]),
-    "svc_diffsvc_eps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]),
-    "svc_bigvgan": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "svc_diffsvc_sample": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_void_p, c_void_p,
+                                   c_uint64, c_void_p, c_void_p, c_void_p]),
+    "svc_diffsvc_eps": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+    "svc_bigvgan": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "svc_op_conv1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int,
                               c_int, c_void_p, c_void_p]),
     "svc_op_conv_transpose1d": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
@@ -55,6 +55,8 @@ PROTOTYPES = {
     "svc_mel_filterbank": (c_int, [c_int, c_int, c_int, c_double, c_double, c_void_p]),
 }
 
+ABI_VERSION = 2  # svc_abi_version() of the library these prototypes describe (2: ragged-batch length tables)
+
 _lib = None
 
 
@@ -74,6 +76,8 @@ def load():
         fn = getattr(lib, name)  # AttributeError if an exported symbol is missing
         fn.restype = res
         fn.argtypes = args
+    if lib.svc_abi_version() != ABI_VERSION:
+        raise SVCError(f"{LIB_PATH}: ABI version {lib.svc_abi_version()}, these bindings need {ABI_VERSION} (rebuild)")
     _lib = lib
     return lib
 

@@ -20,7 +20,8 @@ template <int CG>
 __global__ __launch_bounds__(256) void activation1d_v2_kernel(const float* __restrict__ x, f16* __restrict__ y, int L,
                                                               int C, int ldy, const float* __restrict__ alpha_log,
                                                               const float* __restrict__ beta_log,
-                                                              const float* __restrict__ filt) {
+                                                              const float* __restrict__ filt, const int* __restrict__ tv,
+                                                              int tv_mul) {
   constexpr int NL = 256 / CG;  // time lanes
   __shared__ float4 xs[(A2_TT + 12) * CG];
   __shared__ float4 ss[(2 * A2_TT + 12) * CG];
@@ -32,6 +33,9 @@ __global__ __launch_bounds__(256) void activation1d_v2_kernel(const float* __res
   const int b = blockIdx.z;
   const bool cok = c < C;
   const float* xb = x + (int64_t)b * L * C;
+  // ragged batches: the sequence ends at Lb (replicate padding there); rows keep the batch stride L
+  const int Lb = tv ? min(L, tv[b] * tv_mul) : L;
+  if (t0 >= Lb) return;
   float f[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) f[k] = filt[k];
@@ -43,20 +47,20 @@ __global__ __launch_bounds__(256) void activation1d_v2_kernel(const float* __res
   }
   for (int r = tl; r < A2_TT + 12; r += NL) {
     int t = t0 - 6 + r;
-    t = t < 0 ? 0 : (t >= L ? L - 1 : t);
+    t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
     xs[r * CG + g] = cok ? *reinterpret_cast<const float4*>(xb + (int64_t)t * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
   for (int jj = tl; jj < 2 * A2_TT + 12; jj += NL) {
     int j = 2 * t0 - 5 + jj;
-    j = j < 0 ? 0 : (j >= 2 * L ? 2 * L - 1 : j);
+    j = j < 0 ? 0 : (j >= 2 * Lb ? 2 * Lb - 1 : j);
     const int qq = j >> 1;
     const int odd = j & 1;
     float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int a = 0; a < 6; ++a) {
       int xt = qq - 3 + odd + a;
-      xt = xt < 0 ? 0 : (xt >= L ? L - 1 : xt);
+      xt = xt < 0 ? 0 : (xt >= Lb ? Lb - 1 : xt);
       const float w = f[11 - odd - 2 * a];
       const float4 xv = xs[(xt - (t0 - 6)) * CG + g];
       u.x += xv.x * w;
@@ -76,7 +80,7 @@ __global__ __launch_bounds__(256) void activation1d_v2_kernel(const float* __res
   if (!cok) return;
   for (int r = tl; r < A2_TT; r += NL) {
     const int t = t0 + r;
-    if (t >= L) break;
+    if (t >= Lb) break;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
@@ -107,7 +111,8 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
                                                               int B, int L, int C, int ldy,
                                                               const float* __restrict__ alpha_log,
                                                               const float* __restrict__ beta_log,
-                                                              const float* __restrict__ filt) {
+                                                              const float* __restrict__ filt,
+                                                              const int* __restrict__ tv, int tv_mul) {
   static_assert(R % P == 0, "run = whole blocks");
   using V = ActVec<VEC>;
   const int ngroups = C / VEC;
@@ -120,6 +125,9 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
   const int c = g * VEC;
   const float* xb = x + (int64_t)b * L * C + c;
   f16* yb = y + (int64_t)b * L * ldy + c;
+  // ragged batches: this utterance's sequence ends at Lb (replicate padding there); rows keep the stride L
+  const int Lb = tv ? min(L, tv[b] * tv_mul) : L;
+  if (run * R >= Lb) return;
   float f[12];
 #pragma unroll
   for (int k = 0; k < 12; ++k) f[k] = filt[k];
@@ -130,7 +138,7 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
     ib[v] = 1.0f / (expf(beta_log[c + v]) + 0.000000001f);
   }
   auto xload = [&](int t, float* o) {
-    t = t < 0 ? 0 : (t >= L ? L - 1 : t);
+    t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
     V::load(xb + (int64_t)t * C, o);
   };
   auto snake = [&](float* u) {
@@ -158,7 +166,7 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
   };
 
   const int t0 = run * R;
-  const int t_end = t0 + R < L ? t0 + R : L;
+  const int t_end = t0 + R < Lb ? t0 + R : Lb;
   float xw[P + 10][VEC], sw[2 * P + 10][VEC];
 #pragma unroll
   for (int k = 0; k < 10; ++k) xload(t0 - 5 + k, xw[k]);
@@ -167,7 +175,7 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
   // replicate padding of the upsampled signal: s[j] = s[2L-1] past the end, s[0] before the start
 #pragma unroll
   for (int i = 1; i < 10; ++i)
-    if (2 * t0 - 5 + i > 2 * L - 1)
+    if (2 * t0 - 5 + i > 2 * Lb - 1)
 #pragma unroll
       for (int v = 0; v < VEC; ++v) sw[i][v] = sw[i - 1][v];
 #pragma unroll
@@ -180,10 +188,10 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
     for (int k = 0; k < P; ++k) xload(t + 5 + k, xw[10 + k]);
 #pragma unroll
     for (int i = 10; i < 2 * P + 10; ++i) s_win(xw, i, sw[i]);
-    if (2 * t + 2 * P + 4 > 2 * L - 1) {
+    if (2 * t + 2 * P + 4 > 2 * Lb - 1) {
 #pragma unroll
       for (int i = 10; i < 2 * P + 10; ++i)
-        if (2 * t - 5 + i > 2 * L - 1)
+        if (2 * t - 5 + i > 2 * Lb - 1)
 #pragma unroll
           for (int v = 0; v < VEC; ++v) sw[i][v] = sw[i - 1][v];
     }
@@ -213,14 +221,15 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
 
 template <int VEC, int P, int R>
 static void launch_rs(const float* x, f16* y, int B, int L, int C, int ldy, const float* al, const float* bl,
-                      const float* filt, hipStream_t s) {
+                      const float* filt, const int* tv, int tv_mul, hipStream_t s) {
   const int64_t n = (int64_t)B * cdiv(L, R) * (C / VEC);
   hipLaunchKernelGGL((activation1d_rs_kernel<VEC, P, R>), dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, y, B, L,
-                     C, ldy, al, bl, filt);
+                     C, ldy, al, bl, filt, tv, tv_mul);
 }
 
+// tv / tv_mul (optional): ragged batches, utterance b's sequence is min(L, tv[b] * tv_mul) rows long
 int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const float* alpha_log, const float* beta_log,
-                 const float* filt, hipStream_t s) {
+                 const float* filt, hipStream_t s, const int* tv, int tv_mul) {
   SVC_REQUIRE(L >= 1 && C >= 4 && C % 4 == 0 && ldy % 4 == 0, "activation1d: L=%d C=%d ldy=%d", L, C, ldy);
   SVC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "activation1d: alignment");
   const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * (4 + 2), s);
@@ -228,22 +237,22 @@ int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const flo
   const char* venv = getenv("SVC_ACT_VARIANT");
   const int variant = venv ? atoi(venv) : 2;
   if (variant == 1) {
-    launch_rs<4, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
+    launch_rs<4, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   } else if (variant == 2) {
-    launch_rs<2, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
+    launch_rs<2, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   } else if (variant == 3) {
-    launch_rs<4, 4, 64>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
+    launch_rs<4, 4, 64>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   } else if (variant == 4) {
-    launch_rs<1, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, s);
+    launch_rs<1, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   } else if (C % 64 == 0) {
     hipLaunchKernelGGL(activation1d_v2_kernel<16>, dim3(cdiv(L, A2_TT), C / 64, B), dim3(256), 0, s, x, y, L, C, ldy,
-                       alpha_log, beta_log, filt);
+                       alpha_log, beta_log, filt, tv, tv_mul);
   } else if (C % 48 == 0) {
     hipLaunchKernelGGL(activation1d_v2_kernel<12>, dim3(cdiv(L, A2_TT), C / 48, B), dim3(256), 0, s, x, y, L, C, ldy,
-                       alpha_log, beta_log, filt);
+                       alpha_log, beta_log, filt, tv, tv_mul);
   } else {
     hipLaunchKernelGGL(activation1d_v2_kernel<6>, dim3(cdiv(L, A2_TT), cdiv(C, 24), B), dim3(256), 0, s, x, y, L, C,
-                       ldy, alpha_log, beta_log, filt);
+                       ldy, alpha_log, beta_log, filt, tv, tv_mul);
   }
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();

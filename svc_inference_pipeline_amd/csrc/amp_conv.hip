@@ -55,6 +55,10 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
   const int L = p.L;
   const int ntiles = (L + CF::BT - 1) / CF::BT;
   const int b = blockIdx.x / ntiles, t0 = (blockIdx.x - b * ntiles) * CF::BT;
+  // ragged batches: this utterance ends at Lb (activation replicate padding, conv zero padding); the rows keep the
+  // batch stride L. Tiles wholly past Lb have nothing to compute (block-uniform exit before any barrier).
+  const int Lb = p.tv ? min(L, p.tv[b] * p.tv_mul) : L;
+  if (t0 >= Lb) return;
   const int P = (p.k - 1) / 2 * p.d;
   const int rows = CF::BT + 2 * P;
 
@@ -87,7 +91,7 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
         ib[v] = 1.0f / (expf(p.beta_log[c + v]) + 0.000000001f);
       }
       auto xload = [&](int t, float* o) {
-        t = t < 0 ? 0 : (t >= L ? L - 1 : t);
+        t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
         V::load(xb + (int64_t)t * C + c, o);
       };
       auto snake = [&](float* u) {
@@ -100,7 +104,7 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
       };
       // s at the two ends of the up-sampled signal (the low-pass filter's replicate padding uses them); only runs
       // within 6 rows of an utterance end need them (wave-uniform in practice: runs are 32-64 rows)
-      const bool edge = rs - 6 < 0 || re + 6 > L;
+      const bool edge = rs - 6 < 0 || re + 6 > Lb;
       float s0[VEC], sE[VEC];
 #pragma unroll
       for (int v = 0; v < VEC; ++v) s0[v] = sE[v] = 0.f;
@@ -109,7 +113,7 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
       for (int a = 0; a < 6; ++a) {
         float x0[VEC], x1[VEC];
         xload(-3 + a, x0);         // j = 0: even, q = 0
-        xload(L - 3 + a, x1);      // j = 2L-1: odd, q = L-1
+        xload(Lb - 3 + a, x1);     // j = 2Lb-1: odd, q = Lb-1
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
           s0[v] += x0[v] * f[11 - 2 * a];
@@ -134,7 +138,7 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
         snake(o);
         if (edge) {
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) o[v] = j < 0 ? s0[v] : (j > 2 * L - 1 ? sE[v] : o[v]);
+          for (int v = 0; v < VEC; ++v) o[v] = j < 0 ? s0[v] : (j > 2 * Lb - 1 ? sE[v] : o[v]);
         }
       };
       float xw[BLK + 10][VEC], sw[2 * BLK + 10][VEC], xn[BLK][VEC];
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
             float y[VEC];
 #pragma unroll
             for (int v = 0; v < VEC; ++v) y[v] = 0.f;
-            if (row >= 0 && row < L) {
+            if (row >= 0 && row < Lb) {
 #pragma unroll
               for (int kk = 0; kk < 12; ++kk)
 #pragma unroll
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
   }
   // ------------------------------------------------------------------ 3. epilogue in registers: each lane owns 4
   // consecutive channels of one row, so bias / residual / accumulator / outputs move as 16-byte vectors
-  const int nvalid = min(CF::BT, L - t0);
+  const int nvalid = min(CF::BT, Lb - t0);
   const int64_t base = ((int64_t)b * L + t0) * C;
 #pragma unroll
   for (int j = 0; j < CF::FN; ++j) {

@@ -5,6 +5,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
 
 typedef _Float16 f16;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -94,7 +97,15 @@ struct ConvGemmArgs {
   int N;         // valid (packed) output columns
   int ntiles_n;
   int halo;      // conv_gemm3 tap-reuse mode: max |tap shift| (0 = off); set by conv_gemm3 itself
+  // ragged batches: utterance b has min(T_in, tv[b] * tv_mul) valid input rows (NULL = all T_in); rows past it read
+  // as zero, exactly the Conv1d zero padding of a clip of that length (its own rows keep the batch stride T_in)
+  const int* tv;
+  int tv_mul;
 };
+
+__device__ __forceinline__ int valid_in_rows(const ConvGemmArgs& a, int b) {
+  return a.tv ? min(a.T_in, a.tv[b] * a.tv_mul) : a.T_in;
+}
 
 // Epilogue kinds (runtime-selected inside one kernel family)
 enum EpiKind : int {
@@ -133,6 +144,45 @@ struct EpiArgs {
   f16* lo16;
   // host-side launch hint: keep conv_gemm3's LDS-staged epilogue for this call (set by run_gemm, see gemm3.hip)
   int no_reg_epi;
+};
+
+// Per-call host tables (ragged-batch lengths) staged to the device, stream-ordered: a ring of pinned host + device
+// slots, so a table is never rewritten while an earlier copy (or a kernel reading an earlier table) may still be in
+// flight. Each slot's event marks its last copy; a slot is reused only after that copy, kRing calls ago, finished.
+struct StageRing {
+  static constexpr int kRing = 8;
+  void* h[kRing] = {};
+  void* d[kRing] = {};
+  size_t cap[kRing] = {};
+  hipEvent_t ev[kRing] = {};
+  int next = 0;
+  // copies `bytes` from `src` to device memory owned by the ring; *dev receives it
+  int put(const void* src, size_t bytes, hipStream_t s, void** dev) {
+    const int k = next;
+    next = (next + 1) % kRing;
+    if (ev[k]) SVC_HIP_CHECK(hipEventSynchronize(ev[k]));
+    else SVC_HIP_CHECK(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming));
+    if (cap[k] < bytes) {
+      if (h[k]) SVC_HIP_CHECK(hipHostFree(h[k]));
+      if (d[k]) SVC_HIP_CHECK(hipFree(d[k]));
+      const size_t want = std::max<size_t>(bytes, 4096);
+      SVC_HIP_CHECK(hipHostMalloc(&h[k], want, hipHostMallocDefault));
+      SVC_HIP_CHECK(hipMalloc(&d[k], want));
+      cap[k] = want;
+    }
+    memcpy(h[k], src, bytes);
+    SVC_HIP_CHECK(hipMemcpyAsync(d[k], h[k], bytes, hipMemcpyHostToDevice, s));
+    SVC_HIP_CHECK(hipEventRecord(ev[k], s));
+    *dev = d[k];
+    return SVC_OK;
+  }
+  void release() {
+    for (int k = 0; k < kRing; ++k) {
+      if (ev[k]) (void)hipEventSynchronize(ev[k]), (void)hipEventDestroy(ev[k]);
+      if (h[k]) (void)hipHostFree(h[k]);
+      if (d[k]) (void)hipFree(d[k]);
+    }
+  }
 };
 
 int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);

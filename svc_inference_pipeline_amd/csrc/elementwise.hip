@@ -369,7 +369,8 @@ __global__ void ddpm_kernel(float* x, const float* eps, f16* x16, int ld16, int 
     z = a.z[i];
   } else {
     int b = (int)(r / T), t = (int)(r - (int64_t)b * T);
-    z = philox_normal(a.seed, (uint32_t)a.utt_ids[b], (uint32_t)a.step, (uint32_t)(c * T + t));
+    // keyed by (t, c) like x_T, not by c * T + t: an utterance draws the same noise in any batch (ragged or not)
+    z = philox_normal(a.seed, (uint32_t)a.utt_ids[b], (uint32_t)a.step, (uint32_t)(t * C + c));
   }
   float xn = mean + a.sigma * z;
   x[i] = xn;
@@ -387,32 +388,41 @@ int ddpm_update(float* x, const float* eps, f16* x16, int ld16, int B, int T, in
 // ============================================================================ conv_post + tanh + fade
 // modules/bigvgan.py:593,619-620 (Conv1d(ch,1,7,pad 3) + tanh) and modules/bigvgan_inference.py:37-42
 // (trim to T*256 and linear fade-out of the last 20*256 samples). a: f16 [B*L][C], w: f32 [C][7].
+// Ragged batches (tv != NULL): utterance b has Lb = tv[b] * tv_mul samples; its conv zero padding, trim and fade-out
+// are at Lb, and the samples [Lb, L) of its output row are written as zeros.
 __global__ void conv_post_kernel(const f16* __restrict__ a, int lda, int L, int C, const float* __restrict__ w,
-                                 float bias, const float* __restrict__ fade, int nfade, float* __restrict__ out) {
+                                 float bias, const float* __restrict__ fade, int nfade, float* __restrict__ out,
+                                 const int* __restrict__ tv, int tv_mul) {
   __shared__ float ws[96 * 7];
   for (int i = threadIdx.x; i < C * 7; i += blockDim.x) ws[i] = w[i];
   __syncthreads();
   const int b = blockIdx.y;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= L) return;
+  const int Lb = tv ? min(L, tv[b] * tv_mul) : L;
+  if (t >= Lb) {
+    out[(int64_t)b * L + t] = 0.f;
+    return;
+  }
   const f16* ab = a + (int64_t)b * L * lda;
   float acc = 0.f;
   for (int k = 0; k < 7; ++k) {
     int tt = t + k - 3;
-    if (tt < 0 || tt >= L) continue;
+    if (tt < 0 || tt >= Lb) continue;
     const f16* row = ab + (int64_t)tt * lda;
     for (int c = 0; c < C; ++c) acc += (float)row[c] * ws[c * 7 + k];
   }
   float y = tanhf(acc + bias);
-  int fs = L - nfade;
+  int fs = Lb - nfade;
   if (t >= fs) y *= fade[t - fs];
   out[(int64_t)b * L + t] = y;
 }
 
 int conv_post(const f16* a, int lda, int B, int L, int C, const float* w, float bias, const float* fade, int nfade,
-              float* out, hipStream_t s) {
+              float* out, hipStream_t s, const int* tv, int tv_mul) {
   SVC_REQUIRE(C <= 96 && L >= nfade, "conv_post: C=%d L=%d", C, L);
-  hipLaunchKernelGGL(conv_post_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, s, a, lda, L, C, w, bias, fade, nfade, out);
+  hipLaunchKernelGGL(conv_post_kernel, dim3(cdiv(L, 256), B), dim3(256), 0, s, a, lda, L, C, w, bias, fade, nfade, out,
+                     tv, tv_mul);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

@@ -75,7 +75,7 @@ int attention(const f16* qkv, f16* out, int B, int L, int D, hipStream_t s);
 int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int rows, int D, int ldy, hipStream_t s);
 int layernorm_f32(const float* x, const float* g, const float* b, float* y, int rows, int D, int ldy, hipStream_t s);
 int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const float* alpha_log, const float* beta_log,
-                 const float* filt, hipStream_t s);
+                 const float* filt, hipStream_t s, const int* tv = nullptr, int tv_mul = 1);
 int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s);
 int denorm_mel(const float* x, f16* y, float* y32, int ldy, int rows, int C, const float* mn, const float* mx,
                hipStream_t s);
@@ -98,12 +98,14 @@ int ddpm_update(float* x, const float* eps, f16* x16, int ld16, int B, int T, in
 int init_noise(float* x, f16* x16, int ld16, int B, int T, int C, uint64_t seed, const int* utt_ids, float std,
                hipStream_t s);
 int conv_post(const f16* a, int lda, int B, int L, int C, const float* w, float bias, const float* fade, int nfade,
-              float* out, hipStream_t s);
-struct DftArgs {
+              float* out, hipStream_t s, const int* tv = nullptr, int tv_mul = 1);
+struct DftArgs {  // (features.hip)
   const float* wav; int64_t wav_stride; int64_t n_valid; int64_t n_logical;
   int n_fft, hop, pad, n_frames, nbins;
   const float* window; int mode; float* out;
+  const int64_t* nb; const int* Tb;
 };
+int zero_tail_rows(float* x, int B, int T, int C, const int* Tb, hipStream_t s);
 int dft_frames(const DftArgs& a, int B, hipStream_t s);
 int mel_log(const float* spec, int nbins, const float* fb, int n_mels, float* out, int rows, int mode, hipStream_t s);
 int energy_from_mel(const float* mel, int n_mels, float* en, int rows, hipStream_t s);
@@ -142,8 +144,8 @@ int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f
                    hipStream_t s);
 int pack_qkv(const float* q, const float* k, const float* v, f16* qkv, int64_t rows, int D, float scale, hipStream_t s);
 int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double time_step, double floor_hz,
-                double ceiling_hz, double voicing_threshold, int T, double* f0_out, void* workspace, size_t ws_bytes,
-                hipStream_t s);
+                double ceiling_hz, double voicing, int T, double* f0_out, void* workspace, size_t ws_bytes,
+                hipStream_t s, const int64_t* n_b = nullptr, const int* T_b = nullptr, StageRing* ring = nullptr);
 size_t f0_workspace_bytes(int B, int64_t n_samples, double fs, double time_step, double floor_hz);
 
 // ---------------------------------------------------------------------------- host helpers
@@ -257,6 +259,8 @@ using namespace svc;
 
 struct svc_ctx {
   int device = 0;
+  // ragged-batch length tables, one ring per stage (the feature stages run on their own stream)
+  StageRing lens_feat, lens_main;
   std::map<std::string, Param> params;
   std::map<std::string, double> cfg;
   bool finalized = false;
@@ -566,15 +570,18 @@ static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cv
   return a;
 }
 
+// tv / tv_mul: ragged batches, utterance b's valid input rows are tv[b] * tv_mul (ConvGemmArgs::tv; NULL = all)
 int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
-             hipStream_t s, const char* site = "") {
+             hipStream_t s, const char* site = "", const int* tv = nullptr, int tv_mul = 1) {
   prof_site(site);
   // conv_gemm3's register epilogues (SVC_GEMM3_DIRECT mask, gemm3.hip) stay off inside the DiffSVC sampler unless
   // bit 8 is set: there its sub-batch GEMMs run beside the gate GEMMs of the other streams, which then ran slower
   const char* denv = getenv("SVC_GEMM3_DIRECT");
   const int dmask = denv ? atoi(denv) : 3;
   if (!(dmask & 8) && site && strncmp(site, "diffsvc.", 8) == 0) e.no_reg_epi = 1;
-  const ConvGemmArgs a = gemm_args(g, X, ldx, Cvalid, B, T_in, T_out, e);
+  ConvGemmArgs a = gemm_args(g, X, ldx, Cvalid, B, T_in, T_out, e);
+  a.tv = tv;
+  a.tv_mul = tv_mul;
   const bool pair = e.kind == EPI_GATE;
   // SVC_GEMM_VARIANT: -1 = v1 (gemm.hip) for plain GEMMs; 10..14 = conv_gemm3 tile,
   // 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired epilogue, K = 1152)
@@ -1204,7 +1211,8 @@ int build_features(svc_ctx* c) {
 extern "C" {
 
 const char* svc_last_error(void) { return get_error(); }
-int svc_abi_version(void) { return 1; }
+// 2: ragged-batch length tables (utt_samples / frames) in the stage entry points
+int svc_abi_version(void) { return 2; }
 
 svc_status svc_ctx_create(int device, svc_ctx** out) {
   SVC_REQUIRE(out, "svc_ctx_create: null out");
@@ -1230,6 +1238,8 @@ svc_status svc_ctx_destroy(svc_ctx* c) {
     (void)hipEventDestroy(c->ev_join[i]);
   }
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  c->lens_feat.release();
+  c->lens_main.release();
   delete c;
   return SVC_OK;
 }
@@ -1374,13 +1384,52 @@ svc_status svc_mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double
   }
 
 // ---------------------------------------------------------------------------- mel + energy
-svc_status svc_mel_energy(svc_ctx* c, const float* wav, int B, int64_t n, float* mel, float* energy, void* stream) {
+// mel frames of an n-sample clip (utils/mel.py:148-167: reflect pad (n_fft - hop) / 2 each side, center=False)
+static int64_t mel_frames_of(const svc_ctx* c, int64_t n) {
+  const int pad = (c->n_fft - c->hop) / 2;
+  return (n + 2 * pad - c->n_fft) / c->hop + 1;
+}
+
+// ragged batches: validate the per-utterance sample counts (host) and stage them with their mel frame counts
+// (int64 n[B] then int T[B]) to the device through `ring`
+static int stage_samples(svc_ctx* c, StageRing& ring, const int64_t* n_samples, int B, int64_t n, hipStream_t s,
+                         const int64_t** nb_dev, const int** Tb_dev, std::vector<int>* Tb_host) {
+  *nb_dev = nullptr;
+  *Tb_dev = nullptr;
+  if (!n_samples) return SVC_OK;
+  const int pad = (c->n_fft - c->hop) / 2;
+  std::vector<char> buf((size_t)B * (8 + 4));
+  int64_t* nv = reinterpret_cast<int64_t*>(buf.data());
+  int* tv = reinterpret_cast<int*>(buf.data() + (size_t)B * 8);
+  Tb_host->resize(B);
+  for (int b = 0; b < B; ++b) {
+    SVC_REQUIRE(n_samples[b] > pad && n_samples[b] <= n, "utterance %d: %lld samples (batch length %lld)", b,
+                (long long)n_samples[b], (long long)n);
+    nv[b] = n_samples[b];
+    tv[b] = (int)mel_frames_of(c, n_samples[b]);
+    (*Tb_host)[b] = tv[b];
+  }
+  void* dev = nullptr;
+  int st = ring.put(buf.data(), buf.size(), s, &dev);
+  if (st) return st;
+  *nb_dev = reinterpret_cast<const int64_t*>(dev);
+  *Tb_dev = reinterpret_cast<const int*>(reinterpret_cast<char*>(dev) + (size_t)B * 8);
+  return SVC_OK;
+}
+
+svc_status svc_mel_energy(svc_ctx* c, const float* wav, int B, int64_t n, const int64_t* n_samples, float* mel,
+                          float* energy, void* stream) {
   CTX_READY(c);
   hipStream_t s = (hipStream_t)stream;
   const int pad = (c->n_fft - c->hop) / 2;
-  const int64_t T64 = (n + 2 * pad - c->n_fft) / c->hop + 1;
+  const int64_t T64 = mel_frames_of(c, n);
   SVC_REQUIRE(B > 0 && n > pad && T64 > 0 && T64 < (1 << 30), "mel_energy: n=%lld", (long long)n);
   const int T = (int)T64, nb = c->n_fft / 2 + 1;
+  const int64_t* nb_dev;
+  const int* Tb_dev;
+  std::vector<int> Tb_host;
+  int st0 = stage_samples(c, c->lens_feat, n_samples, B, n, s, &nb_dev, &Tb_dev, &Tb_host);
+  if (st0) return st0;
   size_t need = (size_t)B * T * nb * 4 + 4096;
   int st;
   if ((st = c->auxws.reserve(std::max(need, c->auxws.cap)))) return st;
@@ -1400,20 +1449,31 @@ svc_status svc_mel_energy(svc_ctx* c, const float* wav, int B, int64_t n, float*
   a.window = c->win_mel;
   a.mode = 0;
   a.out = spec;
+  a.nb = nb_dev;
+  a.Tb = Tb_dev;
   if ((st = dft_frames(a, B, s))) return st;
   if ((st = mel_log(spec, nb, c->fb24, c->n_mels, mel, B * T, 0, s))) return st;
-  return energy_from_mel(mel, c->n_mels, energy, B * T, s);
+  if ((st = energy_from_mel(mel, c->n_mels, energy, B * T, s))) return st;
+  if (Tb_dev && ((st = zero_tail_rows(mel, B, T, c->n_mels, Tb_dev, s)) || (st = zero_tail_rows(energy, B, T, 1, Tb_dev, s))))
+    return st;
+  return SVC_OK;
 }
 
 // ---------------------------------------------------------------------------- F0
-svc_status svc_f0_ac(svc_ctx* c, const float* wav, int B, int64_t n, int T, double* f0, void* stream) {
+svc_status svc_f0_ac(svc_ctx* c, const float* wav, int B, int64_t n, const int64_t* n_samples, int T, double* f0,
+                     void* stream) {
   CTX_READY(c);
   const double ts = (double)c->hop / c->fs;
   size_t need = f0_workspace_bytes(B, n, c->fs, ts, c->f0_min);
   int st;
   if ((st = c->auxws.reserve(std::max(need + 4096, c->auxws.cap)))) return st;
+  std::vector<int> Tb;
+  if (n_samples) {
+    Tb.resize(B);
+    for (int b = 0; b < B; ++b) Tb[b] = (int)mel_frames_of(c, n_samples[b]);
+  }
   return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->auxws.base, c->auxws.cap,
-                     (hipStream_t)stream);
+                     (hipStream_t)stream, n_samples, n_samples ? Tb.data() : nullptr, &c->lens_feat);
 }
 
 svc_status svc_pitch_shift(svc_ctx* c, double* f0, int B, int T, double target_median, void* stream) {
@@ -1769,7 +1829,9 @@ static bool fused_layers(svc_ctx* c) {
   return (int)c->dl_wd.size() == c->n_layers && v && atoi(v) == 1;
 }
 
-static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s) {
+// tv (device, optional): ragged batches, utterance b has tv[b] valid frames; only the dilated convs look across frames
+static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s,
+                   const int* tv) {
   const int C = c->C, NL = c->n_layers, rows = B * T;
   const int ldx16 = (int)round_up(c->n_mel, 8);
   const float* dp = c->dproj + (size_t)t * NL * C;
@@ -1792,6 +1854,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.add16 = dp;  // layer 0 diffusion projection
   if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
   if (fused_layers(c)) {
+    SVC_REQUIRE(!tv, "the fused residual-layer kernel (SVC_DIFF_FUSED) takes uniform lengths only");
     f16* cur = bb.y16;
     f16* nxt = bb.y16b;
     for (int i = 0; i < NL; ++i) {
@@ -1822,7 +1885,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     g.ld_cp = 2 * C;
     g.y16 = bb.g16 + (size_t)i * bb.g_ls;
     g.ldy16 = C;
-    if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s, "diffsvc.dilated"))) return st;
+    if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s, "diffsvc.dilated", tv, 1))) return st;
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
     // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step)
     EpiArgs r = epi();
@@ -1930,12 +1993,26 @@ static int project_cond(svc_ctx* c, const float* cond, int B, int T, const Denoi
   return SVC_OK;
 }
 
-svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B, int T, int t, float* eps,
-                           void* stream) {
+// ragged batches: validate the per-utterance frame counts (host) and stage them to the device through `ring`
+static int stage_frames(StageRing& ring, const int32_t* frames, int B, int T, hipStream_t s, const int** dev_out) {
+  *dev_out = nullptr;
+  if (!frames) return SVC_OK;
+  for (int b = 0; b < B; ++b)
+    SVC_REQUIRE(frames[b] >= 1 && frames[b] <= T, "utterance %d: %d frames (batch length %d)", b, frames[b], T);
+  void* dev = nullptr;
+  int st = ring.put(frames, (size_t)B * sizeof(int32_t), s, &dev);
+  *dev_out = reinterpret_cast<const int*>(dev);
+  return st;
+}
+
+svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B, int T, const int32_t* frames, int t,
+                           float* eps, void* stream) {
   CTX_READY(c);
   SVC_REQUIRE(c->has_mapper, "mapper weights not loaded");
   SVC_REQUIRE(t >= 0 && t < c->steps, "eps: t=%d", t);
   hipStream_t s = (hipStream_t)stream;
+  const int* tv;
+  if (int st0 = stage_frames(c->lens_main, frames, B, T, s, &tv)) return st0;
   const int rows = B * T, ld16 = (int)round_up(c->n_mel, 8);
   int st;
   if ((st = c->ws.reserve(std::max(denoise_bytes(c, B, T) + (size_t)rows * (ld16 * 2 + c->C * 6) + 8192, c->ws.cap))))
@@ -1947,12 +2024,29 @@ svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B,
   if ((st = fragment_cp(c, bb, rows, s))) return st;
   WS_GET(f16, x16, (size_t)rows * ld16);
   if ((st = f32_to_f16(x, c->n_mel, x16, ld16, rows, c->n_mel, ld16, s))) return st;
-  return denoise(c, bb, x16, B, T, t, eps, s);
+  if ((st = denoise(c, bb, x16, B, T, t, eps, s, tv))) return st;
+  return tv ? zero_tail_rows(eps, B, T, c->n_mel, tv, s) : SVC_OK;
 }
 
-svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int mode, int interval, const float* x_T,
-                              const float* noise, uint64_t seed, const int32_t* utt_ids, float* x0, void* stream) {
+static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* tv, int mode, int interval,
+                       const float* x_T, const float* noise, uint64_t seed, const int32_t* utt_ids, float* x0,
+                       hipStream_t stream);
+
+svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, const int32_t* frames, int mode,
+                              int interval, const float* x_T, const float* noise, uint64_t seed,
+                              const int32_t* utt_ids, float* x0, void* stream) {
   CTX_READY(c);
+  hipStream_t s = (hipStream_t)stream;
+  const int* tv;
+  int st = stage_frames(c->lens_main, frames, B, T, s, &tv);
+  if (st || (st = sample_impl(c, cond, B, T, tv, mode, interval, x_T, noise, seed, utt_ids, x0, s))) return st;
+  // frames past an utterance's end hold no sample: zero them
+  return tv ? zero_tail_rows(x0, B, T, c->n_mel, tv, s) : SVC_OK;
+}
+
+static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* tv, int mode, int interval,
+                       const float* x_T, const float* noise, uint64_t seed, const int32_t* utt_ids, float* x0,
+                       hipStream_t stream) {
   SVC_REQUIRE(c->has_mapper, "mapper weights not loaded");
   SVC_REQUIRE(mode == SVC_MODE_DDPM || (mode == SVC_MODE_PLMS && interval >= 1), "sample: mode %d interval %d", mode,
               interval);
@@ -2038,7 +2132,8 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
       for (int h = 0; h < S; ++h) {
         const Sub& u = sub[h];
         const size_t r = u.r0;
-        if ((st = denoise(c, sub_bufs(u), x16 + r * ld16, u.B, T, i, eps + r * nm, u.s))) return st;
+        if ((st = denoise(c, sub_bufs(u), x16 + r * ld16, u.B, T, i, eps + r * nm, u.s, tv ? tv + u.b0 : nullptr)))
+          return st;
         DdpmArgs a{};
         a.sra = c->sra[i];
         a.srm1 = c->srm1[i];
@@ -2071,7 +2166,7 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
       const int urows = u.B * T;
       const DenoiseBufs ub = sub_bufs(u);
       float* ecur = hist[head] + r * nm;
-      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s))) return st;
+      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr))) return st;
       PlmsArgs p{};
       p.d = d;
       p.A = A;
@@ -2091,7 +2186,7 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
         q.x16 = xp16 + r * ld16;
         if ((st = plms_update(q, urows, nm, u.s))) return st;
         float* eprev = hist[(head + 1) % 5] + r * nm;
-        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s))) return st;
+        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s, tv ? tv + u.b0 : nullptr))) return st;
         p.e[0] = ecur;
         p.e[1] = eprev;
         p.c[0] = 1.0f;
@@ -2135,10 +2230,18 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, int m
 }
 
 // ---------------------------------------------------------------------------- BigVGAN
-svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, float* mel_out, void* stream) {
+svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t* frames, float* wav, float* mel_out,
+                       void* stream) {
   CTX_READY(c);
   SVC_REQUIRE(c->has_vocoder && c->has_mapper, "vocoder (and mapper stats) not loaded");
   hipStream_t s = (hipStream_t)stream;
+  // ragged batches: utterance b has frames[b] mel frames; at a point where the signal is `mul` times the mel rate
+  // its valid length is tv[b] * mul, and every conv / activation / the fade-out ends there
+  const int* tv;
+  if (int st0 = stage_frames(c->lens_main, frames, B, T, s, &tv)) return st0;
+  for (int b = 0; frames && b < B; ++b)
+    SVC_REQUIRE(frames[b] * c->hop_out >= c->nfade, "bigvgan: utterance %d (%d frames) shorter than the fade-out", b,
+                frames[b]);
   const int nm = c->v_in, ldm = (int)round_up(nm, 8);
   int maxLC = 0, Lr = T;  // max over stages of L_i*C_i / T  (6144 for the reference config)
   for (auto& S : c->vstages) {
@@ -2190,17 +2293,23 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
     EpiArgs e = epi();
     e.out16 = pre16 + r * c->v_c0;
     e.ld16 = c->v_c0;
-    if ((st = run_gemm(c->vpre, mel16 + r * ldm, ldm, nm, Bh, T, T, e, ss[h], "bigvgan.conv_pre"))) return st;
+    if ((st = run_gemm(c->vpre, mel16 + r * ldm, ldm, nm, Bh, T, T, e, ss[h], "bigvgan.conv_pre",
+                       tv ? tv + b0[h] : nullptr, 1)))
+      return st;
   }
   int L = T;
+  int mul = 1;  // samples of the current stage per mel frame
   for (int i = 0; i < ns; ++i) {
     VStage& S = c->vstages[i];
     const int Lin = L;
+    const int mul_in = mul;
     L = Lin * S.rate;
+    mul = mul_in * S.rate;
     const int ch = S.cout;
     for (int h = 0; h < NS; ++h) {
       const int Bh = b0[h + 1] - b0[h];
       const hipStream_t sh = ss[h];
+      const int* tvh = tv ? tv + b0[h] : nullptr;
       // each sub-batch owns the fixed region [b0 * T * maxLC, b1 * T * maxLC) of every stage buffer for all
       // stages (offsets that moved with L * C would let a lagging stream's reads overlap another's writes)
       const size_t ro = (size_t)b0[h] * T * maxLC;
@@ -2216,7 +2325,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
         u.ophase = r;
         u.out32 = Xh;
         u.ld32 = ch;
-        if ((st = run_gemm(S.phases[r], in16, S.cin, S.cin, Bh, Lin, Lin, u, sh, "bigvgan.ups"))) return st;
+        if ((st = run_gemm(S.phases[r], in16, S.cin, S.cin, Bh, Lin, Lin, u, sh, "bigvgan.ups", tvh, mul_in))) return st;
       }
       const int nk = (int)S.c1.size();
       for (int j = 0; j < nk; ++j) {
@@ -2240,15 +2349,18 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
             e1.ld32 = ch;
             if (fuse) {
               const PackedGemm& g1 = S.c1[j][l];
-              const AmpConvArgs p1{src, Bh, L, S.rk[j], S.rd[j][l], a1.alpha, a1.beta, a1.filt, g1.W, g1.Kpad, g1.bias};
+              AmpConvArgs p1{src, Bh, L, S.rk[j], S.rd[j][l], a1.alpha, a1.beta, a1.filt, g1.W, g1.Kpad, g1.bias};
+              p1.tv = tvh;
+              p1.tv_mul = mul;
               prof_site("bigvgan.amp_c1");
               if ((st = amp_conv(p1, ch, e1, sh))) return st;
             } else {
-              if ((st = activation1d(src, a16h, Bh, L, ch, ch, a1.alpha, a1.beta, a1.filt, sh))) return st;
-              if ((st = run_gemm(S.c1[j][l], a16h, ch, ch, Bh, L, L, e1, sh, "bigvgan.amp_c1"))) return st;
+              if ((st = activation1d(src, a16h, Bh, L, ch, ch, a1.alpha, a1.beta, a1.filt, sh, tvh, mul))) return st;
+              if ((st = run_gemm(S.c1[j][l], a16h, ch, ch, Bh, L, L, e1, sh, "bigvgan.amp_c1", tvh, mul))) return st;
             }
           }
-          if (!fuse && (st = activation1d(act_in, a16h, Bh, L, ch, ch, a2.alpha, a2.beta, a2.filt, sh))) return st;
+          if (!fuse && (st = activation1d(act_in, a16h, Bh, L, ch, ch, a2.alpha, a2.beta, a2.filt, sh, tvh, mul)))
+            return st;
           EpiArgs e2 = epi();
           e2.add_row = src;
           e2.ld_add_row = ch;
@@ -2277,10 +2389,12 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
           }
           if (fuse) {
             const PackedGemm& g2 = S.c2[j][l];
-            const AmpConvArgs p2{act_in, Bh, L, S.rk[j], d2, a2.alpha, a2.beta, a2.filt, g2.W, g2.Kpad, g2.bias};
+            AmpConvArgs p2{act_in, Bh, L, S.rk[j], d2, a2.alpha, a2.beta, a2.filt, g2.W, g2.Kpad, g2.bias};
+            p2.tv = tvh;
+            p2.tv_mul = mul;
             prof_site("bigvgan.amp_c2");
             if ((st = amp_conv(p2, ch, e2, sh))) return st;
-          } else if ((st = run_gemm(S.c2[j][l], a16h, ch, ch, Bh, L, L, e2, sh, "bigvgan.amp_c2"))) {
+          } else if ((st = run_gemm(S.c2[j][l], a16h, ch, ch, Bh, L, L, e2, sh, "bigvgan.amp_c2", tvh, mul))) {
             return st;
           }
         }
@@ -2292,18 +2406,19 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, float* wav, fl
   for (int h = 0; h < NS; ++h) {
     const int Bh = b0[h + 1] - b0[h];
     const size_t ro = (size_t)b0[h] * T * maxLC;
+    const int* tvh = tv ? tv + b0[h] : nullptr;
     if ((st = activation1d(XS + ro, a16 + ro, Bh, L, chl, chl, c->vact_post.alpha, c->vact_post.beta,
-                           c->vact_post.filt, ss[h])))
+                           c->vact_post.filt, ss[h], tvh, mul)))
       return st;
     if ((st = conv_post(a16 + ro, chl, Bh, L, chl, c->vpost_w, c->vpost_b, c->fade, c->nfade,
-                        wav + (size_t)b0[h] * L, ss[h])))
+                        wav + (size_t)b0[h] * L, ss[h], tvh, mul)))
       return st;
     if (NS > 1) {
       SVC_HIP_CHECK(hipEventRecord(c->ev_join[h], ss[h]));
       SVC_HIP_CHECK(hipStreamWaitEvent(s, c->ev_join[h], 0));
     }
   }
-  return SVC_OK;
+  return (tv && mel_out) ? zero_tail_rows(mel_out, B, T, nm, tv, s) : SVC_OK;
 }
 
 // ---------------------------------------------------------------------------- op-level (tests)

@@ -13,6 +13,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "common.h"
 
@@ -190,9 +191,22 @@ __device__ double brent_neg_sinc(SINC sinc, const double* y, int n, int depth, d
   return x;
 }
 
+// Ragged batches: per-utterance sound length and the frame grid it implies (f0_params of that length), set by the
+// host; NULL = every utterance has the batch length (the uniform P). Rows keep the batch stride (n_max samples,
+// nf_max frames, T_max output frames).
+struct F0Utt {
+  int64_t n;  // samples
+  double t1;  // first frame time
+  int nf;     // frames
+  int pad;    // left zero padding of the mel-length output (utils/f0.py:156-157)
+  int T;      // mel frames of this utterance
+};
+
 // ---------------------------------------------------------------------------- kernels
-__global__ void f0_global_kernel(const float* __restrict__ wav, int64_t n, double* __restrict__ gpeak) {
-  const float* x = wav + (int64_t)blockIdx.x * n;
+__global__ void f0_global_kernel(const float* __restrict__ wav, int64_t stride, const F0Utt* __restrict__ utt,
+                                 double* __restrict__ gpeak) {
+  const float* x = wav + (int64_t)blockIdx.x * stride;
+  const int64_t n = utt ? utt[blockIdx.x].n : stride;
   __shared__ double red[16];
   double s = 0;
   for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += (double)x[i];
@@ -267,7 +281,8 @@ struct F0Out {
 
 __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__ wav, int64_t n, F0Params P,
                                                        const double* __restrict__ win, const double* __restrict__ winR,
-                                                       const double* __restrict__ gpeak, F0Out o) {
+                                                       const double* __restrict__ gpeak, F0Out o,
+                                                       const F0Utt* __restrict__ utt) {
   extern __shared__ double sm[];
   double* frame = sm;               // [nw]
   double* r = frame + P.nw;         // [2*bmax+1], lag L at r[L + bmax]
@@ -278,8 +293,9 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
   __shared__ int cim[F0_MAXC];
   __shared__ int ncs;
   const int fi = blockIdx.x, b = blockIdx.y;
+  if (utt && fi >= utt[b].nf) return;  // past this utterance's frames (block-uniform, before any barrier)
   const float* x = wav + (int64_t)b * n;
-  const double t = P.t1 + fi * P.ts;
+  const double t = (utt ? utt[b].t1 : P.t1) + fi * P.ts;
   const int left = (int)floor((t - P.x1) / P.dx) + 1;  // 1-based
   const int right = left + 1;
   // local mean: 1-based samples [right - nsp, left + nsp]
@@ -413,9 +429,16 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
 // ps_lds: the back-pointers of all frames fit in dynamic LDS as bytes (nf * F0_MAXC bytes), so the final serial
 // backtrack chases LDS instead of global memory; otherwise they go to psi (global).
 __global__ void f0_path_kernel(F0Params P, F0Out o, int* __restrict__ psi, int T, int pad, double* __restrict__ f0out,
-                               int ps_lds) {
+                               int ps_lds, const F0Utt* __restrict__ utt) {
   extern __shared__ unsigned char psl[];
   const int b = blockIdx.x;
+  // frame-array stride is the batch's P.nf; this utterance's own frame count / padding / length come from utt
+  const int nf_stride = P.nf;
+  const int Tb = utt ? utt[b].T : T;
+  if (utt) {
+    P.nf = utt[b].nf;
+    pad = utt[b].pad;
+  }
   const int j = threadIdx.x;
   const int jc = threadIdx.x >> 4, kk = threadIdx.x & 15;  // blockDim = 16 * F0_MAXC... at least F0_MAXC x 16
   // The Viterbi recursion is serial over frames, so each step must not wait on global memory: the candidates of
@@ -430,9 +453,9 @@ __global__ void f0_path_kernel(F0Params P, F0Out o, int* __restrict__ psi, int T
   const double tsc = 0.01 / P.ts;
   const double ojc = P.octave_jump * tsc, vuv = P.vuv_cost * tsc;
   const double ceil2 = P.ceiling;
-  int* ps = psi + (int64_t)b * P.nf * F0_MAXC;
+  int* ps = psi + (int64_t)b * nf_stride * F0_MAXC;
   for (int i = 0; i < P.nf; ++i) {
-    const int gf = b * P.nf + i;
+    const int gf = b * nf_stride + i;
     const int li = i % F0_PCH;
     if (li == 0) {
       __syncthreads();
@@ -500,7 +523,7 @@ __global__ void f0_path_kernel(F0Params P, F0Out o, int* __restrict__ psi, int T
   if (j == 0) {
     double* out = f0out + (int64_t)b * T;
     for (int t = 0; t < T; ++t) out[t] = 0.0;
-    const int gl = b * P.nf + P.nf - 1;
+    const int gl = b * nf_stride + P.nf - 1;
     int place = 0;
     double best = dprev[0];
     for (int kk = 1; kk < o.ncand[gl]; ++kk)
@@ -509,9 +532,9 @@ __global__ void f0_path_kernel(F0Params P, F0Out o, int* __restrict__ psi, int T
         place = kk;
       }
     for (int i = P.nf - 1; i >= 0; --i) {
-      const int gf = b * P.nf + i;
+      const int gf = b * nf_stride + i;
       const int t = pad + i;
-      if (t >= 0 && t < T) out[t] = o.freq[(int64_t)gf * F0_MAXC + place];
+      if (t >= 0 && t < Tb) out[t] = o.freq[(int64_t)gf * F0_MAXC + place];
       place = i > 0 ? (ps_lds ? (int)psl[i * F0_MAXC + place] : ps[(int64_t)i * F0_MAXC + place]) : 0;
     }
   }
@@ -524,10 +547,36 @@ size_t f0_workspace_bytes(int B, int64_t n, double fs, double ts, double floor_h
   return nf * F0_MAXC * (8 + 8 + 4) + nf * (4 + 8) + (size_t)B * 8 + (size_t)(P.nw + P.bmax + 2) * 8 + 8 * 4096;
 }
 
+// n_b (host, [B], optional): ragged batches, utterance b has n_b[b] <= n samples and T_b[b] <= T mel frames; its F0
+// is computed on its own samples exactly as a clip of that length, and written zero past T_b[b]. The per-utterance
+// frame grids are staged to the device through `ring`.
 int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double floor_hz, double ceiling_hz,
-                double voicing, int T, double* f0_out, void* workspace, size_t ws_bytes, hipStream_t s) {
+                double voicing, int T, double* f0_out, void* workspace, size_t ws_bytes, hipStream_t s,
+                const int64_t* n_b, const int* T_b, StageRing* ring) {
   F0Params P = f0_params(n, fs, ts, floor_hz, ceiling_hz);
   SVC_REQUIRE(P.nf >= 1, "f0: sound (%lld samples) shorter than the 3-period window", (long long)n);
+  const int hop = (int)llround(ts * fs);
+  // utils/f0.py:156-157: pad = (len(audio)//hop - len(f0) + 1)//2 (python floor division)
+  auto pad_of = [&](int64_t nn, int nf) {
+    const int64_t num = nn / hop - nf + 1;
+    return (int)(num >= 0 ? num / 2 : -((-num + 1) / 2));
+  };
+  const F0Utt* utt = nullptr;
+  if (n_b) {
+    std::vector<F0Utt> u((size_t)B);
+    for (int b = 0; b < B; ++b) {
+      SVC_REQUIRE(n_b[b] >= 1 && n_b[b] <= n && T_b[b] >= 1 && T_b[b] <= T, "f0: utterance %d: %lld samples", b,
+                  (long long)n_b[b]);
+      const F0Params Pb = f0_params(n_b[b], fs, ts, floor_hz, ceiling_hz);
+      SVC_REQUIRE(Pb.nf >= 1, "f0: utterance %d (%lld samples) shorter than the 3-period window", b,
+                  (long long)n_b[b]);
+      u[b] = F0Utt{n_b[b], Pb.t1, Pb.nf, pad_of(n_b[b], Pb.nf), T_b[b]};
+    }
+    void* dev = nullptr;
+    int st = ring->put(u.data(), u.size() * sizeof(F0Utt), s, &dev);
+    if (st) return st;
+    utt = (const F0Utt*)dev;
+  }
   SVC_REQUIRE(P.nw <= 2048 && P.maxc <= F0_MAXC, "f0: window %d / candidates %d too large", P.nw, P.maxc);
   P.voicing = voicing;
   if (const char* dbg = getenv("SVC_F0_DBG")) P.dbg = atoi(dbg);
@@ -552,20 +601,17 @@ int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double
   double* gpeak = (double*)take((size_t)B * 8);
   double* win = (double*)take((size_t)P.nw * 8);
   double* winR = (double*)take((size_t)(P.bmax + 1) * 8);
-  hipLaunchKernelGGL(f0_global_kernel, dim3(B), dim3(1024), 0, s, wav, n, gpeak);
+  hipLaunchKernelGGL(f0_global_kernel, dim3(B), dim3(1024), 0, s, wav, n, utt, gpeak);
   SVC_LAUNCH_CHECK();
   hipLaunchKernelGGL(f0_window_kernel, dim3(1), dim3(256), 0, s, P.nw, P.bmax, win, winR);
   SVC_LAUNCH_CHECK();
   const size_t lds = (size_t)(P.nw + 2 * P.bmax + 1 + 8 + 2 * (P.bmax + 1)) * sizeof(double);
-  hipLaunchKernelGGL(f0_frame_kernel, dim3(P.nf, B), dim3(256), lds, s, wav, n, P, win, winR, gpeak, o);
+  hipLaunchKernelGGL(f0_frame_kernel, dim3(P.nf, B), dim3(256), lds, s, wav, n, P, win, winR, gpeak, o, utt);
   SVC_LAUNCH_CHECK();
-  // utils/f0.py:156-157: pad = (len(audio)//hop - len(f0) + 1)//2 (python floor division)
-  const int hop = (int)llround(ts * fs);
-  const int64_t num = n / hop - P.nf + 1;
-  const int pad = (int)(num >= 0 ? num / 2 : -((-num + 1) / 2));
+  const int pad = pad_of(n, P.nf);
   const int ps_lds = (size_t)P.nf * F0_MAXC <= 32768 ? 1 : 0;  // 10 s: 934 frames -> 15 KB
   hipLaunchKernelGGL(f0_path_kernel, dim3(B), dim3(16 * F0_MAXC), ps_lds ? (size_t)P.nf * F0_MAXC : 0, s, P, o, psi, T,
-                     pad, f0_out, ps_lds);
+                     pad, f0_out, ps_lds, utt);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

@@ -18,6 +18,9 @@ struct DftArgs {
   const float* window;  // [n_fft]
   int mode;             // 0: sqrt(|X|^2 + 1e-9) ; 1: |X|^2
   float* out;           // [B*n_frames][nbins]
+  // ragged batches (optional): utterance b has nb[b] samples (its n_valid and n_logical) and Tb[b] frames
+  const int64_t* nb;
+  const int* Tb;
 };
 
 __global__ __launch_bounds__(256) void dft_kernel(DftArgs a) {
@@ -28,6 +31,9 @@ __global__ __launch_bounds__(256) void dft_kernel(DftArgs a) {
   const int f0 = blockIdx.y * DFT_FR;
   const int b = blockIdx.z;
   const float* w = a.wav + (int64_t)b * a.wav_stride;
+  const int64_t n_valid = a.nb ? a.nb[b] : a.n_valid, n_logical = a.nb ? a.nb[b] : a.n_logical;
+  const int n_frames = a.Tb ? min(a.n_frames, a.Tb[b]) : a.n_frames;
+  if (f0 >= n_frames) return;  // block-uniform, before any barrier (zero_tail_rows clears those rows' outputs)
   for (int i = threadIdx.x; i < a.n_fft; i += blockDim.x) {
     double s, c;
     sincospi(2.0 * (double)i / (double)a.n_fft, &s, &c);
@@ -38,11 +44,11 @@ __global__ __launch_bounds__(256) void dft_kernel(DftArgs a) {
     int fr = i / a.n_fft, j = i - fr * a.n_fft;
     int f = f0 + fr;
     float v = 0.f;
-    if (f < a.n_frames) {
+    if (f < n_frames) {
       int64_t idx = (int64_t)f * a.hop + j - a.pad;
       if (idx < 0) idx = -idx;
-      if (idx >= a.n_logical) idx = 2 * (a.n_logical - 1) - idx;
-      v = idx < a.n_valid ? w[idx] : 0.f;
+      if (idx >= n_logical) idx = 2 * (n_logical - 1) - idx;
+      v = idx < n_valid ? w[idx] : 0.f;
       v = v * a.window[j];
     }
     xs[i] = v;
@@ -68,7 +74,7 @@ __global__ __launch_bounds__(256) void dft_kernel(DftArgs a) {
 #pragma unroll
   for (int fr = 0; fr < DFT_FR; ++fr) {
     const int f = f0 + fr;
-    if (f >= a.n_frames) break;
+    if (f >= n_frames) break;
     const float r = (float)re[fr], i = (float)im[fr];
     float v;
     if (a.mode == 0) {
@@ -86,6 +92,23 @@ int dft_frames(const DftArgs& a, int B, hipStream_t s) {
   size_t lds = (size_t)a.n_fft * 2 * sizeof(double) + (size_t)DFT_FR * a.n_fft * sizeof(float);
   dim3 grid(cdiv(a.nbins, 256), cdiv(a.n_frames, DFT_FR), B);
   hipLaunchKernelGGL(dft_kernel, grid, dim3(256), lds, s, a);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+// ragged batches: rows t >= Tb[b] of a [B][T][C] f32 tensor are set to zero (the frames a clip of that length
+// does not have)
+__global__ void zero_tail_kernel(float* __restrict__ x, int T, int C, const int* __restrict__ Tb) {
+  const int b = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int t0 = Tb[b];
+  const int64_t n = (int64_t)(T - t0) * C;
+  if (t0 >= T || i >= n) return;
+  x[((int64_t)b * T + t0) * C + i] = 0.f;
+}
+
+int zero_tail_rows(float* x, int B, int T, int C, const int* Tb, hipStream_t s) {
+  hipLaunchKernelGGL(zero_tail_kernel, dim3(cdiv((int64_t)T * C, 256), B), dim3(256), 0, s, x, T, C, Tb);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
 
   // ---- per-thread A rows (fixed over the K loop)
   const int kv = tid & 7;
-  int a_base[CF::AV], a_tt[CF::AV];
+  int a_base[CF::AV], a_tt[CF::AV], a_tin[CF::AV];
 #pragma unroll
   for (int i = 0; i < CF::AV; ++i) {
     int rr = (tid >> 3) + 32 * i;
@@ -67,9 +67,11 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
       int t = m - b * a.T_out;
       a_base[i] = b * a.T_in;
       a_tt[i] = t * a.istride;
+      a_tin[i] = valid_in_rows(a, b);
     } else {
       a_base[i] = 0;
       a_tt[i] = -(1 << 29);  // never valid
+      a_tin[i] = 0;
     }
   }
 
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(256, 2) void conv_gemm_kernel(ConvGemmArgs a, EpiAr
     for (int i = 0; i < CF::AV; ++i) {
       int st = a_tt[i] + off;
       uint4 v = make_uint4(0, 0, 0, 0);
-      if (kin && st >= 0 && st < a.T_in) {
+      if (kin && st >= 0 && st < a_tin[i]) {
         const f16* p = a.X + (int64_t)(a_base[i] + st) * a.ldx + c;
         if (c + 8 <= a.Cvalid) {
           v = *reinterpret_cast<const uint4*>(p);

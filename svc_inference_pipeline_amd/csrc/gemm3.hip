@@ -108,7 +108,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
 
   // ---- DMA slots. A half h, instruction v: image rows rb .. rb+7, lane -> row rb + (lane >> 3),
   // LDS chunk lane & 7 holding logical k-chunk kv = sw3(row, lane & 7).
-  int a_rb[2][CF::AH], a_kv[2][CF::AH], a_t[2][CF::AH];
+  int a_rb[2][CF::AH], a_kv[2][CF::AH], a_t[2][CF::AH], a_tin[2][CF::AH];
   const f16* a_p[2][CF::AH];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
@@ -124,9 +124,11 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
       if (m < M) {
         const int b = m / a.T_out, t = m - b * a.T_out;
         a_t[h][v] = t * a.istride;
+        a_tin[h][v] = valid_in_rows(a, b);
         a_p[h][v] = a.X + (int64_t)b * a.T_in * a.ldx + kv * 8;
       } else {
         a_t[h][v] = -(1 << 29);
+        a_tin[h][v] = 0;
         a_p[h][v] = a.X;
       }
     }
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
 #pragma unroll
       for (int v = 0; v < CF::AH; ++v) {
         const int st = a_t[h][v] + shift;
-        const bool ok = kt < nk && st >= 0 && st < a.T_in;
+        const bool ok = kt < nk && st >= 0 && st < a_tin[h][v];
         const f16* src = ok ? a_p[h][v] + (int64_t)a_t[h][v] * a.ldx + off : zsrc;
         g3_dma(src, dst + a_rb[h][v] * 128);
       }
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
         if (tap * a.Cp > kg) --tap;
         const int c = kg - tap * a.Cp;
         const int st = a_t[h][v] + tap * a.tap_mul + a.tap_add;
-        const bool ok = kt < nk && kg < a.K && st >= 0 && st < a.T_in;
+        const bool ok = kt < nk && kg < a.K && st >= 0 && st < a_tin[h][v];
         // a_p already carries the lane's kv * 8 column offset: add the tap-local column base only
         const f16* src = ok ? a_p[h][v] + (int64_t)st * a.ldx + (c - a_kv[h][v] * 8) : zsrc;
         g3_dma(src, dst + a_rb[h][v] * 128);
@@ -495,7 +497,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
 // bound by the L2 -> LDS byte rate; kept, parity-tested, for the next schedule revision.
 static int halo_of(const ConvGemmArgs& a) {
   const char* v = getenv("SVC_GEMM_HALO");  // read per call (A/B runs and tests switch it)
-  if (!(v && atoi(v) == 1)) return 0;
+  if (!(v && atoi(v) == 1) || a.tv) return 0;  // (the halo image masks by the uniform T_in only)
   const int taps = a.Cp > 0 ? a.K / a.Cp : 0;
   if (!(a.Cp % 64 == 0 && a.K == a.Kpad && taps >= 2 && a.istride == 1 && a.T_in == a.T_out)) return 0;
   const int h = std::max(std::abs(a.tap_add), std::abs((taps - 1) * a.tap_mul + a.tap_add));

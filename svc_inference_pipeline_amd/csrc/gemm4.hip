@@ -70,7 +70,7 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
   const f16* zsrc = zpage + lane * 8;
 
   // DMA slots: image rows (wave * 4 + v) * 8 + (lane >> 3), v < 4, for A and for B
-  int a_t[4], a_kv[4];
+  int a_t[4], a_kv[4], a_tin[4];
   const f16* a_p[4];
   const f16* b_p[4];
 #pragma unroll
@@ -82,9 +82,11 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
     if (m < M) {
       const int b = m / a.T_out, t = m - b * a.T_out;
       a_t[v] = t * a.istride;
+      a_tin[v] = valid_in_rows(a, b);
       a_p[v] = a.X + (int64_t)b * a.T_in * a.ldx + kv * 8;
     } else {
       a_t[v] = -(1 << 29);
+      a_tin[v] = 0;
       a_p[v] = a.X;
     }
     b_p[v] = a.W + (int64_t)(n0 + row) * a.Kpad + kv * 8;
@@ -102,7 +104,7 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int st = a_t[v] + shift;
-        const bool ok = live && st >= 0 && st < a.T_in;
+        const bool ok = live && st >= 0 && st < a_tin[v];
         g4_dma(ok ? (const void*)(a_p[v] + (int64_t)a_t[v] * a.ldx + off) : (const void*)zsrc,
                A + (wave * 4 + v) * 1024);
       }
@@ -115,7 +117,7 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
         if (tap * a.Cp > kg) --tap;
         const int c = kg - tap * a.Cp;
         const int st = a_t[v] + tap * a.tap_mul + a.tap_add;
-        const bool ok = live && kg < a.K && st >= 0 && st < a.T_in;
+        const bool ok = live && kg < a.K && st >= 0 && st < a_tin[v];
         g4_dma(ok ? (const void*)(a_p[v] + (int64_t)st * a.ldx + (c - a_kv[v] * 8)) : (const void*)zsrc,
                A + (wave * 4 + v) * 1024);
       }

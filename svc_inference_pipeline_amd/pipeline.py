@@ -127,17 +127,22 @@ class SVCPipeline:
         return ConvertResult(wav=wav, mel=mel, f0=f0, x0=x0)
 
     def convert_many(self, wavs24, wavs16, singers, wavs16_float=None, fast_inference=True, speedup=10, seed=0,
-                     utt_ids=None):
+                     utt_ids=None, bucketed=False):
         """Ragged requests: lists of per-utterance device tensors (24 kHz f32 [N_i],
         16 kHz [N16_i], optional float 16 kHz for ContentVec) and singer ids -> list of waveforms f32 [T_i*hop] in
-        input order. Utterances are bucketed by exact length and each bucket runs as one batch; no kernel mixes
-        utterances and every per-element reduction order is independent of the batch composition, so each output
-        is bit-identical to converting that clip alone with the same utterance id (tests/test_gpu_ragged.py).
-        utt_ids (default: list positions) key the device noise, as in convert()."""
+        input order, each bit-identical to converting that clip alone with the same utterance id
+        (tests/test_gpu_ragged.py). utt_ids (default: list positions) key the device noise, as in convert().
+
+        Default: ONE padded batch with per-utterance lengths (convert_ragged): every kernel that looks across time
+        (STFT, Praat frames, convolutions, anti-aliased activations, fade-out) stops at each utterance's own end.
+        bucketed=True instead runs one batch per distinct length."""
         n = len(wavs24)
         if not (len(wavs16) == n == len(singers)) or (wavs16_float is not None and len(wavs16_float) != n):
             raise ValueError("convert_many: wavs24, wavs16, singers (and wavs16_float) must have one entry per utterance")
         ids = list(range(n)) if utt_ids is None else [int(u) for u in utt_ids]
+        if not bucketed:
+            return self.convert_ragged(wavs24, wavs16, singers, wavs16_float=wavs16_float,
+                                       fast_inference=fast_inference, speedup=speedup, seed=seed, utt_ids=ids)
         buckets = {}
         for i in range(n):
             key = (int(wavs24[i].shape[-1]), int(wavs16[i].shape[-1]),
@@ -158,3 +163,82 @@ class SVCPipeline:
                 out[i] = res.wav[j]
         return out
 
+    @staticmethod
+    def _pad_stack(tensors):
+        """list of 1-D device tensors -> zero-padded [B, max_len] and the host lengths"""
+        lens = [int(t.shape[-1]) for t in tensors]
+        out = torch.zeros(len(tensors), max(lens), dtype=tensors[0].dtype, device=tensors[0].device)
+        for i, t in enumerate(tensors):
+            out[i, :lens[i]] = t.reshape(-1)
+        return out, lens
+
+    def ragged_content(self, wavs16, T_b, T, wavs16_float=None):
+        """Content features for a ragged batch -> f16 [B, T, D]; rows [b, :T_b[b]] equal convert()'s for that clip
+        alone. Whisper runs on zero-padded 16 kHz audio (pad_or_trim pads with zeros, so the padding is exact), in two
+        groups: clips the reference maps in one 30 s window (T_b <= 2812) and long clips (per-window, see
+        whisper_content). HuBERT / ContentVec attends over every frame and normalises over time, so it runs per
+        exact-length bucket."""
+        e = self.engine
+        m = e.cfg.mapper
+        types = sorted(m.content_feature)
+        widths = [int(m.input_content_dim[t]) for t in types]
+        B = len(wavs16)
+        dev = wavs16[0].device
+        out = torch.zeros(B, T, sum(widths), device=dev, dtype=torch.float16)
+        col = 0
+        for t, w in zip(types, widths):
+            if t == "whisper":
+                for group in ([i for i in range(B) if T_b[i] <= MAX_MAPPED], [i for i in range(B) if T_b[i] > MAX_MAPPED]):
+                    if not group:
+                        continue
+                    w16, _ = self._pad_stack([wavs16[i] for i in group])
+                    Tg = max(T_b[i] for i in group)
+                    c = self.whisper_content(w16, Tg)
+                    for j, i in enumerate(group):
+                        out[i, :T_b[i], col:col + w] = c[j, :T_b[i]]
+            elif t in HUBERT_CONTENT_TYPES:
+                src = wavs16 if wavs16_float is None else wavs16_float
+                buckets = {}
+                for i in range(B):
+                    buckets.setdefault((int(src[i].shape[-1]), T_b[i]), []).append(i)
+                for (_, tb), idx in sorted(buckets.items()):
+                    feats = e.hubert_encode(torch.stack([src[i].reshape(-1) for i in idx]).contiguous())
+                    c = e.map_content(feats, tb, rule="hubert")
+                    for j, i in enumerate(idx):
+                        out[i, :tb, col:col + w] = c[j]
+            else:
+                raise ValueError(f"content feature {t!r} is not supported (whisper, {', '.join(HUBERT_CONTENT_TYPES)})")
+            col += w
+        return out
+
+    def convert_ragged(self, wavs24, wavs16, singers, wavs16_float=None, fast_inference=True, speedup=10, seed=0,
+                       utt_ids=None):
+        """infer.py's sequence for B clips of different lengths as ONE padded batch: the C-ABI stages take the
+        per-utterance lengths (include/svc_hip.h, "Ragged batches") and compute each clip exactly as alone.
+        -> list of waveforms f32 [T_b * hop]."""
+        e = self.engine
+        n = len(wavs24)
+        ids = list(range(n)) if utt_ids is None else [int(u) for u in utt_ids]
+        w24, n24 = self._pad_stack(wavs24)
+        dev = w24.device
+        T_b = [mel_frames(k, e.cfg.n_fft, e.cfg.hop_length) for k in n24]
+        T = max(T_b)
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream(dev) if os.environ.get("SVC_F0_SIDE", "1") != "0" else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            mel, energy = e.mel_energy(w24, n_samples=n24)
+            f0 = e.f0(w24, T, n_samples=n24)
+            e.pitch_shift(f0)
+        content = self.ragged_content(list(wavs16), T_b, T, wavs16_float)
+        main.wait_stream(side)
+        for t in (mel, energy, f0):
+            if t.is_cuda:
+                t.record_stream(main)
+        sing = torch.tensor([int(s) for s in singers], device=dev, dtype=torch.int32)
+        cond = e.condition(content, f0, energy, sing)
+        uid = torch.tensor(ids, device=dev, dtype=torch.int32)
+        x0 = e.diffsvc_sample(cond, fast_inference=fast_inference, speedup=speedup, seed=seed, utt_ids=uid, frames=T_b)
+        wav = e.bigvgan(x0, frames=T_b)
+        hop = e.cfg.hop_length
+        return [wav[i, :T_b[i] * hop] for i in range(n)]

@@ -25,6 +25,16 @@ def _stream():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def _host_lengths(lengths, B, ctype):
+    """Ragged-batch length table for the C-ABI: a host ctypes array of B entries, or None (uniform batch)."""
+    if lengths is None:
+        return None
+    vals = [int(v) for v in (lengths.tolist() if hasattr(lengths, "tolist") else lengths)]
+    if len(vals) != B:
+        raise ValueError(f"{len(vals)} lengths for a batch of {B}")
+    return (ctype * B)(*vals)
+
+
 def mel_frames(n_samples, n_fft=1024, hop=256):
     """utils/mel.py:148-167 frame count (reflect pad (n_fft-hop)/2 each side, center=False)."""
     return (n_samples + (n_fft - hop) - n_fft) // hop + 1
@@ -152,20 +162,24 @@ class SVCEngine:
         return wb.value, wsb.value
 
     # ------------------------------------------------------------------ stages
-    def mel_energy(self, wav24):
-        """wav24 f32 [B, N] -> (log-mel f32 [B, T, n_mels], energy f32 [B, T]) — utils/mel.py:179-201."""
+    def mel_energy(self, wav24, n_samples=None):
+        """wav24 f32 [B, N] -> (log-mel f32 [B, T, n_mels], energy f32 [B, T]) — utils/mel.py:179-201.
+        n_samples (ragged batch, host ints [B]): utterance b is wav24[b, :n_samples[b]]; its frames past
+        mel_frames(n_samples[b]) come back as zeros."""
         B, N = wav24.shape
         T = mel_frames(N, self.cfg.n_fft, self.cfg.hop_length)
         mel = torch.empty(B, T, self.cfg.n_mels, device=wav24.device, dtype=torch.float32)
         en = torch.empty(B, T, device=wav24.device, dtype=torch.float32)
-        _lib.call("svc_mel_energy", self._ctx, _ptr(wav24), B, N, _ptr(mel), _ptr(en), _stream())
+        _lib.call("svc_mel_energy", self._ctx, _ptr(wav24), B, N, _host_lengths(n_samples, B, ctypes.c_int64),
+                  _ptr(mel), _ptr(en), _stream())
         return mel, en
 
-    def f0(self, wav24, T):
-        """Praat-AC F0 padded to T frames (utils/f0.py:120-161) -> f64 [B, T]."""
+    def f0(self, wav24, T, n_samples=None):
+        """Praat-AC F0 padded to T frames (utils/f0.py:120-161) -> f64 [B, T]; n_samples as in mel_energy."""
         B, N = wav24.shape
         f0 = torch.empty(B, T, device=wav24.device, dtype=torch.float64)
-        _lib.call("svc_f0_ac", self._ctx, _ptr(wav24), B, N, T, _ptr(f0), _stream())
+        _lib.call("svc_f0_ac", self._ctx, _ptr(wav24), B, N, _host_lengths(n_samples, B, ctypes.c_int64), T,
+                  _ptr(f0), _stream())
         return f0
 
     def pitch_shift(self, f0, target_median=None):
@@ -229,14 +243,17 @@ class SVCEngine:
                   _stream())
         return im, ie
 
-    def diffsvc_eps(self, cond, x, t):
+    def diffsvc_eps(self, cond, x, t, frames=None):
         B, T, _ = cond.shape
         eps = torch.empty_like(x)
-        _lib.call("svc_diffsvc_eps", self._ctx, _ptr(cond), _ptr(x), B, T, int(t), _ptr(eps), _stream())
+        _lib.call("svc_diffsvc_eps", self._ctx, _ptr(cond), _ptr(x), B, T, _host_lengths(frames, B, ctypes.c_int32),
+                  int(t), _ptr(eps), _stream())
         return eps
 
-    def diffsvc_sample(self, cond, fast_inference=False, speedup=10, x_T=None, noise=None, seed=0, utt_ids=None):
-        """svc_model_inference (modules/diffsvcrepo_inference.py:154-240) -> normalised mel x_0 f32 [B, T, n_mel]."""
+    def diffsvc_sample(self, cond, fast_inference=False, speedup=10, x_T=None, noise=None, seed=0, utt_ids=None,
+                       frames=None):
+        """svc_model_inference (modules/diffsvcrepo_inference.py:154-240) -> normalised mel x_0 f32 [B, T, n_mel].
+        frames (ragged batch, host ints [B]): utterance b's mel frames; its rows past them come back as zeros."""
         B, T, _ = cond.shape
         x0 = torch.empty(B, T, self.cfg.mapper.n_mel, device=cond.device, dtype=torch.float32)
         if utt_ids is None and (x_T is None or (noise is None and not fast_inference)):
@@ -244,16 +261,19 @@ class SVCEngine:
             utt_ids = torch.arange(B, device=cond.device, dtype=torch.int32)
         uid = utt_ids.to(torch.int32).contiguous() if utt_ids is not None else None
         mode = MODE_PLMS if fast_inference else MODE_DDPM
-        _lib.call("svc_diffsvc_sample", self._ctx, _ptr(cond), B, T, mode, int(speedup),
+        _lib.call("svc_diffsvc_sample", self._ctx, _ptr(cond), B, T, _host_lengths(frames, B, ctypes.c_int32), mode,
+                  int(speedup),
                   _ptr(x_T.contiguous()) if x_T is not None else None,
                   _ptr(noise.contiguous()) if noise is not None else None, ctypes.c_uint64(seed), _ptr(uid),
                   _ptr(x0), _stream())
         return x0
 
-    def bigvgan(self, x0, return_mel=False):
-        """denormalize_mel_channel + synthesis_audios (Generator, trim, fade) -> wav f32 [B, T*hop]."""
+    def bigvgan(self, x0, return_mel=False, frames=None):
+        """denormalize_mel_channel + synthesis_audios (Generator, trim, fade) -> wav f32 [B, T*hop]. frames (ragged
+        batch, host ints [B]): utterance b's waveform is frames[b]*hop samples long (fade-out there, zeros after)."""
         B, T, _ = x0.shape
         wav = torch.empty(B, T * self.cfg.hop_length, device=x0.device, dtype=torch.float32)
         mel = torch.empty_like(x0) if return_mel else None
-        _lib.call("svc_bigvgan", self._ctx, _ptr(x0.contiguous()), B, T, _ptr(wav), _ptr(mel), _stream())
+        _lib.call("svc_bigvgan", self._ctx, _ptr(x0.contiguous()), B, T, _host_lengths(frames, B, ctypes.c_int32),
+                  _ptr(wav), _ptr(mel), _stream())
         return (wav, mel) if return_mel else wav

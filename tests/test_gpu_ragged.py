@@ -64,3 +64,75 @@ def test_feature_side_stream_and_residual_modes(monkeypatch):
         assert rel < 2e-3, rel
     finally:
         e.close()
+
+
+@pytest.fixture(scope="module")
+def tiny_engine():
+    cfg = C.load_config()
+    dims = W.WHISPER_DIMS["tiny-test"]
+    cfg.mapper.input_content_dim["whisper"] = dims["n_audio_state"]
+    e = SVCEngine(cfg, 0, whisper_state=W.make_whisper_state(dims, 0), mapper_state=W.make_mapper_state(cfg.mapper, 0),
+                  vocoder_state=W.make_vocoder_state(cfg.vocoder, 0))
+    yield e
+    e.close()
+
+
+RAGGED_SECS = [0.45, 1.0, 0.6, 0.3]
+
+
+def _padded(rows, fill):
+    """list of per-utterance [n_i, ...] device tensors -> [B, max, ...] with `fill` past each end (the ragged stages
+    must never read it)"""
+    n = max(r.shape[0] for r in rows)
+    out = torch.full((len(rows), n) + tuple(rows[0].shape[1:]), fill, device=rows[0].device, dtype=rows[0].dtype)
+    for i, r in enumerate(rows):
+        out[i, :r.shape[0]] = r
+    return out
+
+
+def test_ragged_mel_energy_f0(tiny_engine):
+    """svc_mel_energy / svc_f0_ac with utt_samples: each utterance's frames equal its single-clip run bit for bit
+    (own reflect padding, STFT frames, Praat frame grid and F0 padding), rows past its end are zero."""
+    e = tiny_engine
+    w24 = [dev(ON.synth_clip(70 + i, s, 24000)) for i, s in enumerate(RAGGED_SECS)]
+    n = [int(w.shape[0]) for w in w24]
+    big = _padded(w24, 0.37)
+    T_b = [(k + 768 - 1024) // 256 + 1 for k in n]
+    T = max(T_b)
+    mel, en = e.mel_energy(big, n_samples=n)
+    f0 = e.f0(big, T, n_samples=n)
+    assert mel.shape[1] == T
+    for i in range(len(n)):
+        m1, e1 = e.mel_energy(w24[i][None])
+        f1 = e.f0(w24[i][None], T_b[i])
+        assert torch.equal(mel[i, :T_b[i]], m1[0]), i
+        assert torch.equal(en[i, :T_b[i]], e1[0]), i
+        assert torch.equal(f0[i, :T_b[i]], f1[0]), i
+        assert not mel[i, T_b[i]:].any() and not en[i, T_b[i]:].any() and not f0[i, T_b[i]:].any()
+
+
+@pytest.mark.parametrize("fast", [True, False], ids=["plms250", "ddpm"])
+def test_ragged_sampler_and_vocoder(tiny_engine, fast):
+    """svc_diffsvc_sample / svc_bigvgan with frames: the dilated convolutions, the up-sampling, the anti-aliased
+    activations and the fade-out stop at each utterance's own end, and the device noise (x_T and the DDPM z) is
+    keyed by (utterance id, frame, channel), so each utterance equals its single-clip run bit for bit even with
+    garbage in the padding rows of `cond` / x0."""
+    e = tiny_engine
+    T_b = [23, 61, 40, 21]  # >= 20 frames: the 20 * 256-sample fade-out fits (modules/bigvgan_inference.py:37-42)
+    g = torch.Generator().manual_seed(0)
+    conds = [(torch.randn(t, 384, generator=g) * 0.5).cuda() for t in T_b]
+    cond = _padded(conds, 7.0)
+    ids = torch.tensor([5, 1, 9, 2], device="cuda", dtype=torch.int32)
+    x0 = e.diffsvc_sample(cond, fast_inference=fast, speedup=250, seed=11, utt_ids=ids, frames=T_b)
+    x0g = x0.clone()
+    for i, t in enumerate(T_b):
+        x0g[i, t:] = -3.0  # the vocoder must ignore rows past frames[i]
+    wav = e.bigvgan(x0g, frames=T_b)
+    for i, t in enumerate(T_b):
+        one = e.diffsvc_sample(conds[i][None].contiguous(), fast_inference=fast, speedup=250, seed=11,
+                               utt_ids=ids[i:i + 1].contiguous())
+        assert torch.equal(x0[i, :t], one[0]), i
+        assert not x0[i, t:].any()
+        w1 = e.bigvgan(one)
+        assert torch.equal(wav[i, :t * 256], w1[0]), i
+        assert not wav[i, t * 256:].any()

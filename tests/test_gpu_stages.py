@@ -333,7 +333,7 @@ def test_ddpm_without_noise_or_utt_ids_is_rejected(engine, golden):
     xT = dev(g["x_T"])
     x0 = torch.empty(B, T, 100, device="cuda")
     with pytest.raises(_lib.SVCError, match="utt_ids"):
-        _lib.call("svc_diffsvc_sample", engine._ctx, ptr(cond), B, T, 0, 1, ptr(xT), None, ctypes.c_uint64(0), None,
+        _lib.call("svc_diffsvc_sample", engine._ctx, ptr(cond), B, T, None, 0, 1, ptr(xT), None, ctypes.c_uint64(0), None,
                   ptr(x0), stream())
     # the host wrapper defaults the ids instead, and the run is reproducible
     a = engine.diffsvc_sample(cond, fast_inference=False, x_T=xT, seed=3).cpu().numpy()

@@ -24,7 +24,7 @@ def test_library_exports_all_symbols():
     lib = _lib.load()
     for name in header_symbols():
         assert hasattr(lib, name), name
-    assert lib.svc_abi_version() == 1
+    assert lib.svc_abi_version() == _lib.ABI_VERSION == 2  # 2: ragged-batch length tables
 
 
 def test_native_mel_filterbank_kat(golden):
