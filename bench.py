@@ -278,23 +278,19 @@ def main():
     dom_site = max((n for n in prof_all if n.split("@")[0] == dom_name), key=lambda n: prof_all[n]["ms"])
     dom_site = dom_site.split("@")[1] if "@" in dom_site else ""
 
-    # The sampler runs utterance-aligned sub-batches on concurrent streams (SVC_SAMPLER_STREAMS, default 3),
-    # so a launch's HIP-event duration includes time shared with the other streams' kernels. One extra untimed
-    # step with the sampler on a single stream gives the dominant call site's isolated per-launch rate.
+    # The sampler runs utterance-aligned sub-batches on concurrent streams (kernel switch sampler_streams, default 3,
+    # SVC_SAMPLER_STREAMS), so a launch's HIP-event duration includes time shared with the other streams' kernels. One
+    # extra untimed step with the sampler on a single stream gives the dominant call site's isolated per-launch rate.
     streams = int(os.environ.get("SVC_SAMPLER_STREAMS", "3"))
     isolated = None
     if streams > 1 and dom_site.startswith("diffsvc."):
-        saved = os.environ.get("SVC_SAMPLER_STREAMS")
-        os.environ["SVC_SAMPLER_STREAMS"] = "1"
+        eng.tune(sampler_streams=1)
         _lib.profile_enable(True)
         step()
         torch.cuda.synchronize()
         iso = _lib.profile_read()
         _lib.profile_enable(False)
-        if saved is None:
-            os.environ.pop("SVC_SAMPLER_STREAMS")
-        else:
-            os.environ["SVC_SAMPLER_STREAMS"] = saved
+        eng.tune(sampler_streams=streams)
         at_site = {n.split("@")[0]: v for n, v in iso.items() if n.endswith("@" + dom_site)}
         if at_site:
             k, v = max(at_site.items(), key=lambda kv: kv[1]["ms"])

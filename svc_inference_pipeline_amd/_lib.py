@@ -93,6 +93,13 @@ def call(name, *args):
     return check(getattr(load(), name)(*args))
 
 
+def tune(ctx=None, **switches):
+    """Kernel switches (include/svc_hip.h "tune.<name>", csrc/common.h Tuning) of a context, or with ctx None of the
+    op-level entry points' context; tune(ctx, reset=1) restores the values the context was created with."""
+    for k, v in switches.items():
+        call("svc_ctx_set_config", ctx, f"tune.{k}".encode(), float(v))
+
+
 def profile_enable(on=True):
     call("svc_profile_enable", 1 if on else 0)
 

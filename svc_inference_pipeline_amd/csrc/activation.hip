@@ -233,9 +233,8 @@ int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const flo
   SVC_REQUIRE(L >= 1 && C >= 4 && C % 4 == 0 && ldy % 4 == 0, "activation1d: L=%d C=%d ldy=%d", L, C, ldy);
   SVC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "activation1d: alignment");
   const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * (4 + 2), s);
-  // SVC_ACT_VARIANT (read per call, for A/B runs): 0 = LDS-tiled kernel, 1..4 = register streaming
-  const char* venv = getenv("SVC_ACT_VARIANT");
-  const int variant = venv ? atoi(venv) : 2;
+  // tuning act_variant (A/B runs, tests): 0 = LDS-tiled kernel, 1..4 = register streaming
+  const int variant = tuning().act_variant;
   if (variant == 1) {
     launch_rs<4, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   } else if (variant == 2) {

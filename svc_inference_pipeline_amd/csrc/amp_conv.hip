@@ -278,10 +278,9 @@ static int launch_amp_mode(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s
   const char* tag = C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>");
   const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
   // the activation image needs BT + 2P rows, not BT + 2 MAXP: sized per launch, C = 48 fits 5 workgroups per CU
-  // (instead of 4) for every conv with P <= 15 (SVC_AMP_LDS=max keeps the worst-case size, A/B runs)
-  const char* lenv = getenv("SVC_AMP_LDS");
+  // (instead of 4) for every conv with P <= 15 (tuning amp_lds_max keeps the worst-case size, A/B runs)
   const int P = (p.k - 1) / 2 * p.d;
-  const int lds = lenv && lenv[0] == 'm' ? CF::LDS : (CF::BT + 2 * P) * CF::LDA * 2;
+  const int lds = tuning().amp_lds_max ? CF::LDS : (CF::BT + 2 * P) * CF::LDA * 2;
   hipLaunchKernelGGL((amp_conv_kernel<C, MODE>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, p, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
@@ -290,8 +289,7 @@ static int launch_amp_mode(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s
 
 template <int C>
 static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
-  const char* mv = getenv("SVC_AMP_MODE");  // A/B runs of the register / packed-activation forms (read per call)
-  const int mode = mv ? atoi(mv) : 3;
+  const int mode = tuning().amp_mode;  // A/B runs of the register / packed-activation forms
   if (mode == 0) return launch_amp_mode<C, 0>(p, e, s);
   if (mode == 1) return launch_amp_mode<C, 1>(p, e, s);
   if (mode == 2) return launch_amp_mode<C, 2>(p, e, s);
@@ -310,18 +308,14 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
                   (!e.acc32 || e.ld_acc == C) && !e.add16 && e.act == ACT_NONE && e.kind == EPI_GENERIC,
               "amp_conv: epilogue must be contiguous rows of C channels (bias / add_row / acc32 / out32 / out16)");
   SVC_REQUIRE(((uintptr_t)p.x & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "amp_conv: alignment");
-  static const int run_adapt = [] {
-    const char* v = getenv("SVC_AMP_RUN");  // "0": the fixed run length (A/B runs)
-    return v && v[0] == '0' ? 0 : 1;
-  }();
-  if (run_adapt && !p.run_adapt) {
+  if (tuning().amp_run && !p.run_adapt) {  // amp_run 0: the fixed run length (A/B runs)
     AmpConvArgs q = p;
     q.run_adapt = 1;
     return amp_conv(q, C, e, s);
   }
-  if (const char* dbg = getenv("SVC_AMP_DBG")) {
+  if (tuning().amp_dbg && !p.dbg) {
     AmpConvArgs q = p;
-    q.dbg = atoi(dbg);
+    q.dbg = tuning().amp_dbg;
     if (C == 24) return launch_amp<24>(q, e, s);
     if (C == 48) return launch_amp<48>(q, e, s);
     return launch_amp<96>(q, e, s);

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <string>
 
 typedef _Float16 f16;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -186,6 +187,41 @@ struct StageRing {
 };
 
 int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
+
+// Kernel-selection switches: the measured production choices by default, other values select the earlier or
+// alternative kernel forms that the parity tests cover and the A/B benches compare (DESIGN.md records each result).
+// A context copies the defaults at creation, where an SVC_<NAME> environment variable overrides each (so a whole
+// benchmark can be A/B-run from the shell); svc_ctx_set_config(ctx, "tune.<name>", v) changes one for that context
+// (ctx NULL: the op-level entry points' context). Launchers read the switches of the context whose entry point is
+// running (tuning(), set per call by TuningScope) instead of the environment.
+struct Tuning {
+  int gemm_variant = 15;    // GEMM kernel: -1 gemm.hip, 10..14 conv_gemm3 tile, 15 fitted choice, 20 / 24 conv_gemm4
+  int gemm3_direct = 3;     // conv_gemm3 register-epilogue forms in use (mask, gemm3.hip direct_form3)
+  int gemm4_rmw = 0;        // DiffSVC output projection on conv_gemm4's register read-modify-write epilogue
+  int gemm4_gate = 1;       // DiffSVC gate GEMM on conv_gemm4's register gate epilogue (0: LDS-staged, variant 20)
+  int gemm_halo = 0;        // conv_gemm3 tap-reuse operand image
+  int act_variant = 2;      // activation1d kernel form (0 LDS-tiled, 1..4 register streaming)
+  int amp_mode = 3;         // amp_conv form (0..3)
+  int amp_run = 1;          // amp_conv activation runs sized one task per thread (0: fixed runs)
+  int amp_lds_max = 0;      // amp_conv worst-case activation image (1) instead of per-launch sizing
+  int amp_dbg = 0;          // amp_conv diagnostics (1 no activation phase, 2 no conv phase)
+  int amp_fused = 1;        // BigVGAN small-C fused activation + conv (0: activation1d + GEMM everywhere)
+  int amp_maxc = 48;        // widest channel count that takes the fused kernel
+  int whisper_streams = 1;  // Whisper encoder sub-batch streams
+  int sampler_streams = 3;  // DiffSVC sampler sub-batch streams
+  int vocoder_streams = 1;  // BigVGAN sub-batch streams
+  int diff_res32 = 0;       // DiffSVC residual stream in f32 (default: split-fp16 hi / lo halves)
+  int f0_dbg = 0;           // F0 kernel diagnostics
+  std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only)
+  void from_env();
+  bool set(const char* name, double v);  // false: unknown name ("reset" restores the creation-time values)
+};
+const Tuning& tuning();
+struct TuningScope {
+  explicit TuningScope(const Tuning* t);
+  ~TuningScope();
+  const Tuning* prev;
+};
 
 // live per-kernel timing (bench roofline): when enabled, launches are bracketed by hipEvents and
 // aggregated by kernel name together with their algorithmic FLOPs / bytes.

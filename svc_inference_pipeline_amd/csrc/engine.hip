@@ -119,22 +119,6 @@ int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
 bool conv_gemm4_rmw_form(const ConvGemmArgs& a, const EpiArgs& e);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
-struct DiffLayerArgs {
-  const f16* x16;
-  const f16* Wd;
-  const f16* cpF;
-  const f16* Wo;
-  const float* bo;
-  const float* dpn;
-  float* x32;
-  f16* x16n;
-  f16* g16;
-  int ldg;
-  int B, T, dil;
-  const f16* zpage;
-};
-int diff_layer(const DiffLayerArgs& a, bool out, hipStream_t s);
-int cp_fragment(const f16* cp16, int ldcp, const float* bdil, int rows, int rows_pad, f16* cpF, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s);
 int hubert_frames5(const float* wav, int B, int64_t n, f16* out, bool split, hipStream_t s);
@@ -253,12 +237,60 @@ struct VStage {
   std::vector<std::vector<int>> rd;
 };
 
+// ---------------------------------------------------------------------------- kernel switches
+static thread_local const Tuning* t_tuning = nullptr;
+
+void Tuning::from_env() {
+  struct {
+    const char* env;
+    int* v;
+  } ints[] = {{"SVC_GEMM_VARIANT", &gemm_variant}, {"SVC_GEMM3_DIRECT", &gemm3_direct}, {"SVC_GEMM4_RMW", &gemm4_rmw},
+              {"SVC_GEMM4_GATE", &gemm4_gate},     {"SVC_GEMM_HALO", &gemm_halo},       {"SVC_ACT_VARIANT", &act_variant},
+              {"SVC_AMP_MODE", &amp_mode},         {"SVC_AMP_RUN", &amp_run},           {"SVC_AMP_DBG", &amp_dbg},
+              {"SVC_AMP_FUSED", &amp_fused},       {"SVC_AMP_MAXC", &amp_maxc},         {"SVC_WHISPER_STREAMS", &whisper_streams},
+              {"SVC_SAMPLER_STREAMS", &sampler_streams}, {"SVC_VOCODER_STREAMS", &vocoder_streams},
+              {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg}};
+  for (auto& it : ints)
+    if (const char* v = getenv(it.env)) *it.v = atoi(v);
+  if (const char* v = getenv("SVC_AMP_LDS")) amp_lds_max = v[0] == 'm' ? 1 : 0;
+  if (const char* v = getenv("SVC_SITE_VARIANT")) site_variant = v;
+}
+
+bool Tuning::set(const char* name, double v) {
+  struct {
+    const char* name;
+    int* v;
+  } ints[] = {{"gemm_variant", &gemm_variant}, {"gemm3_direct", &gemm3_direct}, {"gemm4_rmw", &gemm4_rmw},
+              {"gemm4_gate", &gemm4_gate},     {"gemm_halo", &gemm_halo},       {"act_variant", &act_variant},
+              {"amp_mode", &amp_mode},         {"amp_run", &amp_run},           {"amp_lds_max", &amp_lds_max},
+              {"amp_dbg", &amp_dbg},           {"amp_fused", &amp_fused},       {"amp_maxc", &amp_maxc},
+              {"whisper_streams", &whisper_streams}, {"sampler_streams", &sampler_streams},
+              {"vocoder_streams", &vocoder_streams}, {"diff_res32", &diff_res32}, {"f0_dbg", &f0_dbg}};
+  for (auto& it : ints)
+    if (strcmp(it.name, name) == 0) {
+      *it.v = (int)v;
+      return true;
+    }
+  return false;
+}
+
+const Tuning& tuning() {
+  static const Tuning env_default = [] {
+    Tuning t;
+    t.from_env();
+    return t;
+  }();
+  return t_tuning ? *t_tuning : env_default;
+}
+TuningScope::TuningScope(const Tuning* t) : prev(t_tuning) { t_tuning = t; }
+TuningScope::~TuningScope() { t_tuning = prev; }
 }  // namespace svc
 
 using namespace svc;
 
 struct svc_ctx {
   int device = 0;
+  Tuning tune, tune0;  // kernel switches (tune0: their values at creation, for "tune.reset")
   // ragged-batch length tables, one ring per stage (the feature stages run on their own stream)
   StageRing lens_feat, lens_main;
   std::map<std::string, Param> params;
@@ -299,10 +331,6 @@ struct svc_ctx {
   int C = 384, n_mel = 100, n_layers = 20, dil_cycle = 4, steps = 1000, content_dim = 1024, n_bins = 256;
   PackedGemm content_lin, cp_all, melpre, skipproj, outproj;
   std::vector<PackedGemm> dil, outres;  // per layer: dilated conv (paired), residual half of output_projection
-  // fused residual-layer kernel (diff_layer.hip): pair16-packed dilated conv [2C][3C], residual half of
-  // output_projection [C][C], its bias [C], the dilated conv bias [2C] (folded into the fragment-major cp)
-  std::vector<f16*> dl_wd, dl_wo;
-  std::vector<float*> dl_bo, dl_bdil;
   PackedGemm skip_all;                  // skip halves of all layers' output_projection, K = layers * C
   float *emb_m = nullptr, *emb_l = nullptr, *emb_s = nullptr, *mbins = nullptr, *ebins = nullptr;
   float* dproj = nullptr;  // [steps][layers][C]
@@ -570,33 +598,31 @@ static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cv
   return a;
 }
 
+
 // tv / tv_mul: ragged batches, utterance b's valid input rows are tv[b] * tv_mul (ConvGemmArgs::tv; NULL = all)
 int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
              hipStream_t s, const char* site = "", const int* tv = nullptr, int tv_mul = 1) {
   prof_site(site);
-  // conv_gemm3's register epilogues (SVC_GEMM3_DIRECT mask, gemm3.hip) stay off inside the DiffSVC sampler unless
+  const Tuning& tu = tuning();
+  // conv_gemm3's register epilogues (gemm3_direct mask, gemm3.hip) stay off inside the DiffSVC sampler unless
   // bit 8 is set: there its sub-batch GEMMs run beside the gate GEMMs of the other streams, which then ran slower
-  const char* denv = getenv("SVC_GEMM3_DIRECT");
-  const int dmask = denv ? atoi(denv) : 3;
-  if (!(dmask & 8) && site && strncmp(site, "diffsvc.", 8) == 0) e.no_reg_epi = 1;
+  if (!(tu.gemm3_direct & 8) && site && strncmp(site, "diffsvc.", 8) == 0) e.no_reg_epi = 1;
   ConvGemmArgs a = gemm_args(g, X, ldx, Cvalid, B, T_in, T_out, e);
   a.tv = tv;
   a.tv_mul = tv_mul;
   const bool pair = e.kind == EPI_GATE;
-  // SVC_GEMM_VARIANT: -1 = v1 (gemm.hip) for plain GEMMs; 10..14 = conv_gemm3 tile,
+  // gemm_variant: -1 = v1 (gemm.hip) for plain GEMMs; 10..14 = conv_gemm3 tile,
   // 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired epilogue, K = 1152)
   // which runs conv_gemm4 with its register gate epilogue (24; 3-9 % faster than conv_gemm3); 20 = conv_gemm4,
   // 24 = conv_gemm4 with its register epilogues (gate; residual read-modify-write) where the epilogue has that form.
   // (The round-1 conv_gemm2 tiles and conv_gemm5 ring variants were measured slower and removed.)
-  const char* venv = getenv("SVC_GEMM_VARIANT");  // read per call (A/B runs and tests switch it)
-  int variant = venv ? atoi(venv) : 15;
-  // SVC_GEMM4_RMW=1: the output projection on conv_gemm4's register epilogue too. Alone it is 12 % faster per sampler
+  int variant = tu.gemm_variant;
+  // gemm4_rmw = 1: the output projection on conv_gemm4's register epilogue too. Alone it is 12 % faster per sampler
   // sub-batch launch (tools/gemm_bench.py), but beside the other sampler streams the whole step measured 1.5 % slower
   // (703 vs 713 audio-s/s, same box), so it is opt-in.
-  const char* renv = getenv("SVC_GEMM4_RMW");
-  const char* genv = getenv("SVC_GEMM4_GATE");  // 0: the gate GEMM on conv_gemm4's LDS-staged epilogue (variant 20)
-  // SVC_SITE_VARIANT="site=variant,...": per-call-site override (tile / kernel A/B runs, e.g. diffsvc.outproj=20)
-  if (const char* senv = getenv("SVC_SITE_VARIANT")) {
+  // site_variant = "site=variant,...": per-call-site override (tile / kernel A/B runs, e.g. diffsvc.outproj=20)
+  if (!tu.site_variant.empty()) {
+    const char* senv = tu.site_variant.c_str();
     const size_t sl = site ? strlen(site) : 0;
     for (const char* p = senv; sl && (p = strstr(p, site)) != nullptr; p += sl)
       if ((p == senv || p[-1] == ',') && p[sl] == '=') {
@@ -604,10 +630,10 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
         break;
       }
   }
-  if (variant == 15 && pair) variant = (genv && !atoi(genv)) ? 20 : 24;
-  if (variant == 15 && renv && atoi(renv) && conv_gemm4_rmw_form(a, e)) variant = 24;
+  if (variant == 15 && pair) variant = tu.gemm4_gate ? 24 : 20;
+  if (variant == 15 && tu.gemm4_rmw && conv_gemm4_rmw_form(a, e)) variant = 24;
   SVC_REQUIRE(variant == -1 || (variant >= 10 && variant <= 15) || variant == 20 || variant == 24,
-              "SVC_GEMM_VARIANT %d: -1, 10..15, 20 or 24", variant);
+              "gemm_variant %d: -1, 10..15, 20 or 24", variant);
   if (pair || g.N > 64) {
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), s, variant == 24);
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
@@ -925,27 +951,6 @@ int build_mapper(svc_ctx* c) {
     if ((st = pack_conv1d(c, c->dil[i], dw->host, db->host, 2 * C, C, 3, C, d, d, 1, &perm))) return st;
     // rows 0..C-1 of output_projection are the residual, C..2C-1 the skip (modules/diffsvc.py:229-231)
     if ((st = pack_conv1d(c, c->outres[i], ow->host, ob->host, C, C, 1, C, 1, 0, 1))) return st;
-    if (C == 384) {  // the fused layer kernel is specialised for the reference's 384 residual channels
-      std::vector<f16> wd((size_t)2 * C * 3 * C), wo((size_t)C * C);
-      for (int n = 0; n < 2 * C; ++n) {
-        const int o = ((n & 16) ? C : 0) + (n >> 5) * 16 + (n & 15);  // pair16: gate/filter of one channel
-        for (int tap = 0; tap < 3; ++tap)
-          for (int ci = 0; ci < C; ++ci)
-            wd[(size_t)n * 3 * C + tap * C + ci] = (f16)dw->host[((int64_t)o * C + ci) * 3 + tap];
-      }
-      for (int n = 0; n < C; ++n)
-        for (int ci = 0; ci < C; ++ci) wo[(size_t)n * C + ci] = (f16)ow->host[(int64_t)n * C + ci];
-      f16 *dwp, *wop;
-      float *bop, *bdp;
-      if ((st = upload_vec(c, wd, &dwp)) || (st = upload_vec(c, wo, &wop))) return st;
-      if ((st = dev_upload(c, ob->host, (size_t)C * 4, (void**)&bop)) ||
-          (st = dev_upload(c, db->host, (size_t)2 * C * 4, (void**)&bdp)))
-        return st;
-      c->dl_wd.push_back(dwp);
-      c->dl_wo.push_back(wop);
-      c->dl_bo.push_back(bop);
-      c->dl_bdil.push_back(bdp);
-    }
     opw_l[i] = ow;
     opb_l[i] = ob;
   }
@@ -1222,6 +1227,8 @@ svc_status svc_ctx_create(int device, svc_ctx** out) {
   SVC_HIP_CHECK(hipSetDevice(device));
   svc_ctx* c = new svc_ctx();
   c->device = device;
+  c->tune.from_env();
+  c->tune0 = c->tune;
   *out = c;
   return SVC_OK;
 }
@@ -1244,8 +1251,20 @@ svc_status svc_ctx_destroy(svc_ctx* c) {
   return SVC_OK;
 }
 
+static int op_ws(svc_ctx** tmp);
+
 svc_status svc_ctx_set_config(svc_ctx* c, const char* key, double value) {
-  SVC_REQUIRE(c && key, "set_config: null");
+  SVC_REQUIRE(key, "set_config: null key");
+  if (strncmp(key, "tune.", 5) == 0) {  // kernel switches (Tuning); NULL context: the op-level entry points'
+    if (!c) op_ws(&c);
+    if (strcmp(key + 5, "reset") == 0) {
+      c->tune = c->tune0;
+      return SVC_OK;
+    }
+    SVC_REQUIRE(c->tune.set(key + 5, value), "set_config: unknown kernel switch %s", key);
+    return SVC_OK;
+  }
+  SVC_REQUIRE(c, "set_config: null context");
   c->cfg[key] = value;
   return SVC_OK;
 }
@@ -1367,6 +1386,7 @@ svc_status svc_mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double
 }
 
 #define CTX_READY(c)                                                        \
+  TuningScope tuning_scope_((c) ? &(c)->tune : nullptr);                    \
   do {                                                                      \
     SVC_REQUIRE((c), "null context");                                       \
     if (!(c)->finalized) {                                                  \
@@ -1541,12 +1561,11 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   WS_GET(f16, o16, rows2 * D);
   WS_GET(f16, h16, rows2 * 4 * D * X3);
   const float qk_scale = powf((float)(D / c->wH), -0.25f);
-  // SVC_WHISPER_STREAMS = n > 1 runs the 24 blocks as utterance-aligned sub-batches on n streams (as the sampler
+  // whisper_streams = n > 1 runs the 24 blocks as utterance-aligned sub-batches on n streams (as the sampler
   // does): rows are time-major per utterance, so a sub-batch is a row range of every buffer, and one sub-batch's
   // HBM-bound GEMM epilogues / layer norms run beside the other's MFMA phases. Default 1: with the F0 stage on its
   // side stream the single full-batch stream measured 0.3-0.4 % faster end to end (three A/B pairs, r01i kernels).
-  const char* wenv = getenv("SVC_WHISPER_STREAMS");
-  const int NSW = std::max(1, std::min(std::min(wenv ? atoi(wenv) : 1, B), (int)kMaxSubStreams));
+  const int NSW = std::max(1, std::min(std::min(tuning().whisper_streams, B), (int)kMaxSubStreams));
   if ((st = c->ensure_sub_streams(NSW))) return st;
   if (NSW > 1) {
     SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
@@ -1804,10 +1823,7 @@ svc_status svc_condition(svc_ctx* c, const void* content16, const double* f0, co
 // ---------------------------------------------------------------------------- DiffSVC denoiser
 struct DenoiseBufs {
   f16* cp16;     // [rows][NL*2C] conditioner projections of every layer (hoisted out of the sampler loop)
-  f16* cpF;      // fused path: [NL][rows_pad][2C] fragment-major cp + dilated bias (diff_layer.hip)
-  int rows_pad;  // rows of this (sub-)batch rounded up to 64
-  f16* y16b;     // [rows][C] ping-pong partner of y16 (the fused layer reads one and writes the other)
-  float* h32;    // [rows][C] residual stream (f32: the fused path and SVC_DIFF_RES32=1)
+  float* h32;    // [rows][C] residual stream (f32, tuning diff_res32)
   f16* y16;      // [rows][C] next layer input x + diffusion_projection
   f16* g16;      // [rows][NL*C] gate outputs of every layer (A operand of the skip GEMM)
   f16* s16;      // [rows][3C] sum(skip) / sqrt(NL) ([hi | lo | hi] split-fp16 with head_split, else [rows][C])
@@ -1820,14 +1836,6 @@ struct DenoiseBufs {
                  // shift is the layer stride (tap_mul = rows_total)
 };
 
-// The fused residual-layer kernel (diff_layer.hip) is opt-in (SVC_DIFF_FUSED=1): owning all 768 gate columns
-// per 64-row tile makes every workgroup stream the whole 1.77 MB dilated-conv weight, and at the measured
-// ~12 B/clk/CU L2->LDS fill rate that costs more (155 us/layer at B=32) than it saves over the two tiled GEMMs
-// (97 + 45 us) — DESIGN.md, "Fused residual layer (measured, not adopted)".
-static bool fused_layers(svc_ctx* c) {
-  const char* v = getenv("SVC_DIFF_FUSED");  // read per call (A/B runs and tests switch it)
-  return (int)c->dl_wd.size() == c->n_layers && v && atoi(v) == 1;
-}
 
 // tv (device, optional): ragged batches, utterance b has tv[b] valid frames; only the dilated convs look across frames
 static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s,
@@ -1838,9 +1846,8 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   int st;
   // Residual stream x: by default split-fp16 storage (x + dproj_l = y16 + lo16, ~22 significand bits in 4 bytes):
   // the layer's GEMM operand y16 is its high half, so each residual update moves 10 instead of 12 bytes per element.
-  // SVC_DIFF_RES32=1 (and the fused path) keep x in f32 (h32).
-  const char* r32env = getenv("SVC_DIFF_RES32");
-  const bool res32 = fused_layers(c) || (r32env && atoi(r32env) == 1);
+  // tuning diff_res32 = 1 keeps x in f32 (h32).
+  const bool res32 = tuning().diff_res32 == 1;
   EpiArgs e = epi();
   e.act = ACT_RELU;
   if (res32) {
@@ -1853,32 +1860,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
   if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
-  if (fused_layers(c)) {
-    SVC_REQUIRE(!tv, "the fused residual-layer kernel (SVC_DIFF_FUSED) takes uniform lengths only");
-    f16* cur = bb.y16;
-    f16* nxt = bb.y16b;
-    for (int i = 0; i < NL; ++i) {
-      DiffLayerArgs a{};
-      a.x16 = cur;
-      a.Wd = c->dl_wd[i];
-      a.cpF = bb.cpF + (size_t)i * bb.rows_pad * 2 * C;
-      a.Wo = c->dl_wo[i];
-      a.bo = c->dl_bo[i];
-      a.dpn = i + 1 < NL ? dp + (size_t)(i + 1) * C : nullptr;
-      a.x32 = bb.h32;
-      a.x16n = nxt;
-      a.g16 = bb.g16 + (size_t)i * bb.g_ls;
-      a.ldg = C;
-      a.B = B;
-      a.T = T;
-      a.dil = 1 << (i % c->dil_cycle);
-      a.zpage = zero_page();
-      prof_site("diffsvc.layer");
-      if ((st = diff_layer(a, i + 1 < NL, s))) return st;
-      std::swap(cur, nxt);
-    }
-  }
-  for (int i = 0; i < NL && !fused_layers(c); ++i) {
+  for (int i = 0; i < NL; ++i) {
     EpiArgs g = epi();
     g.kind = EPI_GATE;
     g.cp = bb.cp16 + (size_t)i * bb.cp_ls;
@@ -1939,38 +1921,20 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
 
 static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   const size_t rows = (size_t)B * T, C = c->C;
-  const size_t fm_rows = fused_layers(c) ? rows + 64 * kMaxSubStreams : 0;  // sub-batch regions padded to 64 rows
   WS_GET(f16, cp16, rows * c->n_layers * 2 * C);
-  WS_GET(f16, cpF, fm_rows * c->n_layers * 2 * C + 8);
   WS_GET(float, h32, rows * C);
   WS_GET(f16, y16, rows * C);
-  WS_GET(f16, y16b, rows * C);
   WS_GET(f16, g16, rows * c->n_layers * C);
   WS_GET(f16, s16, rows * C * 3);  // [hi | lo | hi] when head_split
   WS_GET(f16, u16, rows * C * 3);
   WS_GET(f16, lo16, rows * C);
-  bb = DenoiseBufs{cp16, cpF, (int)round_up((int64_t)rows, 64), y16b, h32, y16, g16, s16, u16, lo16, rows * 2 * C,
-                   rows * C};
+  bb = DenoiseBufs{cp16, h32, y16, g16, s16, u16, lo16, rows * 2 * C, rows * C};
   return SVC_OK;
 }
 
 static size_t denoise_bytes(svc_ctx* c, int B, int T) {
   const size_t rows = (size_t)B * T, C = c->C;
-  return rows * c->n_layers * 2 * C * 2 + (fused_layers(c) ? rows + 64 * kMaxSubStreams : 0) * c->n_layers * 2 * C * 2 +
-         rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 9) + 22 * 4096;
-}
-
-// fused path: the hoisted conditioner projection of one (sub-)batch -> fragment-major records with the dilated
-// conv bias folded in (bb.cpF / bb.rows_pad describe that sub-batch's region; cp16 points at its first row)
-static int fragment_cp(svc_ctx* c, const DenoiseBufs& bb, int rows, hipStream_t s) {
-  if (!fused_layers(c)) return SVC_OK;
-  const int C = c->C, NL = c->n_layers;
-  int st;
-  for (int l = 0; l < NL; ++l)
-    if ((st = cp_fragment(bb.cp16 + (size_t)l * bb.cp_ls, 2 * C, c->dl_bdil[l], rows, bb.rows_pad,
-                          bb.cpF + (size_t)l * bb.rows_pad * 2 * C, s)))
-      return st;
-  return SVC_OK;
+  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 8) + 22 * 4096;
 }
 
 static int project_cond(svc_ctx* c, const float* cond, int B, int T, const DenoiseBufs& bb, hipStream_t s) {
@@ -2021,7 +1985,6 @@ svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B,
   DenoiseBufs bb;
   if ((st = alloc_denoise(c, B, T, bb))) return st;
   if ((st = project_cond(c, cond, B, T, bb, s))) return st;
-  if ((st = fragment_cp(c, bb, rows, s))) return st;
   WS_GET(f16, x16, (size_t)rows * ld16);
   if ((st = f32_to_f16(x, c->n_mel, x16, ld16, rows, c->n_mel, ld16, s))) return st;
   if ((st = denoise(c, bb, x16, B, T, t, eps, s, tv))) return st;
@@ -2085,9 +2048,8 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
   // launches overlap on the GPU, so one sub-batch's epilogue / prologue phases (HBM-bound, ~40 % of a
   // denoiser GEMM launch at this size) run beside the other's MFMA phases. Utterances are independent,
   // so results are identical to a single stream. Default 3 (measured best with the caller stream on the 4
-  // hardware queues; 2: -4 %, 4: -13 %); SVC_SAMPLER_STREAMS=1 disables the split.
-  const char* ns_env = getenv("SVC_SAMPLER_STREAMS");
-  const int S = std::max(1, std::min(std::min(ns_env ? atoi(ns_env) : 3, B), (int)kMaxSubStreams));
+  // hardware queues; 2: -4 %, 4: -13 %); sampler_streams = 1 disables the split.
+  const int S = std::max(1, std::min(std::min(tuning().sampler_streams, B), (int)kMaxSubStreams));
   struct Sub {
     int B, b0;
     size_t r0;
@@ -2100,22 +2062,12 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
     sub[h].r0 = (size_t)sub[h].b0 * T;
     sub[h].s = S == 1 ? s : c->sub_streams[h];
   }
-  size_t fm_off[kMaxSubStreams];  // start of each sub-batch's fragment-major cp region (rows padded to 64)
-  for (int h = 0, acc = 0; h < S; ++h) {
-    fm_off[h] = (size_t)acc;
-    acc += (int)round_up((int64_t)sub[h].B * T, 64);
-  }
   auto sub_bufs = [&](const Sub& u) {
     const size_t r = u.r0;
-    const int C = c->C, NL = c->n_layers;
-    const int h = (int)(&u - sub);
-    const int rp = (int)round_up((int64_t)u.B * T, 64);
-    return DenoiseBufs{bb.cp16 + r * 2 * C, bb.cpF + fm_off[h] * NL * 2 * C, rp, bb.y16b + r * C,
-                       bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * 3 * C, bb.u16 + r * 3 * C,
-                       bb.lo16 + r * C, bb.cp_ls, bb.g_ls};
+    const int C = c->C;
+    return DenoiseBufs{bb.cp16 + r * 2 * C, bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * 3 * C,
+                       bb.u16 + r * 3 * C, bb.lo16 + r * C, bb.cp_ls, bb.g_ls};
   };
-  for (int h = 0; h < S; ++h)
-    if ((st = fragment_cp(c, sub_bufs(sub[h]), sub[h].B * T, s))) return st;
   SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
   for (int h = 0; h < S && S > 1; ++h) SVC_HIP_CHECK(hipStreamWaitEvent(sub[h].s, c->ev_fork, 0));
   auto join = [&]() -> int {
@@ -2262,19 +2214,17 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
   WS_GET(float, XS, big);
   WS_GET(f16, a16, big);
   WS_GET(f16, next16, big);
-  const char* amp_env = getenv("SVC_AMP_FUSED");  // "0" = unfused activation1d + GEMM everywhere (A/B runs)
-  const bool use_amp = !(amp_env && amp_env[0] == '0');
-  const char* amp_max = getenv("SVC_AMP_MAXC");   // widest channel count that takes the fused kernel (A/B runs)
-  // C = 96 measured 1.2 % faster end to end as activation1d + conv_gemm3 (736 vs 727 audio-s/s, same box); C = 48
-  // unfused is 9 % slower (its N = 48 GEMMs are too narrow for the MFMA tiles)
-  const int amp_maxc = amp_max ? atoi(amp_max) : 48;
+  const bool use_amp = tuning().amp_fused != 0;  // 0 = unfused activation1d + GEMM everywhere (A/B runs)
+  // amp_maxc: widest channel count that takes the fused kernel. C = 96 measured 1.2 % faster end to end as
+  // activation1d + conv_gemm3 (736 vs 727 audio-s/s, same box); C = 48 unfused is 9 % slower (its N = 48 GEMMs are too
+  // narrow for the MFMA tiles)
+  const int amp_maxc = tuning().amp_maxc;
   const int ns = (int)c->vstages.size();
 
   // Utterance-aligned sub-batches on their own streams (as in svc_diffsvc_sample): every buffer is
   // time-major per utterance, so a sub-batch is a row offset into each; launches alternate between streams.
-  // Default 1: its launches are long (0.3-2 ms) and measured no faster split (SVC_VOCODER_STREAMS=2/3).
-  const char* vs_env = getenv("SVC_VOCODER_STREAMS");
-  const int NS = std::max(1, std::min(std::min(vs_env ? atoi(vs_env) : 1, B), (int)kMaxSubStreams));
+  // Default 1: its launches are long (0.3-2 ms) and measured no faster split (vocoder_streams = 2 / 3).
+  const int NS = std::max(1, std::min(std::min(tuning().vocoder_streams, B), (int)kMaxSubStreams));
   if ((st = c->ensure_sub_streams(NS))) return st;
   SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
   int b0[kMaxSubStreams + 1];
@@ -2426,6 +2376,8 @@ static int op_ws(svc_ctx** tmp) {
   static svc_ctx* g = nullptr;
   if (!g) {
     g = new svc_ctx();
+    g->tune.from_env();
+    g->tune0 = g->tune;
     int dev = 0;
     (void)hipGetDevice(&dev);
     g->device = dev;
@@ -2463,6 +2415,7 @@ svc_status svc_op_conv1d(const float* x, int B, int T_in, int Cin, const float* 
                          int stride, int dilation, int pad, int act, float* y, void* stream) {
   svc_ctx* c;
   op_ws(&c);
+  TuningScope tuning_scope_(&c->tune);
   hipStream_t s = (hipStream_t)stream;
   const int T_out = (T_in + 2 * pad - dilation * (k - 1) - 1) / stride + 1;
   SVC_REQUIRE(T_out > 0, "op_conv1d: T_out=%d", T_out);
@@ -2491,6 +2444,7 @@ svc_status svc_op_amp_conv(const float* x, int B, int L, int C, const float* alp
                            float* y, void* stream) {
   svc_ctx* c;
   op_ws(&c);
+  TuningScope tuning_scope_(&c->tune);
   hipStream_t s = (hipStream_t)stream;
   SVC_REQUIRE(amp_conv_supported(C, k, d), "op_amp_conv: C=%d k=%d d=%d unsupported", C, k, d);
   std::vector<float> wh, bh;
@@ -2514,6 +2468,7 @@ svc_status svc_op_conv_transpose1d(const float* x, int B, int T_in, int Cin, con
                                    int Cout, int k, int stride, int pad, float* y, void* stream) {
   svc_ctx* c;
   op_ws(&c);
+  TuningScope tuning_scope_(&c->tune);
   hipStream_t s = (hipStream_t)stream;
   const int T_out = (T_in - 1) * stride - 2 * pad + k;
   SVC_REQUIRE(T_out == T_in * stride, "op_conv_transpose1d: only T_out = T_in*stride supported (got %d)", T_out);
@@ -2546,6 +2501,7 @@ svc_status svc_op_activation1d(const float* x, int B, int L, int C, const float*
                                float* y, void* stream) {
   svc_ctx* c;
   op_ws(&c);
+  TuningScope tuning_scope_(&c->tune);
   hipStream_t s = (hipStream_t)stream;
   int st;
   if ((st = c->ws.reserve(std::max((size_t)B * L * C * 2 + 4096, c->ws.cap)))) return st;
@@ -2560,6 +2516,7 @@ svc_status svc_op_attention(const float* q, const float* k, const float* v, int 
                             void* stream) {
   svc_ctx* c;
   op_ws(&c);
+  TuningScope tuning_scope_(&c->tune);
   hipStream_t s = (hipStream_t)stream;
   int st;
   const size_t rows = (size_t)B * L;
@@ -2592,6 +2549,9 @@ __global__ void fill_f16_kernel(f16* p, int64_t n, uint32_t seed) {
 }
 
 extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_kind, int variant, int iters, double* ms_out) {
+  svc_ctx* oc;
+  op_ws(&oc);
+  TuningScope tuning_scope_(&oc->tune);
   SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters >= 1, "gemm_bench: bad args");
   SVC_REQUIRE(epi_kind < 3 || epi_kind == 6 || variant == 24,
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");

@@ -579,7 +579,7 @@ int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double
   }
   SVC_REQUIRE(P.nw <= 2048 && P.maxc <= F0_MAXC, "f0: window %d / candidates %d too large", P.nw, P.maxc);
   P.voicing = voicing;
-  if (const char* dbg = getenv("SVC_F0_DBG")) P.dbg = atoi(dbg);
+  P.dbg = tuning().f0_dbg;
   P.silence = 0.03;
   P.octave_cost = 0.01;
   P.octave_jump = 0.35;

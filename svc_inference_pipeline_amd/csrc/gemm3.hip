@@ -492,25 +492,23 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
 }
 
 // tap reuse applies to same-length stride-1 multi-tap convs whose K-tiles are whole taps, with |shift| <= 32
-// Opt-in (SVC_GEMM_HALO=1): measured on MI355X it moves ~40 % fewer operand bytes yet runs 5-10 % SLOWER than
+// Opt-in (tuning gemm_halo = 1): measured on MI355X it moves ~40 % fewer operand bytes yet runs 5-10 % SLOWER than
 // the per-tap schedule on the DiffSVC / BigVGAN shapes (tools/gemm_bench.py), so these GEMMs are not
 // bound by the L2 -> LDS byte rate; kept, parity-tested, for the next schedule revision.
 static int halo_of(const ConvGemmArgs& a) {
-  const char* v = getenv("SVC_GEMM_HALO");  // read per call (A/B runs and tests switch it)
-  if (!(v && atoi(v) == 1) || a.tv) return 0;  // (the halo image masks by the uniform T_in only)
+  if (tuning().gemm_halo != 1 || a.tv) return 0;  // (the halo image masks by the uniform T_in only)
   const int taps = a.Cp > 0 ? a.K / a.Cp : 0;
   if (!(a.Cp % 64 == 0 && a.K == a.Kpad && taps >= 2 && a.istride == 1 && a.T_in == a.T_out)) return 0;
   const int h = std::max(std::abs(a.tap_add), std::abs((taps - 1) * a.tap_mul + a.tap_add));
   return h >= 1 && h <= 32 ? h : 0;
 }
 
-// Register epilogue form of a generic epilogue (G3_LDS when it has none). SVC_GEMM3_DIRECT is a mask of the forms in
+// Register epilogue form of a generic epilogue (G3_LDS when it has none). tuning gemm3_direct is a mask of the forms in
 // use: 1 = G3_F16, 2 = G3_RES32, 4 = G3_SPLIT, 8 = also inside the DiffSVC sampler (run_gemm sets no_reg_epi there
 // otherwise); default 3, 0 = the LDS epilogue everywhere. Alone every form is as fast or faster (Whisper fc1 12 %,
 // the DiffSVC 3-tap store 12 %, skip sum 3 %); inside the 3-stream sampler the gate GEMMs beside them ran slower.
 static int direct_form3(const ConvGemmArgs& a, const EpiArgs& e) {
-  const char* v = getenv("SVC_GEMM3_DIRECT");  // read per call (A/B runs and tests switch it)
-  const int mask = v ? atoi(v) : 3;
+  const int mask = tuning().gemm3_direct;
   if (e.no_reg_epi || e.kind != EPI_GENERIC || e.add_t) return G3_LDS;
   const bool acc16 = e.acc16_hi || e.acc16_lo || e.acc_sub || e.lo16;
   if (e.out16 && !e.out32 && !e.add_row && !e.acc32 && !acc16 && !e.add16) return (mask & 1) ? G3_F16 : G3_LDS;

@@ -23,8 +23,6 @@ overlap-add seams.
 """
 from dataclasses import dataclass
 
-import os
-
 import torch
 
 from .runtime import SVCEngine, mel_frames
@@ -44,8 +42,11 @@ class ConvertResult:
 
 
 class SVCPipeline:
-    def __init__(self, engine: SVCEngine):
+    def __init__(self, engine: SVCEngine, f0_side=True):
+        """f0_side: run the 24 kHz features (mel / energy, F0, pitch shift) on the context's sub-stream 2 beside the
+        content encoder (default; measured +0.4 %) instead of on the caller's stream."""
         self.engine = engine
+        self.f0_side = f0_side
 
     def content(self, wav16, T, wav16_float=None):
         """Content features of every type in cfg.mapper.content_feature mapped to T mel frames -> f16
@@ -106,7 +107,7 @@ class SVCPipeline:
         # run on the context's sub-stream 2 beside the content encoder (they use their own workspace), joined before
         # the conditioner needs them
         main = torch.cuda.current_stream(wav24.device)
-        side = self._side_stream(wav24.device) if os.environ.get("SVC_F0_SIDE", "1") != "0" else main
+        side = self._side_stream(wav24.device) if self.f0_side else main
         side.wait_stream(main)
         with torch.cuda.stream(side):
             mel, energy = e.mel_energy(wav24)
@@ -224,7 +225,7 @@ class SVCPipeline:
         T_b = [mel_frames(k, e.cfg.n_fft, e.cfg.hop_length) for k in n24]
         T = max(T_b)
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream(dev) if os.environ.get("SVC_F0_SIDE", "1") != "0" else main
+        side = self._side_stream(dev) if self.f0_side else main
         side.wait_stream(main)
         with torch.cuda.stream(side):
             mel, energy = e.mel_energy(w24, n_samples=n24)

@@ -161,6 +161,13 @@ class SVCEngine:
         _lib.call("svc_ctx_memory", self._ctx, ctypes.byref(wb), ctypes.byref(wsb))
         return wb.value, wsb.value
 
+    def tune(self, **switches):
+        """Kernel switches of this context (csrc/common.h Tuning: A/B runs and parity tests), e.g.
+        tune(sampler_streams=1); tune(reset=1) restores the values at creation (defaults, SVC_<NAME> environment)."""
+        if not self._ctx:
+            raise _lib.SVCError("tune: the engine is closed")
+        _lib.tune(self._ctx, **switches)
+
     # ------------------------------------------------------------------ stages
     def mel_energy(self, wav24, n_samples=None):
         """wav24 f32 [B, N] -> (log-mel f32 [B, T, n_mels], energy f32 [B, T]) — utils/mel.py:179-201.

@@ -21,3 +21,26 @@ def golden():
     def load(name):
         return np.load(os.path.join(GOLDEN, name + ".npz"))
     return load
+
+
+@pytest.fixture
+def tune():
+    """Kernel switches for one test (include/svc_hip.h, svc_ctx_set_config "tune.<name>"): tune(target, name=value, ...)
+    on an SVCEngine, or with target None on the op-level entry points' context. Every context touched is reset to its
+    creation-time switches when the test ends."""
+    from svc_inference_pipeline_amd import _lib
+    touched = {}
+
+    def set_(target, **kv):
+        if target is None:
+            _lib.tune(None, **kv)
+        else:
+            target.tune(**kv)
+        touched[id(target)] = target
+
+    yield set_
+    for target in touched.values():
+        if target is None:
+            _lib.tune(None, reset=1)
+        elif target._ctx:  # (an engine the test closed itself has nothing left to reset)
+            target.tune(reset=1)

@@ -20,7 +20,7 @@ def _tm(x):  # [B, C, T] -> time-major [B*T, C]
     return x.permute(0, 2, 1).contiguous()
 
 
-# (SVC_GEMM_VARIANT, SVC_GEMM_HALO, SVC_GEMM3_DIRECT): every kernel variant with the defaults, and the conv_gemm3
+# (gemm_variant, gemm_halo, gemm3_direct kernel switches): every kernel variant with the defaults, and the conv_gemm3
 # tap-reuse / LDS-epilogue switches only where they change the schedule (no skip-only combinations are collected)
 _GEMM_MODES = ([(v, "1", "15") for v in ("-1", "10", "11", "12", "13", "14", "15", "20", "24")] +
                [(v, "0", d) for v in ("10", "14", "15") for d in ("15", "0")])
@@ -45,10 +45,10 @@ _GEMM_MODES = ([(v, "1", "15") for v in ("-1", "10", "11", "12", "13", "14", "15
     (1, 90, 128, 256, 7, 1, 7, 21, 0),       # |shift| 21, T < tile
 ])
 @pytest.mark.parametrize("variant,halo,direct", _GEMM_MODES)
-def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, halo, direct, monkeypatch):
-    monkeypatch.setenv("SVC_GEMM_VARIANT", variant)  # -1: v1, 10..14: conv_gemm3 tiles, 15: auto, 20/24: conv_gemm4
-    monkeypatch.setenv("SVC_GEMM_HALO", halo)        # conv_gemm3 tap reuse (multi-tap, Cin % 64 == 0, |shift| <= 32)
-    monkeypatch.setenv("SVC_GEMM3_DIRECT", direct)   # conv_gemm3 register epilogues (all forms) or LDS-staged C tile
+def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, halo, direct, tune):
+    # gemm_variant -1: v1, 10..14: conv_gemm3 tiles, 15: auto, 20/24: conv_gemm4; gemm_halo: conv_gemm3 tap reuse
+    # (multi-tap, Cin % 64 == 0, |shift| <= 32); gemm3_direct: conv_gemm3 register epilogues (all forms) or LDS C tile
+    tune(None, gemm_variant=variant, gemm_halo=halo, gemm3_direct=direct)
     g = torch.Generator().manual_seed(0)
     x = torch.randn(B, Cin, T, generator=g)
     w = torch.randn(Cout, Cin, k, generator=g) / np.sqrt(Cin * k)
@@ -66,8 +66,8 @@ def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, halo, direct
 @pytest.mark.parametrize("B,T,Cin,Cout,k,s", [(2, 25, 768, 384, 8, 4), (1, 40, 96, 48, 4, 2), (2, 33, 48, 24, 4, 2),
                                               (1, 9, 1536, 768, 8, 4)])
 @pytest.mark.parametrize("variant", ["-1", "10", "14", "15", "20", "24"])
-def test_conv_transpose1d(B, T, Cin, Cout, k, s, variant, monkeypatch):
-    monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
+def test_conv_transpose1d(B, T, Cin, Cout, k, s, variant, tune):
+    tune(None, gemm_variant=variant)
     g = torch.Generator().manual_seed(1)
     x = torch.randn(B, Cin, T, generator=g)
     w = torch.randn(Cin, Cout, k, generator=g) / np.sqrt(Cin * k / s)
@@ -86,8 +86,8 @@ def test_conv_transpose1d(B, T, Cin, Cout, k, s, variant, monkeypatch):
 @pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
 @pytest.mark.parametrize("B,L,C", [(2, 37, 24), (1, 1, 24), (1, 2, 48), (1, 3, 8), (2, 11, 12), (3, 129, 96),
                                    (1, 300, 768), (2, 64, 40), (2, 257, 48)])
-def test_activation1d(B, L, C, variant, monkeypatch):
-    monkeypatch.setenv("SVC_ACT_VARIANT", variant)
+def test_activation1d(B, L, C, variant, tune):
+    tune(None, act_variant=variant)
     from svc_inference_pipeline_amd import weights as W
     g = torch.Generator().manual_seed(2)
     x = torch.randn(B, C, L, generator=g) * 2
@@ -108,11 +108,11 @@ def test_activation1d(B, L, C, variant, monkeypatch):
 @pytest.mark.parametrize("C", [24, 48, 96])
 @pytest.mark.parametrize("B,L,k,d", [(2, 37, 3, 1), (1, 1, 11, 5), (1, 5, 7, 3), (2, 130, 11, 5), (1, 300, 7, 3),
                                      (3, 257, 11, 1)])
-def test_amp_conv(B, L, k, d, C, mode, monkeypatch):
+def test_amp_conv(B, L, k, d, C, mode, tune):
     """Fused SnakeBeta Activation1d -> dilated conv -> bias + residual (BigVGAN C <= 96 stages), in every kernel form
-    (SVC_AMP_MODE: 3 = default packed channel-pair activation, 2 = packed for C = 48 only, 1 / 0 = scalar activation
+    (amp_mode: 3 = default packed channel-pair activation, 2 = packed for C = 48 only, 1 / 0 = scalar activation
     with / without the occupancy launch bound)."""
-    monkeypatch.setenv("SVC_AMP_MODE", mode)
+    tune(None, amp_mode=mode)
     from svc_inference_pipeline_amd import weights as W
     g = torch.Generator().manual_seed(5)
     x = torch.randn(B, C, L, generator=g) * 2

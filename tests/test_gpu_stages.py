@@ -57,10 +57,10 @@ def test_mel_energy(engine, cfg, golden):
 
 
 @pytest.mark.parametrize("direct", ["15", "0"])
-def test_whisper_encoder_tiny(engine, golden, direct, monkeypatch):
+def test_whisper_encoder_tiny(engine, golden, direct, tune):
     """Whisper encoder against the reference-pinned golden, with conv_gemm3's register epilogues (qkv / fc1: f16
-    outputs, out / fc2: f32 residual) and with the LDS-staged epilogue (SVC_GEMM3_DIRECT=0)."""
-    monkeypatch.setenv("SVC_GEMM3_DIRECT", direct)
+    outputs, out / fc2: f32 residual) and with the LDS-staged epilogue (gemm3_direct = 0)."""
+    tune(engine, gemm3_direct=direct)
     g = golden("whisper_logmel")
     wav16 = g["wav16"]
     feats = engine.whisper_encode(dev(wav16[None]))
@@ -68,16 +68,16 @@ def test_whisper_encoder_tiny(engine, golden, direct, monkeypatch):
     assert rel_l2(feats[0].cpu().numpy(), ref) < 5e-3
 
 
-def test_whisper_stream_split(engine, golden, monkeypatch):
-    """SVC_WHISPER_STREAMS = 2 / 3 (utterance-aligned sub-batches on concurrent streams) against the default single
+def test_whisper_stream_split(engine, golden, tune):
+    """whisper_streams = 2 / 3 (utterance-aligned sub-batches on concurrent streams) against the default single
     full-batch stream, on a batch of 3 clips; the sub-batch launches may pick other GEMM tiles, so the bound is fp32
     rounding, not bit equality."""
     g = golden("whisper_logmel")
     w = dev(np.stack([g["wav16"], g["wav16"][::-1].copy(), 0.5 * g["wav16"]]))
-    monkeypatch.setenv("SVC_WHISPER_STREAMS", "1")
+    tune(engine, whisper_streams=1)
     one = engine.whisper_encode(w).cpu().numpy()
     for ns in ("2", "3"):
-        monkeypatch.setenv("SVC_WHISPER_STREAMS", ns)
+        tune(engine, whisper_streams=ns)
         split = engine.whisper_encode(w).cpu().numpy()
         for b in range(3):
             assert rel_l2(split[b], one[b]) < 1e-4, (ns, b)
@@ -111,32 +111,26 @@ def test_eps_single_step(engine, cfg, states, golden):
         assert rel_l2(eps.cpu().numpy(), g[f"eps_t{t}"]) < 5e-3, t
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700)])
-def test_fused_layer_vs_oracle(engine, states, cfg, fused, B, T, monkeypatch):
-    """The fused residual-layer kernel (diff_layer.hip, opt-in) and the default GEMM path against the oracle on
-    ragged shapes (B*T not a multiple of the 64-row tile, utterance boundaries inside a tile), and against each
-    other: relative L2 <= 5e-3 vs the oracle (fp16 operands), <= 2e-3 between the two HIP paths."""
+def test_denoiser_vs_oracle(engine, states, cfg, B, T):
+    """The denoiser (tiled GEMMs with the paired gate epilogue, the split-fp16 residual stream, the skip-sum GEMM)
+    against the oracle on ragged shapes (B*T not a multiple of the GEMM tiles, utterance boundaries inside a tile):
+    relative L2 <= 5e-3 (fp16 operands)."""
     rng = np.random.default_rng(B * 1000 + T)
     cond = rng.standard_normal((B, T, 384)).astype(np.float32)
     x = rng.standard_normal((B, T, 100)).astype(np.float32)
     table = W.step_embedding_table(1000)
-    monkeypatch.setenv("SVC_DIFF_FUSED", fused)
     for t in (3, 640):
         eps = engine.diffsvc_eps(dev(cond), dev(x), t).cpu().numpy()
         with torch.no_grad():
             ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond),
                                      torch.full((B,), t, dtype=torch.long), table).numpy()
         assert rel_l2(eps, ref) < 5e-3, (t, rel_l2(eps, ref))
-        monkeypatch.setenv("SVC_DIFF_FUSED", "1" if fused == "0" else "0")
-        other = engine.diffsvc_eps(dev(cond), dev(x), t).cpu().numpy()
-        monkeypatch.setenv("SVC_DIFF_FUSED", fused)
-        assert rel_l2(eps, other) < 2e-3
 
 
 @pytest.mark.parametrize("variant", ["20", "24", "rmw", "rmw32"])
 @pytest.mark.parametrize("B,T", [(3, 50), (2, 700), (5, 937)])
-def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, monkeypatch):
+def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, tune):
     """The DiffSVC gate GEMM kernels (LDS-staged and in-register gate epilogues) and the register
     residual epilogue of the output projection (rmw: split-fp16 residual, rmw32: f32 residual) on ragged row counts
     (B*T not a multiple of the 128-row tile, utterance boundaries inside tiles) against the oracle's eps."""
@@ -145,11 +139,9 @@ def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, monkeypatch):
     x = rng.standard_normal((B, T, 100)).astype(np.float32)
     table = W.step_embedding_table(1000)
     if variant.startswith("rmw"):
-        monkeypatch.setenv("SVC_GEMM4_RMW", "1")
-        monkeypatch.setenv("SVC_DIFF_RES32", "1" if variant == "rmw32" else "0")
+        tune(engine, gemm4_rmw=1, diff_res32=int(variant == "rmw32"))
         variant = "15"
-    monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
-    monkeypatch.setenv("SVC_DIFF_FUSED", "0")
+    tune(engine, gemm_variant=variant)
     eps = engine.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()
     with torch.no_grad():
         ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond),
@@ -158,14 +150,13 @@ def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, monkeypatch):
 
 
 @pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "24"])
-def test_eps_gemm_variants(engine, golden, variant, monkeypatch):
+def test_eps_gemm_variants(engine, golden, variant, tune):
     """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path); 15lds:
     conv_gemm3 with the LDS-staged epilogue everywhere; 15reg: with every register form, in the sampler too."""
     if variant in ("15lds", "15reg"):
-        monkeypatch.setenv("SVC_GEMM3_DIRECT", "0" if variant == "15lds" else "15")
+        tune(engine, gemm3_direct=0 if variant == "15lds" else 15)
         variant = "15"
-    monkeypatch.setenv("SVC_GEMM_VARIANT", variant)
-    monkeypatch.setenv("SVC_DIFF_FUSED", "0")
+    tune(engine, gemm_variant=variant)
     g = golden("conditioner_diffsvc")
     eps = engine.diffsvc_eps(dev(g["cond"]), dev(g["x_in"]), 500)
     assert rel_l2(eps.cpu().numpy(), g["eps_t500"]) < 5e-3
@@ -184,7 +175,7 @@ def test_plms_and_ddpm(engine, cfg, states, golden):
     assert rel_l2(x[0].cpu().numpy().T, g["ddpm1000"]) < 2e-2
 
 
-def test_sampler_sub_streams_bit_identical(engine, golden, monkeypatch):
+def test_sampler_sub_streams_bit_identical(engine, golden, tune):
     """Utterance-aligned sub-batches on 2-3 streams (the default sampler schedule) reproduce the single-stream
     result bit for bit, for PLMS and for DDPM with device noise, including an uneven split (B = 3)."""
     g = golden("conditioner_diffsvc")
@@ -192,7 +183,7 @@ def test_sampler_sub_streams_bit_identical(engine, golden, monkeypatch):
     utt = dev(np.array([5, 6, 7]), torch.int32)
     outs = {}
     for ns in ("1", "2", "3"):
-        monkeypatch.setenv("SVC_SAMPLER_STREAMS", ns)
+        tune(engine, sampler_streams=ns)
         plms = engine.diffsvc_sample(cond, fast_inference=True, speedup=250, seed=9, utt_ids=utt).cpu().numpy()
         ddpm = engine.diffsvc_sample(cond, fast_inference=False, seed=9, utt_ids=utt).cpu().numpy()
         outs[ns] = (plms, ddpm)
@@ -201,8 +192,8 @@ def test_sampler_sub_streams_bit_identical(engine, golden, monkeypatch):
 
 
 @pytest.mark.parametrize("direct", ["15", "0"])
-def test_bigvgan(engine, cfg, states, golden, direct, monkeypatch):
-    monkeypatch.setenv("SVC_GEMM3_DIRECT", direct)  # conv_gemm3 register epilogues (default) or the LDS-staged one
+def test_bigvgan(engine, cfg, states, golden, direct, tune):
+    tune(engine, gemm3_direct=direct)  # conv_gemm3 register epilogues (default) or the LDS-staged one
     g = golden("bigvgan")
     stats = C.load_stats(cfg)
     mel = g["mel"]  # de-normalised mel [100, T]
@@ -220,10 +211,10 @@ def test_bigvgan(engine, cfg, states, golden, direct, monkeypatch):
 
 
 @pytest.mark.parametrize("variant", list(W.VOCODER_VARIANTS))
-def test_bigvgan_variants(cfg, states, golden, variant, monkeypatch):
+def test_bigvgan_variants(cfg, states, golden, variant, tune):
     """F4: AMPBlock2 / Snake (log and linear scale) generators against the oracle, which
     tests/test_oracle_golden.py::test_bigvgan_variants pins to the reference's own Generator. Both the fused
-    small-channel path (amp_conv, C <= 48) and the unfused activation1d + GEMM path (SVC_AMP_MAXC=0) are checked,
+    small-channel path (amp_conv, C <= 48) and the unfused activation1d + GEMM path (amp_maxc = 0) are checked,
     with test_bigvgan's tolerance (1.5 x the fp16-operand emulation's distance + 1e-3)."""
     import copy
     g = golden("bigvgan_variants")
@@ -241,20 +232,20 @@ def test_bigvgan_variants(cfg, states, golden, variant, monkeypatch):
     e = SVCEngine(c2, 0, mapper_state=states["mapper"], vocoder_state=vsd)
     try:
         for maxc in ("48", "0"):
-            monkeypatch.setenv("SVC_AMP_MAXC", maxc)
+            tune(e, amp_maxc=maxc)
             wav = e.bigvgan(dev(x_norm.T[None].astype(np.float32)))[0].cpu().numpy()
             assert rel_l2(wav, ref) < budget, (maxc, rel_l2(wav, ref), budget)
     finally:
         e.close()
 
 
-def test_vocoder_sub_streams_bit_identical(engine, monkeypatch):
+def test_vocoder_sub_streams_bit_identical(engine, tune):
     """BigVGAN with utterance-aligned sub-batches on 1, 2 or 3 streams: identical waveforms."""
     rng = np.random.default_rng(1)
     x = dev(rng.uniform(-1, 1, (3, 40, 100)).astype(np.float32))
     outs = {}
     for ns in ("1", "2", "3"):
-        monkeypatch.setenv("SVC_VOCODER_STREAMS", ns)
+        tune(engine, vocoder_streams=ns)
         outs[ns] = engine.bigvgan(x).cpu().numpy()
     assert np.array_equal(outs["2"], outs["1"]) and np.array_equal(outs["3"], outs["1"])
 

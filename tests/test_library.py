@@ -50,3 +50,15 @@ def test_no_gpu_error_is_loud():
     ctx = ctypes.c_void_p()
     st = _lib.load().svc_ctx_create(0, ctypes.byref(ctx))
     assert st != 0 and _lib.load().svc_last_error()
+
+
+def test_kernel_switches_are_per_context_config():
+    """Kernel switches go through svc_ctx_set_config("tune.<name>") (here on the op-level context, ctx NULL; no GPU
+    call is made): known names are accepted, unknown ones are rejected loudly, "tune.reset" restores the defaults."""
+    import pytest
+    _lib.tune(None, gemm_variant=24, sampler_streams=1, amp_maxc=0)
+    _lib.tune(None, reset=1)
+    with pytest.raises(_lib.SVCError, match="unknown kernel switch"):
+        _lib.tune(None, no_such_switch=1)
+    with pytest.raises(_lib.SVCError, match="null context"):
+        _lib.call("svc_ctx_set_config", None, b"mapper.n_mel", 100.0)

@@ -100,11 +100,10 @@ class _FakeEngine:
 
 def test_convert_many_is_one_ragged_batch(monkeypatch):
     import contextlib
-    monkeypatch.setenv("SVC_F0_SIDE", "0")
     monkeypatch.setattr(torch.cuda, "current_stream", lambda *a: types.SimpleNamespace(wait_stream=lambda s: None))
     monkeypatch.setattr(torch.cuda, "stream", lambda s: contextlib.nullcontext())
     eng = _FakeEngine()
-    pipe = SVCPipeline(eng)
+    pipe = SVCPipeline(eng, f0_side=False)
     lens = [2400, 4800, 24000, 1000]
     w24 = [torch.zeros(n) for n in lens]
     w16 = [torch.full((n * 2 // 3,), float(i + 1)) for i, n in enumerate(lens)]  # marker = position + 1

@@ -1,4 +1,4 @@
-"""Activation1d microbenchmark (GPU): achieved GB/s of each SVC_ACT_VARIANT on the BigVGAN stage shapes
+"""Activation1d microbenchmark (GPU): achieved GB/s of each activation1d kernel form (kernel switch act_variant) on the BigVGAN stage shapes
 (B = 32 clips x 10 s). Algorithmic bytes = 4 (f32 in) + 2 (f16 out) per element.
 Usage: python tools/act_bench.py [variant ...]"""
 import os
@@ -7,6 +7,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
+from svc_inference_pipeline_amd import _lib  # noqa: E402
 from svc_inference_pipeline_amd._lib import call, profile_enable, profile_read  # noqa: E402
 
 SHAPES = [(32, 3748, 768), (32, 14992, 384), (32, 29984, 192), (32, 119936, 48), (32, 239872, 24)]
@@ -23,7 +24,7 @@ def main():
         f = torch.rand(12, device="cuda")
         row = []
         for v in variants:
-            os.environ["SVC_ACT_VARIANT"] = v
+            _lib.tune(None, act_variant=int(v))
             args = (x.data_ptr(), B, L, C, al.data_ptr(), be.data_ptr(), f.data_ptr(), y.data_ptr(), s)
             call("svc_op_activation1d", *args)
             torch.cuda.synchronize()

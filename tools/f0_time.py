@@ -1,4 +1,4 @@
-"""F0 (Praat AC) kernel timing on B = 32 x 10 s synthetic clips, with the diagnostic phase cuts of SVC_F0_DBG
+"""F0 (Praat AC) kernel timing on B = 32 x 10 s synthetic clips, with the diagnostic phase cuts of the f0_dbg kernel switch
 (1 = autocorrelation only, 2 = no Brent refinement). Usage: python tools/f0_time.py"""
 import os
 import sys
@@ -18,10 +18,7 @@ def main():
     wav = torch.from_numpy(np.stack([synth_clip(i, 10.0, 24000) for i in range(32)])).cuda()
     T = (wav.shape[1] + 768 - 1024) // 256 + 1
     for mode in ("", "1", "2", ""):
-        if mode:
-            os.environ["SVC_F0_DBG"] = mode
-        else:
-            os.environ.pop("SVC_F0_DBG", None)
+        eng.tune(f0_dbg=int(mode or 0))
         eng.f0(wav, T)
         torch.cuda.synchronize()
         t0 = time.time()
@@ -29,7 +26,6 @@ def main():
             eng.f0(wav, T)
         torch.cuda.synchronize()
         print("mode", mode or "full", round((time.time() - t0) / 3 * 1000, 2), "ms", flush=True)
-    os.environ.pop("SVC_F0_DBG", None)
 
 
 if __name__ == "__main__":
