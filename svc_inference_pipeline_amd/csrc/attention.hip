@@ -7,25 +7,65 @@
 // 32 queries (two 16-column fragments). Scores are computed TRANSPOSED (S^T = K Q^T) so that a
 // lane's accumulator column is one query: the row max / row sum need only two cross-lane shuffles
 // (xor 16, xor 32), and the f32 accumulator, converted to f16, is directly the B operand of
-// O^T = V^T P^T (k-order permuted; V^T staged in LDS with the same permutation read as 2 x b64).
+// O^T = V^T P^T (k-order permuted). V stays row-major in LDS (one ds_write_b128 per 8 values, as K) and the V^T
+// A operand is read with gfx950's transposing ds_read_b64_tr_b16 (a 16-lane group reads 4 keys x 16 head columns and
+// each lane receives its column), from an image whose 16-B chunks are XOR-swizzled so those reads are conflict-free.
+// Softmax VALU work: the key mask only on the last tile, exp2 arguments as one FMA, and the O rescale skipped when no
+// lane of the wave raised its running max (alpha is then exactly 1, so the result is unchanged).
 #include "common.h"
 
 namespace svc {
 
 constexpr int ATT_QT = 128;   // queries per workgroup
 constexpr int ATT_KT = 64;    // keys per tile
-constexpr int VT_LD = 68;     // padded row (f16) of the V^T image: conflict-free ds_read_b64
 
 __device__ __forceinline__ int kswz(int row, int kv) { return row * 64 + ((kv ^ ((row >> 1) & 7)) << 3); }
+// V image: [key][64 f16] rows, 16-B chunk c of row r stored at chunk c ^ (((r >> 1) & 3) << 1). A transposing read of
+// keys r0 + 4g + q (q < 4), head columns 16df + 4p (p < 4) then maps the 32 lanes of a half (g < 2) to distinct
+// (r & 1, chunk, 8-B half) = 64 distinct banks; the row-major ds_write_b128 of 8 lanes covers one whole 128-B row.
+__device__ __forceinline__ int vswz(int row, int c) { return row * 64 + ((c ^ (((row >> 1) & 3) << 1)) << 3); }
 
-__global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict__ qkv, f16* __restrict__ out, int L,
+// cross-lane reductions over the lane pairs (l, l ^ 16) and (l, l ^ 32) on the VALU (gfx950 v_permlane16/32_swap: each
+// lane ends up holding its own value and its partner's), instead of ds_bpermute round trips through the LDS crossbar
+__device__ __forceinline__ float max_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_xor16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef float float2v __attribute__((ext_vector_type(2)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+typedef _Float16 half4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ half4v lds_tr16(const f16* p) {
+  return __builtin_bit_cast(half4v, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)p));
+}
+
+__global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict__ qkv, f16* __restrict__ out, int L,
                                                            int D) {
   // double-buffered K / V^T tiles: tile kt + 1 is loaded into registers while tile kt is multiplied, then written to
   // the other buffer (one barrier per tile)
   __shared__ __align__(16) f16 Ksb[2][ATT_KT * 64];
-  __shared__ __align__(16) f16 Vtb[2][64 * VT_LD];
+  __shared__ __align__(16) f16 Vsb[2][ATT_KT * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int qblk = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+  // 1-D grid, remapped so that consecutive logical workgroups (the query blocks of one utterance and head, which read
+  // the same K / V) run on one XCD: K / V are fetched into each XCD's L2 once instead of by all eight
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int nq = (L + ATT_QT - 1) / ATT_QT, H = D / 64;
+  const int qblk = wg % nq, h = (wg / nq) % H, b = wg / (nq * H);
   const int ld = 3 * D;
   const f16* base = qkv + (int64_t)b * L * ld;
   const int qw0 = qblk * ATT_QT + wave * 32;  // first query of this wave
@@ -65,25 +105,24 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict
       }
     }
   };
-  auto lstore = [&](int buf) {  // K row-major (swizzled), V transposed
+  auto lstore = [&](int buf) {  // K and V row-major (swizzled)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int v = tid + 256 * i;
       const int row = v >> 3, kvv = v & 7;
       *reinterpret_cast<uint4*>(Ksb[buf] + kswz(row, kvv)) = kreg[i];
-      union { uint4 u; f16 e[8]; } vv;
-      vv.u = vreg[i];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) Vtb[buf][(kvv * 8 + j) * VT_LD + row] = vv.e[j];
+      *reinterpret_cast<uint4*>(Vsb[buf] + vswz(row, kvv)) = vreg[i];
     }
   };
+  // transposing-read lane roles: lane 4q + p of its 16-lane group supplies key row q, head columns 4p .. 4p + 3
+  const int trq = c16 >> 2, trp = c16 & 3;
   gload(0);
   lstore(0);
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const int k0 = kt * ATT_KT;
     const f16* Ks = Ksb[kt & 1];
-    const f16* Vt = Vtb[kt & 1];
+    const f16* Vs = Vsb[kt & 1];
     if (kt + 1 < ntiles) gload(kt + 1);  // lands while this tile is multiplied
 
     // ---- S^T = K Q^T : s[kf][f][r] = S[q = f*16 + c16][key = kf*16 + 4g + r]
@@ -100,58 +139,64 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict
       }
     }
     // ---- online softmax per query column
+    const bool tail = k0 + ATT_KT > L;  // keys past L only in the last tile (wave-uniform)
     half8 pb[2][2];  // P^T as B operand: [f][ks'] element j <-> key 32ks' + 4g + (j&3) + 16(j>>2)
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
+      if (tail) {
+#pragma unroll
+        for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (k0 + kf * 16 + 4 * g + r >= L) s[kf][f][r] = -INFINITY;
+      }
       float mx = -INFINITY;
 #pragma unroll
       for (int kf = 0; kf < 4; ++kf)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int key = k0 + kf * 16 + 4 * g + r;
-          float v = key < L ? s[kf][f][r] : -INFINITY;
-          s[kf][f][r] = v;
-          mx = fmaxf(mx, v);
-        }
-      mx = fmaxf(mx, __shfl_xor(mx, 16));
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
+        mx = fmaxf(fmaxf(mx, fmaxf(s[kf][f][0], s[kf][f][1])), fmaxf(s[kf][f][2], s[kf][f][3]));
+      mx = max_xor32(max_xor16(mx));
       const float mnew = fmaxf(mrun[f], mx);
-      const float alpha = __builtin_amdgcn_exp2f((mrun[f] - mnew) * LOG2E);  // v_exp_f32 (arguments <= 0)
+      const float msc = mnew * LOG2E;
+      const float alpha = __builtin_amdgcn_exp2f(fmaf(mrun[f], LOG2E, -msc));  // v_exp_f32 (arguments <= 0)
+      const bool grew = mnew != mrun[f];
       mrun[f] = mnew;
-      float psum = 0.f;
-      float p[4][4];
+      // exponent arguments, row sum and f16 conversion on packed f32 pairs (v_pk_fma_f32, v_pk_add_f32,
+      // v_cvt_pk_f16_f32): half the VALU issue slots of the scalar forms; only v_exp_f32 stays per element
+      const float2v l2e = {LOG2E, LOG2E}, nm = {-msc, -msc};
+      float2v psum2 = {0.f, 0.f};
+      half2v ph[4][2];
 #pragma unroll
       for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          p[kf][r] = __builtin_amdgcn_exp2f((s[kf][f][r] - mnew) * LOG2E);
-          psum += p[kf][r];
+        for (int hh = 0; hh < 2; ++hh) {
+          float2v a = (float2v){s[kf][f][2 * hh], s[kf][f][2 * hh + 1]} * l2e + nm;
+          a.x = __builtin_amdgcn_exp2f(a.x);
+          a.y = __builtin_amdgcn_exp2f(a.y);
+          psum2 += a;
+          ph[kf][hh] = __builtin_convertvector(a, half2v);
         }
-      lrun[f] = lrun[f] * alpha + psum;
+      lrun[f] = lrun[f] * alpha + (psum2.x + psum2.y);
+      if (__ballot(grew)) {  // alpha == 1 exactly in every lane that did not raise its max
 #pragma unroll
-      for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        half8 hv;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          hv[j] = (f16)p[2 * ks][j];
-          hv[4 + j] = (f16)p[2 * ks + 1][j];
-        }
-        pb[f][ks] = hv;
+        for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
       }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        pb[f][ks] = (half8){ph[2 * ks][0].x, ph[2 * ks][0].y, ph[2 * ks][1].x, ph[2 * ks][1].y,
+                            ph[2 * ks + 1][0].x, ph[2 * ks + 1][0].y, ph[2 * ks + 1][1].x, ph[2 * ks + 1][1].y};
     }
     // ---- O^T += V^T P^T
 #pragma unroll
     for (int df = 0; df < 4; ++df) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const f16* vrow = Vt + (df * 16 + c16) * VT_LD + ks * 32 + 4 * g;
-        union { uint2 u[2]; half8 h; } va;
-        va.u[0] = *reinterpret_cast<const uint2*>(vrow);
-        va.u[1] = *reinterpret_cast<const uint2*>(vrow + 16);
+        // A operand V^T[d = 16df + c16][keys 32ks + 4g + 0..3 | + 16]: two transposing reads of 4 keys x 16 columns
+        const int r0 = ks * 32 + 4 * g + trq, c = 2 * df + (trp >> 1), e = 4 * (trp & 1);
+        const half4v lo = lds_tr16(Vs + vswz(r0, c) + e);
+        const half4v hi = lds_tr16(Vs + vswz(r0 + 16, c) + e);
+        const half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int f = 0; f < 2; ++f) o[df][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va.h, pb[f][ks], o[df][f], 0, 0, 0);
+        for (int f = 0; f < 2; ++f) o[df][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[f][ks], o[df][f], 0, 0, 0);
       }
     }
     if (kt + 1 < ntiles) lstore((kt + 1) & 1);  // that buffer was last read in iteration kt - 1, before its barrier
@@ -162,8 +207,7 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
     float l = lrun[f];
-    l += __shfl_xor(l, 16);
-    l += __shfl_xor(l, 32);
+    l = sum_xor32(sum_xor16(l));
     const float inv = 1.0f / l;
     const int q = qw0 + f * 16 + c16;
     if (q >= L) continue;
@@ -180,7 +224,9 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(const f16* __restrict
 
 int attention(const f16* qkv, f16* out, int B, int L, int D, hipStream_t s) {
   SVC_REQUIRE(D % 64 == 0 && L > 0 && B > 0, "attention: bad shape B=%d L=%d D=%d", B, L, D);
-  dim3 grid((L + ATT_QT - 1) / ATT_QT, D / 64, B);
+  const int64_t nwg = (int64_t)((L + ATT_QT - 1) / ATT_QT) * (D / 64) * B;
+  SVC_REQUIRE(nwg < (1ll << 31), "attention: grid");
+  dim3 grid((unsigned)nwg);
   const int tok = prof_begin("attention", 4.0 * B * (double)L * L * D, 0.0, s);
   hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, L, D);
   prof_end(tok, s);

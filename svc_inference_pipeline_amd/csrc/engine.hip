@@ -2552,7 +2552,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   svc_ctx* oc;
   op_ws(&oc);
   TuningScope tuning_scope_(&oc->tune);
-  SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters >= 1, "gemm_bench: bad args");
+  SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters != 0, "gemm_bench: bad args");
   SVC_REQUIRE(epi_kind < 3 || epi_kind == 6 || variant == 24,
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
@@ -2593,19 +2593,39 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_HIP_CHECK(hipEventCreate(&e0));
   SVC_HIP_CHECK(hipEventCreate(&e1));
   int st = SVC_OK;
+  // iters < 0: |iters| launches each after a 1 GiB memset (operands evicted from L2 and the 256 MiB Infinity Cache,
+  // as inside the sampler, where other layers' buffers stream between two launches of one GEMM), timed one by one
+  const bool cold = iters < 0;
+  if (cold) iters = -iters;
+  void* flush = nullptr;
+  if (cold) SVC_HIP_CHECK(hipMalloc(&flush, (size_t)1 << 30));
   auto run = [&]() {
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, 0);
     return conv_gemm(a, e, 0);
   };
   for (int w = 0; w < 2 && !st; ++w) st = run();
-  SVC_HIP_CHECK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters && !st; ++i)
-    st = run();
-  SVC_HIP_CHECK(hipEventRecord(e1, 0));
-  SVC_HIP_CHECK(hipEventSynchronize(e1));
   float ms = 0;
-  SVC_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  if (cold) {
+    for (int i = 0; i < iters && !st; ++i) {
+      SVC_HIP_CHECK(hipMemsetAsync(flush, i & 0xff, (size_t)1 << 30, 0));
+      SVC_HIP_CHECK(hipEventRecord(e0, 0));
+      st = run();
+      SVC_HIP_CHECK(hipEventRecord(e1, 0));
+      SVC_HIP_CHECK(hipEventSynchronize(e1));
+      float one = 0;
+      SVC_HIP_CHECK(hipEventElapsedTime(&one, e0, e1));
+      ms += one;
+    }
+    (void)hipFree(flush);
+  } else {
+    SVC_HIP_CHECK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters && !st; ++i)
+      st = run();
+    SVC_HIP_CHECK(hipEventRecord(e1, 0));
+    SVC_HIP_CHECK(hipEventSynchronize(e1));
+    SVC_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+  }
   *ms_out = ms / iters;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);

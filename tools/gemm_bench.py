@@ -40,7 +40,9 @@ def main():
             if v < 0 and epi == 1:  # v1 has no paired gate epilogue
                 continue
             ms = ctypes.c_double()
-            _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, 10, ctypes.byref(ms))
+            # GEMM_BENCH_COLD=1: each launch after a 1 GiB memset (operands not cache-resident, as in the sampler)
+            iters = -10 if os.environ.get("GEMM_BENCH_COLD") == "1" else 10
+            _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, iters, ctypes.byref(ms))
             tf = 2.0 * M * N * Cin * taps / (ms.value * 1e-3) / 1e12
             row.append(f"v{v}: {ms.value * 1000:8.1f} us {tf:7.1f} TF")
         if os.environ.get("GEMM_BENCH_TORCH", "1") == "1":
