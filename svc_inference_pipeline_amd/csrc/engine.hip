@@ -2593,12 +2593,14 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_HIP_CHECK(hipEventCreate(&e0));
   SVC_HIP_CHECK(hipEventCreate(&e1));
   int st = SVC_OK;
-  // iters < 0: |iters| launches each after a 1 GiB memset (operands evicted from L2 and the 256 MiB Infinity Cache,
+  // iters < 0: |iters| launches each after a 1 GiB (SVC_BENCH_FLUSH_MB) memset (operands evicted from L2 and the 256 MiB Infinity Cache,
   // as inside the sampler, where other layers' buffers stream between two launches of one GEMM), timed one by one
   const bool cold = iters < 0;
   if (cold) iters = -iters;
   void* flush = nullptr;
-  if (cold) SVC_HIP_CHECK(hipMalloc(&flush, (size_t)1 << 30));
+  size_t flush_bytes = (size_t)1 << 30;
+  if (const char* fm = getenv("SVC_BENCH_FLUSH_MB")) flush_bytes = (size_t)atoi(fm) << 20;  // (bench tool only)
+  if (cold) SVC_HIP_CHECK(hipMalloc(&flush, flush_bytes));
   auto run = [&]() {
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
     if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, 0);
@@ -2608,7 +2610,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   float ms = 0;
   if (cold) {
     for (int i = 0; i < iters && !st; ++i) {
-      SVC_HIP_CHECK(hipMemsetAsync(flush, i & 0xff, (size_t)1 << 30, 0));
+      SVC_HIP_CHECK(hipMemsetAsync(flush, i & 0xff, flush_bytes, 0));
       SVC_HIP_CHECK(hipEventRecord(e0, 0));
       st = run();
       SVC_HIP_CHECK(hipEventRecord(e1, 0));
