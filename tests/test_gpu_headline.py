@@ -74,7 +74,8 @@ def test_plms100_vs_golden(engine, golden):
     g = golden("samplers")
     cond = dev(golden("conditioner_diffsvc")["cond"])
     x = engine.diffsvc_sample(cond, fast_inference=True, speedup=10, x_T=dev(g["x_T"]))
-    assert rel_l2(x[0].cpu().numpy().T, g["plms100"]) < 1e-2, rel_l2(x[0].cpu().numpy().T, g["plms100"])
+    # measured 1.3e-4 (round 2)
+    assert rel_l2(x[0].cpu().numpy().T, g["plms100"]) < 1e-3, rel_l2(x[0].cpu().numpy().T, g["plms100"])
 
 
 def _mel_l1(engine, cfg, states, seconds=1.0):

@@ -166,13 +166,14 @@ def test_plms_and_ddpm(engine, cfg, states, golden):
     g = golden("samplers")
     cond = dev(golden("conditioner_diffsvc")["cond"])
     x4 = engine.diffsvc_sample(cond, fast_inference=True, speedup=250, x_T=dev(g["x_T"]))
-    assert rel_l2(x4[0].cpu().numpy().T, g["plms4"]) < 1e-2
+    # measured 1.6e-4 (PLMS-4) and 2.1e-4 (DDPM-1000) against the reference-generated goldens (round 2)
+    assert rel_l2(x4[0].cpu().numpy().T, g["plms4"]) < 1e-3
     # DDPM-1000 with the reference's injected noise: clipping keeps it stable, compare the final mel
     T = cond.shape[1]
     seed = int(g["seed"])
     noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
     x = engine.diffsvc_sample(cond, fast_inference=False, x_T=dev(g["x_T"]), noise=dev(noise))
-    assert rel_l2(x[0].cpu().numpy().T, g["ddpm1000"]) < 2e-2
+    assert rel_l2(x[0].cpu().numpy().T, g["ddpm1000"]) < 1.5e-3
 
 
 def test_sampler_sub_streams_bit_identical(engine, golden, tune):
@@ -331,3 +332,32 @@ def test_ddpm_without_noise_or_utt_ids_is_rejected(engine, golden):
     b = engine.diffsvc_sample(cond, fast_inference=False, x_T=xT, seed=3,
                               utt_ids=torch.zeros(B, dtype=torch.int32, device="cuda")).cpu().numpy()
     assert np.isfinite(a).all() and np.array_equal(a, b)
+
+
+def test_bigvgan_tamed_weights_tight(cfg, states, golden):
+    """BigVGAN outside the chaotic regime: with every weight-normed conv's gain g halved (the reference's own
+    parametrisation, modules/bigvgan.py weight_norm), the random-weight generator no longer saturates tanh, so an
+    indexing or halo bug anywhere in the 6 up-sampling stages would show at the fp16-rounding scale. Tolerance: rel-L2
+    vs the f32 oracle <= 2e-3 and <= 1.2x (+2e-4) the distance of the fp16-operand-emulated oracle (measured 8.5e-4
+    against 8.8e-4, none of the output saturated)."""
+    vsd = {k: (v * 0.5 if k.endswith("weight_g") else v) for k, v in W.make_vocoder_state(cfg.vocoder, 0).items()}
+    e = SVCEngine(cfg, 0, mapper_state=states["mapper"], vocoder_state=vsd)
+    try:
+        g = golden("bigvgan")
+        stats = C.load_stats(cfg)
+        mel = g["mel"]
+        T = mel.shape[-1]
+        x_norm = (mel - stats["mel_min"][:, None]) / (stats["mel_max"] - stats["mel_min"] + 1e-12)[:, None] * 2 - 1
+        wav = e.bigvgan(dev(x_norm.T[None].astype(np.float32)))[0].cpu().numpy()
+        with torch.no_grad():
+            ref = OF.synthesis_fade(OM.bigvgan_forward(vsd, cfg.vocoder, torch.from_numpy(mel)[None])[0, 0], T).numpy()
+            with OM.Fp16Operands():
+                emu = OF.synthesis_fade(OM.bigvgan_forward(vsd, cfg.vocoder, torch.from_numpy(mel)[None])[0, 0],
+                                        T).numpy()
+        sat = float(np.mean(np.abs(ref) > 0.97))
+        d_hip, d_emu = rel_l2(wav, ref), rel_l2(emu, ref)
+        print(f"tamed BigVGAN: saturated {sat:.3f}, rel-L2 HIP {d_hip:.2e}, fp16 emulation {d_emu:.2e}")
+        assert sat < 0.05, sat  # the regime this test is about
+        assert d_hip < 2e-3 and d_hip < 1.2 * d_emu + 2e-4, (d_hip, d_emu)
+    finally:
+        e.close()
