@@ -211,9 +211,13 @@ def main():
     ap.add_argument("--sampler", choices=["plms", "ddpm"], default="plms",
                     help="plms = the reference's fast_inference PLMS (speedup --speedup); ddpm = 1000-step DDPM")
     ap.add_argument("--precision", choices=["wsplit", "split", "fp16"], default="wsplit",
-                    help="wsplit (default): weight-split Whisper linears, split-fp16 conv stem / HuBERT / DiffSVC head, "
-                         "the mode that meets the 1e-3 mel-L1 target (tests/test_gpu_headline.py); split: every "
-                         "content GEMM on split-fp16 operands; fp16: plain fp16 operands (faster, fails the target)")
+                    help="wsplit (default): weight-split Whisper attention linears (every block) and MLP linears "
+                         "(blocks 0-3), split-fp16 conv stem / HuBERT / DiffSVC head, the mode that meets the 1e-3 "
+                         "mel-L1 target (tests/test_gpu_headline.py); split: every content GEMM on split-fp16 "
+                         "operands; fp16: plain fp16 operands (faster, fails the target)")
+    ap.add_argument("--wsplit-mlp", type=int, default=None,
+                    help="wsplit: bit mask of the Whisper blocks whose MLP linears are weight-split (default 0xf; "
+                         "16777215 = all 24, the round-2 default before the precision sweep)")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -239,7 +243,8 @@ def main():
     vs = W.make_vocoder_state(cfg.vocoder, seed=0)
     eng = SVCEngine(cfg, dist.local_rank, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs,
                     content_split={"split": 1, "wsplit": 2, "fp16": 0}[args.precision],
-                    head_split=args.precision != "fp16")
+                    head_split=args.precision != "fp16",
+                    config=None if args.wsplit_mlp is None else {"content.wsplit_mlp": args.wsplit_mlp})
     fast = args.sampler == "plms"
     pipe = SVCPipeline(eng)
     B = args.batch
@@ -390,7 +395,8 @@ def main():
                                    + (f" + PLMS-100 DiffSVC (speedup {args.speedup})" if fast else " + DDPM-1000 DiffSVC")
                                    + " + BigVGAN, fp16 MFMA operands / fp32 accumulate"
                                    + {"split": ", split-fp16 content encoder + DiffSVC head (mel-L1 <= 1e-3 mode)",
-                                      "wsplit": ", weight-split Whisper linears + split-fp16 stem / DiffSVC head",
+                                      "wsplit": ", weight-split Whisper attention linears (all blocks) + MLP linears "
+                                                "(blocks 0-3) + split-fp16 stem / DiffSVC head",
                                       "fp16": ", plain fp16 operands (mel-L1 target not met)"}[args.precision],
                        "global_batch": dist.world * B, "seq_len_frames": int((d24.shape[1] + 768 - 1024) // 256 + 1),
                        "parallelism": f"dp{dist.world} (per-utterance shards, RCCL gather)"},

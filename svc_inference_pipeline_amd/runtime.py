@@ -61,10 +61,11 @@ class SVCEngine:
     bits, 3x the MFMA work); 2 (default) splits only the weights of Whisper's block linears ([x | x] x [W_hi; W_lo],
     2x, no extra activation bytes; the weight rounding is the larger share of their error) with the conv stem and
     HuBERT as in 1. `head_split` runs the DiffSVC head (skip_projection, output_projection) on split-fp16 operands,
-    the largest denoiser-side term left."""
+    the largest denoiser-side term left. `config`: further numeric svc_ctx_set_config keys, set before finalize
+    (e.g. {"content.wsplit_linears": 12} to weight-split only the MLP linears)."""
 
     def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None, hubert_state=None,
-                 hubert_output_layer=9, content_split=2, head_split=True):
+                 hubert_output_layer=9, content_split=2, head_split=True, config=None):
         check_supported(cfg)
         _lib.load()
         self.cfg = cfg
@@ -77,6 +78,8 @@ class SVCEngine:
         # content_split: False / 0 = fp16, True / 1 = split-fp16 operands, 2 = weight-split Whisper linears
         _lib.call("svc_ctx_set_config", self._ctx, b"content.split", float(int(content_split)))
         _lib.call("svc_ctx_set_config", self._ctx, b"mapper.head_split", 1.0 if head_split else 0.0)
+        for k, v in (config or {}).items():  # further svc_ctx_set_config keys (e.g. "content.wsplit_linears")
+            _lib.call("svc_ctx_set_config", self._ctx, k.encode(), float(v))
         if whisper_state is not None:
             self._add_state("whisper.", whisper_state)
             self.whisper_dims = W.whisper_dims_from_state(whisper_state)

@@ -70,7 +70,7 @@ def test_whisper_medium_vs_oracle(engine, states):
 def test_plms100_vs_golden(engine, golden):
     """The headline sampler: PLMS speedup 10 = 100 iterations / 101 denoiser calls, against the reference's own
     svc_model_inference(fast_inference=True, speedup=10) output on the golden conditioning and x_T. Random weights
-    make PLMS diverge (|x| ~ 1e2), so the bound is relative: rel-L2 <= 1e-2 (fp16 operands)."""
+    make PLMS diverge (|x| ~ 1e2), so the bound is relative: rel-L2 <= 1e-3 (fp16 operands; measured 1.3e-4)."""
     g = golden("samplers")
     cond = dev(golden("conditioner_diffsvc")["cond"])
     x = engine.diffsvc_sample(cond, fast_inference=True, speedup=10, x_T=dev(g["x_T"]))

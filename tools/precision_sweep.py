@@ -77,6 +77,11 @@ def main():
     ap.add_argument("--no-vocoder", action="store_true", help="mel-L1 only (skip BigVGAN)")
     ap.add_argument("--seconds", type=float, default=1.0)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--wsplit-variants", default="",
+                    help="with --gpu, only these weight-split Whisper variants: comma-separated attn_mask:mlp_mask "
+                         "(content.wsplit_attn / content.wsplit_mlp, bit i = block i; e.g. 16777215:0 = attention "
+                         "linears of all 24 blocks, no MLP linear)")
+    ap.add_argument("--seed", type=int, default=7, help="synthetic clip seed")
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     cfg = C.load_config()
@@ -85,16 +90,16 @@ def main():
         cfg.mapper.content_feature = ["contentvec"]
         cfg.mapper.input_content_dim["contentvec"] = W.HUBERT_DIMS["contentvec"]["final_dim"]
         hs = W.make_hubert_state(W.HUBERT_DIMS["contentvec"], 0)
-        w16 = ON.synth_clip(7, args.seconds, 16000).astype(np.float32)
+        w16 = ON.synth_clip(args.seed, args.seconds, 16000).astype(np.float32)
     else:
         dims = W.WHISPER_DIMS[args.whisper_dims]
         cfg.mapper.input_content_dim["whisper"] = dims["n_audio_state"]
         ws = W.make_whisper_state(dims, 0)
-        w16 = ON.synth_clip_16k_quantised(7, args.seconds)
+        w16 = ON.synth_clip_16k_quantised(args.seed, args.seconds)
     ms = W.make_mapper_state(cfg.mapper, 0)
     vs = W.make_vocoder_state(cfg.vocoder, 0)
     stats = C.load_stats(cfg)
-    w24 = ON.synth_clip(7, args.seconds, 24000).astype(np.float32)
+    w24 = ON.synth_clip(args.seed, args.seconds, 24000).astype(np.float32)
     T = OF.mel_frames(len(w24))
     f0 = ON.synth_f0(4, T)
     seed = 17
@@ -115,12 +120,19 @@ def main():
     if args.gpu:
         from svc_inference_pipeline_amd.pipeline import SVCPipeline
         from svc_inference_pipeline_amd.runtime import SVCEngine
-        for name, split, head in (("gpu-fp16", False, False), ("gpu, split-fp16 content encoder", True, False),
-                                  ("gpu, split-fp16 DiffSVC head", False, True),
-                                  ("gpu, split-fp16 content encoder + DiffSVC head (default)", True, True),
-                                  ("gpu, weight-split content linears + split-fp16 DiffSVC head", 2, True)):
+        variants = [("gpu-fp16", False, False, None), ("gpu, split-fp16 content encoder", True, False, None),
+                    ("gpu, split-fp16 DiffSVC head", False, True, None),
+                    ("gpu, split-fp16 content encoder + DiffSVC head", True, True, None),
+                    ("gpu, weight-split content linears + split-fp16 DiffSVC head (default)", 2, True, None)]
+        if args.wsplit_variants:
+            variants = []
+            for v in args.wsplit_variants.split(","):
+                att, mlp = (int(x) for x in v.split(":"))
+                variants.append((f"gpu, weight-split attention {att:#x} MLP {mlp:#x} + split-fp16 DiffSVC head", 2, True,
+                                 {"content.wsplit_attn": att, "content.wsplit_mlp": mlp}))
+        for name, split, head, extra in variants:
             e = SVCEngine(cfg, 0, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs,
-                          content_split=split, head_split=head)
+                          content_split=split, head_split=head, config=extra)
             d = lambda a, t=torch.float32: torch.as_tensor(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
             noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
             pipe = SVCPipeline(e)
