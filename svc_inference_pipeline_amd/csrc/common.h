@@ -212,6 +212,7 @@ struct Tuning {
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
   int diff_res32 = 0;       // DiffSVC residual stream in f32 (default: split-fp16 hi / lo halves)
   int f0_dbg = 0;           // F0 kernel diagnostics
+  int dft_dbg = 0;          // DFT / mel kernel diagnostics (1 no DFT loop, 2 no filterbank phase, 3 no frame loads)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only)
   void from_env();
   bool set(const char* name, double v);  // false: unknown name ("reset" restores the creation-time values)

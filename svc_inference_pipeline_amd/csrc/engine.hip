@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "amp_conv.h"
+#include "spectral.h"
 
 namespace svc {
 
@@ -99,16 +100,7 @@ int init_noise(float* x, f16* x16, int ld16, int B, int T, int C, uint64_t seed,
                hipStream_t s);
 int conv_post(const f16* a, int lda, int B, int L, int C, const float* w, float bias, const float* fade, int nfade,
               float* out, hipStream_t s, const int* tv = nullptr, int tv_mul = 1);
-struct DftArgs {  // (features.hip)
-  const float* wav; int64_t wav_stride; int64_t n_valid; int64_t n_logical;
-  int n_fft, hop, pad, n_frames, nbins;
-  const float* window; int mode; float* out;
-  const int64_t* nb; const int* Tb;
-};
 int zero_tail_rows(float* x, int B, int T, int C, const int* Tb, hipStream_t s);
-int dft_frames(const DftArgs& a, int B, hipStream_t s);
-int mel_log(const float* spec, int nbins, const float* fb, int n_mels, float* out, int rows, int mode, hipStream_t s);
-int energy_from_mel(const float* mel, int n_mels, float* en, int rows, hipStream_t s);
 int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s,
                       int split_c);
 int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s);
@@ -165,6 +157,43 @@ static std::vector<float> slaney_mel(int sr, int n_fft, int n_mels, double f_lo,
     }
   }
   return w;
+}
+
+// W_n^m = exp(-2 pi i m / n) as interleaved (re, im) f64 pairs
+static std::vector<double> fft_twiddles(int n) {
+  std::vector<double> t(2 * (size_t)n);
+  for (int m = 0; m < n; ++m) {
+    const double a = 2.0 * M_PI * (double)m / (double)n;
+    t[2 * (size_t)m] = cos(a);
+    t[2 * (size_t)m + 1] = -sin(a);
+  }
+  return t;
+}
+
+// The nonzero band [lo, hi) of each filter row, packed (the DFT kernel keeps only those weights, in LDS):
+// band[3m .. 3m+2] = lo, hi, offset of the band in the packed weights
+struct FilterBands {
+  std::vector<float> w;
+  std::vector<int> band;
+};
+static FilterBands filter_bands(const std::vector<float>& fb, int n_mels) {
+  const int nb = (int)(fb.size() / n_mels);
+  FilterBands r;
+  r.band.assign(3 * n_mels, 0);
+  for (int m = 0; m < n_mels; ++m) {
+    int lo = nb, hi = 0;
+    for (int k = 0; k < nb; ++k)
+      if (fb[(size_t)m * nb + k] != 0.f) {
+        lo = std::min(lo, k);
+        hi = k + 1;
+      }
+    if (hi == 0) lo = 0;
+    r.band[3 * m] = lo;
+    r.band[3 * m + 1] = hi;
+    r.band[3 * m + 2] = (int)r.w.size();
+    for (int k = lo; k < hi; ++k) r.w.push_back(fb[(size_t)m * nb + k]);
+  }
+  return r;
 }
 
 static std::vector<float> hann_periodic(int n) {
@@ -249,7 +278,7 @@ void Tuning::from_env() {
               {"SVC_AMP_MODE", &amp_mode},         {"SVC_AMP_RUN", &amp_run},           {"SVC_AMP_DBG", &amp_dbg},
               {"SVC_AMP_FUSED", &amp_fused},       {"SVC_AMP_MAXC", &amp_maxc},         {"SVC_WHISPER_STREAMS", &whisper_streams},
               {"SVC_SAMPLER_STREAMS", &sampler_streams}, {"SVC_VOCODER_STREAMS", &vocoder_streams},
-              {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg}};
+              {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg},             {"SVC_DFT_DBG", &dft_dbg}};
   for (auto& it : ints)
     if (const char* v = getenv(it.env)) *it.v = atoi(v);
   if (const char* v = getenv("SVC_AMP_LDS")) amp_lds_max = v[0] == 'm' ? 1 : 0;
@@ -265,7 +294,8 @@ bool Tuning::set(const char* name, double v) {
               {"amp_mode", &amp_mode},         {"amp_run", &amp_run},           {"amp_lds_max", &amp_lds_max},
               {"amp_dbg", &amp_dbg},           {"amp_fused", &amp_fused},       {"amp_maxc", &amp_maxc},
               {"whisper_streams", &whisper_streams}, {"sampler_streams", &sampler_streams},
-              {"vocoder_streams", &vocoder_streams}, {"diff_res32", &diff_res32}, {"f0_dbg", &f0_dbg}};
+              {"vocoder_streams", &vocoder_streams}, {"diff_res32", &diff_res32}, {"f0_dbg", &f0_dbg},
+              {"dft_dbg", &dft_dbg}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) {
       *it.v = (int)v;
@@ -304,6 +334,9 @@ struct svc_ctx {
 
   // features
   float *fb24 = nullptr, *fb16 = nullptr, *win_mel = nullptr, *win16 = nullptr;
+  int *band24 = nullptr, *band16 = nullptr;  // [n_mels][3] nonzero band of each filter (lo, hi, offset in fb)
+  int fb24_len = 0, fb16_len = 0;              // fb24 / fb16 hold only those bands, packed
+  double *tw24 = nullptr, *tw16 = nullptr;     // FFT twiddles: [n_fft] (cos, -sin)(2 pi m / n_fft)
   int n_fft = 1024, hop = 256, n_mels = 100, fs = 24000;
   double fmin = 0, fmax = 12000, f0_min = 65, f0_max = 800;
   // content encoders in split-fp16 precision ("content.split" = 1 at finalize): every GEMM operand of Whisper /
@@ -1210,13 +1243,20 @@ int build_features(svc_ctx* c) {
   c->fmax = cfgv(c, "fmax", 12000);
   c->f0_min = cfgv(c, "f0_min", 65);
   c->f0_max = cfgv(c, "f0_max", 800);
-  if ((int)cfgv(c, "win_length", 1024) != c->n_fft) {
-    set_error("win_length != n_fft unsupported");
+  if ((int)cfgv(c, "win_length", 1024) != c->n_fft || !dft_mel_supported(c->n_fft)) {
+    set_error("n_fft %d / win_length unsupported (n_fft 512, 1024 or 2048 and win_length == n_fft)", c->n_fft);
     return SVC_ERR_INVALID;
   }
   int st;
-  if ((st = upload_vec(c, slaney_mel(c->fs, c->n_fft, c->n_mels, c->fmin, c->fmax), &c->fb24))) return st;
-  if ((st = upload_vec(c, slaney_mel(16000, 400, 80, 0.0, 8000.0), &c->fb16))) return st;
+  const std::vector<float> fb24 = slaney_mel(c->fs, c->n_fft, c->n_mels, c->fmin, c->fmax);
+  const std::vector<float> fb16 = slaney_mel(16000, 400, 80, 0.0, 8000.0);
+  const FilterBands b24 = filter_bands(fb24, c->n_mels), b16 = filter_bands(fb16, 80);
+  c->fb24_len = (int)b24.w.size();
+  c->fb16_len = (int)b16.w.size();
+  if ((st = upload_vec(c, b24.w, &c->fb24)) || (st = upload_vec(c, b16.w, &c->fb16))) return st;
+  if ((st = upload_vec(c, b24.band, &c->band24)) || (st = upload_vec(c, b16.band, &c->band16))) return st;
+  if ((st = upload_vec(c, fft_twiddles(c->n_fft), &c->tw24)) || (st = upload_vec(c, fft_twiddles(400), &c->tw16)))
+    return st;
   if ((st = upload_vec(c, hann_periodic(c->n_fft), &c->win_mel))) return st;
   if ((st = upload_vec(c, hann_periodic(400), &c->win16))) return st;
   return SVC_OK;
@@ -1462,12 +1502,7 @@ svc_status svc_mel_energy(svc_ctx* c, const float* wav, int B, int64_t n, const 
   std::vector<int> Tb_host;
   int st0 = stage_samples(c, c->lens_feat, n_samples, B, n, s, &nb_dev, &Tb_dev, &Tb_host);
   if (st0) return st0;
-  size_t need = (size_t)B * T * nb * 4 + 4096;
   int st;
-  if ((st = c->auxws.reserve(std::max(need, c->auxws.cap)))) return st;
-  c->auxws.reset();
-  float* spec = c->auxws.get<float>((size_t)B * T * nb);
-  SVC_REQUIRE(spec, "mel_energy: workspace");
   DftArgs a{};
   a.wav = wav;
   a.wav_stride = n;
@@ -1479,13 +1514,17 @@ svc_status svc_mel_energy(svc_ctx* c, const float* wav, int B, int64_t n, const 
   a.n_frames = T;
   a.nbins = nb;
   a.window = c->win_mel;
+  a.twiddle = reinterpret_cast<const double2*>(c->tw24);
   a.mode = 0;
-  a.out = spec;
+  a.fb = c->fb24;
+  a.band = c->band24;
+  a.fb_len = c->fb24_len;
+  a.n_mels = c->n_mels;
+  a.out = mel;
+  a.energy = energy;
   a.nb = nb_dev;
   a.Tb = Tb_dev;
-  if ((st = dft_frames(a, B, s))) return st;
-  if ((st = mel_log(spec, nb, c->fb24, c->n_mels, mel, B * T, 0, s))) return st;
-  if ((st = energy_from_mel(mel, c->n_mels, energy, B * T, s))) return st;
+  if ((st = dft_mel(a, B, s))) return st;
   if (Tb_dev && ((st = zero_tail_rows(mel, B, T, c->n_mels, Tb_dev, s)) || (st = zero_tail_rows(energy, B, T, 1, Tb_dev, s))))
     return st;
   return SVC_OK;
@@ -1527,12 +1566,11 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   const size_t rows1 = (size_t)B * F, rows2 = (size_t)B * L;
   const int X3 = c->content_split ? 3 : 1;  // split-fp16 block operands are [hi | lo | hi] rows
   const int XS = c->content_mode != 0 ? 3 : 1;  // the conv stem is split-fp16 in both split modes
-  size_t need = rows1 * nb * 4 + rows1 * c->wmels * 4 + rows1 * c->wmels * 2 * XS + rows1 * D * 2 * XS /*h1*/ +
+  size_t need = rows1 * c->wmels * 4 + rows1 * c->wmels * 2 * XS + rows1 * D * 2 * XS /*h1*/ +
                 rows2 * D * 4 + rows2 * D * 2 * X3 + rows2 * 3 * D * 2 + rows2 * D * 2 + rows2 * 4 * D * 2 * X3 + 64 * 4096;
   int st;
   if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
   c->ws.reset();
-  WS_GET(float, spec, rows1 * nb);
   WS_GET(float, ls, rows1 * c->wmels);
   WS_GET(f16, lm16, rows1 * c->wmels * XS);
   WS_GET(float, mx, B);
@@ -1547,10 +1585,14 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   a.n_frames = F;
   a.nbins = nb;
   a.window = c->win16;
+  a.twiddle = reinterpret_cast<const double2*>(c->tw16);
   a.mode = 1;
-  a.out = spec;
-  if ((st = dft_frames(a, B, s))) return st;
-  if ((st = mel_log(spec, nb, c->fb16, c->wmels, ls, (int)rows1, 1, s))) return st;
+  a.fb = c->fb16;
+  a.band = c->band16;
+  a.fb_len = c->fb16_len;
+  a.n_mels = c->wmels;
+  a.out = ls;
+  if ((st = dft_mel(a, B, s))) return st;
   if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s, XS == 3 ? c->wmels : 0))) return st;
   // conv stem
   WS_GET(f16, h1, rows1 * D * XS);

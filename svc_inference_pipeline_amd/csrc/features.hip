@@ -3,97 +3,275 @@
 //     periodic Hann, sqrt(re^2+im^2+1e-9), slaney mel [100x513], ln(clamp 1e-5))
 //   * Whisper log-mel: utils/whisper_extractor/audio.py:92-124 (pad/trim 480000, center reflect pad
 //     200, n_fft 400, hop 160, |X|^2, mel_80, log10(clamp 1e-10), max(x, max-8), (x+4)/4)
-// The DFT is evaluated directly per (frame, bin) with f64 accumulation and an f64 twiddle table in
-// LDS (8 frames per workgroup share every twiddle read); the window multiply is f32 as in torch.stft.
+// One kernel per spectrogram: each workgroup takes FR consecutive frames from the waveform to the log-mel rows (the
+// spectrum never leaves LDS):
+//   1. frame j of n real windowed samples -> LDS as n/2 complex f64 z[m] = x[2m] + i x[2m+1];
+//   2. Z = FFT_{n/2}(z): Stockham autosort stages (radix 4 / 2 for n/2 = 256 / 512 / 1024, 8 / 5 / 5 for Whisper's
+//      n/2 = 200), one thread per butterfly, read -> barrier -> write in place, twiddles from an exact f64 table;
+//   3. X[k] = (Z[k] + Z*[n/2-k]) / 2 + W_n^k (Z[k] - Z*[n/2-k]) / 2i, k = 0..n/2 (the real-input split), |X| (f32, as
+//      torch) -> LDS, then the slaney filterbank over each filter's nonzero band only (the same f32 fma sequence as a
+//      dense dot product: the skipped products are exact zeros), the log, and optionally the frame energy.
+// f64 throughout the transform (the oracle's torch.stft is an f32 FFT; f64 keeps this side's error far below it); the
+// window multiply is f32 as in torch.stft.
 #include "common.h"
+#include "spectral.h"
 
 namespace svc {
 
-constexpr int DFT_FR = 8;  // frames per workgroup
+__device__ __forceinline__ float spec_value(double re, double im, int mode) {
+  const float r = (float)re, i = (float)im;
+  if (mode == 0) return sqrtf(r * r + i * i + 1e-9f);
+  const float m = sqrtf(r * r + i * i);
+  return m * m;
+}
 
-struct DftArgs {
-  const float* wav; int64_t wav_stride; int64_t n_valid;  // samples per utterance actually present
-  int64_t n_logical;  // length of the (zero-extended) signal the reflection is taken on
-  int n_fft, hop, pad, n_frames, nbins;
-  const float* window;  // [n_fft]
-  int mode;             // 0: sqrt(|X|^2 + 1e-9) ; 1: |X|^2
-  float* out;           // [B*n_frames][nbins]
-  // ragged batches (optional): utterance b has nb[b] samples (its n_valid and n_logical) and Tb[b] frames
-  const int64_t* nb;
-  const int* Tb;
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ double2 mul_mi(double2 a) { return make_double2(a.y, -a.x); }  // -i a
+
+// forward R-point DFTs in registers (V[q] = sum_r v[r] e^{-2 pi i r q / R})
+template <int R>
+__device__ __forceinline__ void bfly(double2* v);
+template <>
+__device__ __forceinline__ void bfly<2>(double2* v) {
+  const double2 a = v[0], b = v[1];
+  v[0] = cadd(a, b);
+  v[1] = csub(a, b);
+}
+template <>
+__device__ __forceinline__ void bfly<4>(double2* v) {
+  const double2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]), t2 = cadd(v[1], v[3]), t3 = mul_mi(csub(v[1], v[3]));
+  v[0] = cadd(t0, t2);
+  v[2] = csub(t0, t2);
+  v[1] = cadd(t1, t3);
+  v[3] = csub(t1, t3);
+}
+template <>
+__device__ __forceinline__ void bfly<8>(double2* v) {
+  double2 e[4] = {v[0], v[2], v[4], v[6]}, o[4] = {v[1], v[3], v[5], v[7]};
+  bfly<4>(e);
+  bfly<4>(o);
+  constexpr double h = 0.70710678118654752440;  // W_8 = (h, -h)
+  const double2 w1 = make_double2(h, -h), w3 = make_double2(-h, -h);
+  o[1] = cmul(o[1], w1);
+  o[2] = mul_mi(o[2]);
+  o[3] = cmul(o[3], w3);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v[q] = cadd(e[q], o[q]);
+    v[q + 4] = csub(e[q], o[q]);
+  }
+}
+template <>
+__device__ __forceinline__ void bfly<5>(double2* v) {
+  constexpr double c1 = 0.30901699437494742410, c2 = -0.80901699437494742410;  // cos(2 pi / 5), cos(4 pi / 5)
+  constexpr double s1 = 0.95105651629515357212, s2 = 0.58778525229247312917;   // sin(2 pi / 5), sin(4 pi / 5)
+  const double2 a1 = cadd(v[1], v[4]), a2 = cadd(v[2], v[3]), b1 = csub(v[1], v[4]), b2 = csub(v[2], v[3]);
+  const double2 x0 = v[0];
+  const double2 t1 = make_double2(x0.x + c1 * a1.x + c2 * a2.x, x0.y + c1 * a1.y + c2 * a2.y);
+  const double2 t2 = make_double2(x0.x + c2 * a1.x + c1 * a2.x, x0.y + c2 * a1.y + c1 * a2.y);
+  const double2 u1 = make_double2(s1 * b1.x + s2 * b2.x, s1 * b1.y + s2 * b2.y);
+  const double2 u2 = make_double2(s2 * b1.x - s1 * b2.x, s2 * b1.y - s1 * b2.y);
+  v[0] = cadd(x0, cadd(a1, a2));
+  v[1] = cadd(t1, mul_mi(u1));
+  v[4] = csub(t1, mul_mi(u1));
+  v[2] = cadd(t2, mul_mi(u2));
+  v[3] = csub(t2, mul_mi(u2));
+}
+
+// One Stockham stage of an N-point complex FFT (N = n/2) over the frame's z, radix R, NS = product of the earlier
+// radices: butterfly b reads z[b + r N/R], multiplies by W_{NS R}^{r (b mod NS)} (= W_n^{2 N r (b mod NS) / (NS R)},
+// the table tw holds W_n^m), and writes z[(b / NS) NS R + (b mod NS) + q NS]. All reads of the workgroup precede all
+// writes (barrier), so the stage runs in place.
+template <int N, int R, int NS, int TPF>
+__device__ __forceinline__ void fft_stage(double2* z, const double2* tw, int t) {
+  constexpr int NB = N / R, PER = (NB + TPF - 1) / TPF, TS = 2 * N / (NS * R);
+  static_assert(N % (NS * R) == 0, "radix plan");
+  double2 v[PER][R];
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int b = t + p * TPF;
+    if (b < NB) {
+      const int k = b % NS;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const double2 x = z[b + r * NB];
+        v[p][r] = (NS == 1 || r == 0) ? x : cmul(x, tw[r * k * TS]);
+      }
+      bfly<R>(v[p]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const int b = t + p * TPF;
+    if (b < NB) {
+      const int k = b % NS, d = (b / NS) * NS * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) z[d + r * NS] = v[p][r];
+    }
+  }
+  __syncthreads();
+}
+
+// radix plans: N = n/2 complex points, TPF threads per frame (one per butterfly of the widest stage), FR frames per
+// workgroup
+template <int N>
+struct FftPlan;
+template <>
+struct FftPlan<200> {  // Whisper n_fft 400
+  static constexpr int TPF = 40, FR = 8;
+  __device__ static void run(double2* z, const double2* tw, int t) {
+    fft_stage<200, 8, 1, TPF>(z, tw, t);
+    fft_stage<200, 5, 8, TPF>(z, tw, t);
+    fft_stage<200, 5, 40, TPF>(z, tw, t);
+  }
+};
+template <>
+struct FftPlan<256> {
+  static constexpr int TPF = 64, FR = 4;
+  __device__ static void run(double2* z, const double2* tw, int t) {
+    fft_stage<256, 4, 1, TPF>(z, tw, t);
+    fft_stage<256, 4, 4, TPF>(z, tw, t);
+    fft_stage<256, 4, 16, TPF>(z, tw, t);
+    fft_stage<256, 4, 64, TPF>(z, tw, t);
+  }
+};
+template <>
+struct FftPlan<512> {  // n_fft 1024
+  static constexpr int TPF = 128, FR = 2;
+  __device__ static void run(double2* z, const double2* tw, int t) {
+    fft_stage<512, 4, 1, TPF>(z, tw, t);
+    fft_stage<512, 4, 4, TPF>(z, tw, t);
+    fft_stage<512, 4, 16, TPF>(z, tw, t);
+    fft_stage<512, 4, 64, TPF>(z, tw, t);
+    fft_stage<512, 2, 256, TPF>(z, tw, t);
+  }
+};
+template <>
+struct FftPlan<1024> {
+  static constexpr int TPF = 256, FR = 1;
+  __device__ static void run(double2* z, const double2* tw, int t) {
+    fft_stage<1024, 4, 1, TPF>(z, tw, t);
+    fft_stage<1024, 4, 4, TPF>(z, tw, t);
+    fft_stage<1024, 4, 16, TPF>(z, tw, t);
+    fft_stage<1024, 4, 64, TPF>(z, tw, t);
+    fft_stage<1024, 4, 256, TPF>(z, tw, t);
+  }
 };
 
-__global__ __launch_bounds__(256) void dft_kernel(DftArgs a) {
+template <int N>
+struct MelLds {  // dynamic LDS layout (bytes)
+  using P = FftPlan<N>;
+  static constexpr size_t Z = (size_t)P::FR * N * 16, TW = (size_t)2 * N * 16, SP = (size_t)P::FR * (N + 1) * 4;
+  static size_t bytes(int fb_len, int n_mels) { return Z + TW + SP + (size_t)(fb_len + P::FR * n_mels) * 4; }
+};
+
+template <int N>
+__global__ __launch_bounds__(FftPlan<N>::TPF * FftPlan<N>::FR) void dft_mel_kernel(DftArgs a) {
+  using P = FftPlan<N>;
+  using L = MelLds<N>;
+  constexpr int n = 2 * N, NT = P::TPF * P::FR;
   extern __shared__ __align__(16) unsigned char dsm[];
-  double* cs = reinterpret_cast<double*>(dsm);      // [n_fft] cos
-  double* sn = cs + a.n_fft;                          // [n_fft] sin
-  float* xs = reinterpret_cast<float*>(sn + a.n_fft);  // [DFT_FR][n_fft]
-  const int f0 = blockIdx.y * DFT_FR;
-  const int b = blockIdx.z;
+  double2* zs = reinterpret_cast<double2*>(dsm);         // [FR][N] frame / spectrum
+  double2* tw = reinterpret_cast<double2*>(dsm + L::Z);  // [n] W_n^m = (cos, -sin)(2 pi m / n)
+  float* sp = reinterpret_cast<float*>(dsm + L::Z + L::TW);  // [FR][N + 1] |X|
+  float* fbs = sp + P::FR * (N + 1);                     // packed filterbank bands
+  float* ml = fbs + a.fb_len;                            // [FR][n_mels] log-mel (energy)
+  const int f0 = blockIdx.x * P::FR;
+  const int b = blockIdx.y;
   const float* w = a.wav + (int64_t)b * a.wav_stride;
   const int64_t n_valid = a.nb ? a.nb[b] : a.n_valid, n_logical = a.nb ? a.nb[b] : a.n_logical;
   const int n_frames = a.Tb ? min(a.n_frames, a.Tb[b]) : a.n_frames;
   if (f0 >= n_frames) return;  // block-uniform, before any barrier (zero_tail_rows clears those rows' outputs)
-  for (int i = threadIdx.x; i < a.n_fft; i += blockDim.x) {
-    double s, c;
-    sincospi(2.0 * (double)i / (double)a.n_fft, &s, &c);
-    cs[i] = c;
-    sn[i] = s;
-  }
-  for (int i = threadIdx.x; i < DFT_FR * a.n_fft; i += blockDim.x) {
-    int fr = i / a.n_fft, j = i - fr * a.n_fft;
-    int f = f0 + fr;
-    float v = 0.f;
-    if (f < n_frames) {
-      int64_t idx = (int64_t)f * a.hop + j - a.pad;
+  const int nf = min(P::FR, n_frames - f0);
+  const int tid = threadIdx.x, fr = tid / P::TPF, t = tid - fr * P::TPF;
+  for (int i = tid; i < n; i += NT) tw[i] = a.twiddle[i];
+  for (int i = tid; i < a.fb_len; i += NT) fbs[i] = a.fb[i];
+  // 1. frame fr: sample j -> the j-th double of z (even samples real, odd imaginary)
+  double* zf = reinterpret_cast<double*>(zs + fr * N);
+  for (int j = t; j < n; j += P::TPF) {
+    float x = 0.f;
+    if (fr < nf && a.dbg != 3) {
+      int64_t idx = (int64_t)(f0 + fr) * a.hop + j - a.pad;
       if (idx < 0) idx = -idx;
       if (idx >= n_logical) idx = 2 * (n_logical - 1) - idx;
-      v = idx < n_valid ? w[idx] : 0.f;
-      v = v * a.window[j];
+      x = idx < n_valid ? w[idx] : 0.f;
     }
-    xs[i] = v;
+    zf[j] = (double)(x * a.window[j]);
   }
   __syncthreads();
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= a.nbins) return;
-  double re[DFT_FR], im[DFT_FR];
-#pragma unroll
-  for (int fr = 0; fr < DFT_FR; ++fr) re[fr] = im[fr] = 0.0;
-  int idx = 0;
-  for (int j = 0; j < a.n_fft; ++j) {
-    const double c = cs[idx], s = sn[idx];
-#pragma unroll
-    for (int fr = 0; fr < DFT_FR; ++fr) {
-      const double x = (double)xs[fr * a.n_fft + j];
-      re[fr] += x * c;
-      im[fr] -= x * s;
-    }
-    idx += k;
-    if (idx >= a.n_fft) idx -= a.n_fft;
+  // 2. FFT
+  if (a.dbg != 1) P::run(zs + fr * N, tw, t);
+  // 3. real-input split and magnitudes
+  const double2* Z = zs + fr * N;
+  for (int k = t; k <= N; k += P::TPF) {
+    const double2 zk = Z[k == N ? 0 : k], zm = Z[k == 0 ? 0 : N - k];
+    const double2 e = make_double2(0.5 * (zk.x + zm.x), 0.5 * (zk.y - zm.y));   // (Z[k] + Z*[N-k]) / 2
+    const double2 o = make_double2(0.5 * (zk.y + zm.y), -0.5 * (zk.x - zm.x));  // (Z[k] - Z*[N-k]) / 2i
+    const double2 X = cadd(e, cmul(o, tw[k]));
+    sp[fr * (N + 1) + k] = spec_value(X.x, X.y, a.mode);
   }
-#pragma unroll
-  for (int fr = 0; fr < DFT_FR; ++fr) {
-    const int f = f0 + fr;
-    if (f >= n_frames) break;
-    const float r = (float)re[fr], i = (float)im[fr];
-    float v;
-    if (a.mode == 0) {
-      v = sqrtf(r * r + i * i + 1e-9f);
-    } else {
-      float m = sqrtf(r * r + i * i);
-      v = m * m;
+  __syncthreads();
+  const int64_t row0 = (int64_t)b * a.n_frames + f0;
+  for (int i = tid; i < (a.dbg == 2 ? 0 : nf * a.n_mels); i += NT) {
+    const int f = i / a.n_mels, m = i - f * a.n_mels;
+    const int lo = a.band[3 * m], hi = a.band[3 * m + 1];
+    const float* fbm = fbs + a.band[3 * m + 2] - lo;
+    const float* x = sp + f * (N + 1);
+    float acc = 0.f;
+    for (int kk = lo; kk < hi; ++kk) acc = fmaf(fbm[kk], x[kk], acc);
+    const float v = a.mode == 0 ? logf(fmaxf(acc, 1e-5f)) : log10f(fmaxf(acc, 1e-10f));
+    a.out[row0 * a.n_mels + i] = v;
+    ml[i] = v;
+  }
+  if (a.energy) {
+    __syncthreads();
+    if (tid < nf) {
+      float acc = 0.f;
+      for (int m = 0; m < a.n_mels; ++m) {
+        const float e = expf(ml[tid * a.n_mels + m]);
+        acc += e * e;
+      }
+      a.energy[row0 + tid] = sqrtf(acc);
     }
-    a.out[((int64_t)b * a.n_frames + f) * a.nbins + k] = v;
   }
 }
 
-int dft_frames(const DftArgs& a, int B, hipStream_t s) {
-  SVC_REQUIRE(a.n_fft <= 1024 && a.n_frames > 0, "dft: n_fft=%d frames=%d", a.n_fft, a.n_frames);
-  size_t lds = (size_t)a.n_fft * 2 * sizeof(double) + (size_t)DFT_FR * a.n_fft * sizeof(float);
-  dim3 grid(cdiv(a.nbins, 256), cdiv(a.n_frames, DFT_FR), B);
-  hipLaunchKernelGGL(dft_kernel, grid, dim3(256), lds, s, a);
+bool dft_mel_supported(int n_fft) { return n_fft == 400 || n_fft == 512 || n_fft == 1024 || n_fft == 2048; }
+
+template <int N>
+static int launch_dft_mel(const DftArgs& a, int B, hipStream_t s) {
+  using P = FftPlan<N>;
+  const size_t lds = MelLds<N>::bytes(a.fb_len, a.n_mels);
+  SVC_REQUIRE(lds <= 160 * 1024, "dft_mel: %zu B of LDS", lds);
+  static bool attr = false;
+  if (!attr) {
+    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)dft_mel_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+    attr = true;
+  }
+  DftArgs p = a;
+  p.dbg = tuning().dft_dbg;
+  dim3 grid(cdiv(a.n_frames, P::FR), B);
+  hipLaunchKernelGGL(dft_mel_kernel<N>, grid, dim3(P::TPF * P::FR), lds, s, p);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
+}
+
+int dft_mel(const DftArgs& a, int B, hipStream_t s) {
+  SVC_REQUIRE(dft_mel_supported(a.n_fft) && a.nbins == a.n_fft / 2 + 1 && a.n_frames > 0 && a.fb && a.band &&
+                  a.n_mels > 0 && a.fb_len > 0 && a.twiddle,
+              "dft_mel: n_fft=%d nbins=%d frames=%d mels=%d", a.n_fft, a.nbins, a.n_frames, a.n_mels);
+  switch (a.n_fft) {
+    case 400: return launch_dft_mel<200>(a, B, s);
+    case 512: return launch_dft_mel<256>(a, B, s);
+    case 1024: return launch_dft_mel<512>(a, B, s);
+    default: return launch_dft_mel<1024>(a, B, s);
+  }
 }
 
 // ragged batches: rows t >= Tb[b] of a [B][T][C] f32 tensor are set to zero (the frames a clip of that length
@@ -114,46 +292,6 @@ int zero_tail_rows(float* x, int B, int T, int C, const int* Tb, hipStream_t s) 
 }
 
 // mel projection + log: out[row][m] = log(clamp(sum_k fb[m][k] spec[row][k])) ; mode 0 ln/1e-5, 1 log10/1e-10
-__global__ void mel_log_kernel(const float* __restrict__ spec, int nbins, const float* __restrict__ fb, int n_mels,
-                               float* __restrict__ out, int rows, int mode) {
-  const int row = blockIdx.x;
-  extern __shared__ float sp[];
-  for (int k = threadIdx.x; k < nbins; k += blockDim.x) sp[k] = spec[(int64_t)row * nbins + k];
-  __syncthreads();
-  for (int m = threadIdx.x; m < n_mels; m += blockDim.x) {
-    const float* fr = fb + (int64_t)m * nbins;
-    float acc = 0.f;
-    for (int k = 0; k < nbins; ++k) acc = fmaf(fr[k], sp[k], acc);
-    float v = mode == 0 ? logf(fmaxf(acc, 1e-5f)) : log10f(fmaxf(acc, 1e-10f));
-    out[(int64_t)row * n_mels + m] = v;
-  }
-}
-
-int mel_log(const float* spec, int nbins, const float* fb, int n_mels, float* out, int rows, int mode, hipStream_t s) {
-  hipLaunchKernelGGL(mel_log_kernel, dim3(rows), dim3(128), nbins * sizeof(float), s, spec, nbins, fb, n_mels, out,
-                     rows, mode);
-  SVC_LAUNCH_CHECK();
-  return SVC_OK;
-}
-
-// energy = sqrt(sum_m exp(mel)^2) (utils/mel.py:199)
-__global__ void energy_kernel(const float* __restrict__ mel, int n_mels, float* __restrict__ en, int rows) {
-  int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= rows) return;
-  float acc = 0.f;
-  for (int m = 0; m < n_mels; ++m) {
-    float e = expf(mel[(int64_t)r * n_mels + m]);
-    acc += e * e;
-  }
-  en[r] = sqrtf(acc);
-}
-
-int energy_from_mel(const float* mel, int n_mels, float* en, int rows, hipStream_t s) {
-  hipLaunchKernelGGL(energy_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, s, mel, n_mels, en, rows);
-  SVC_LAUNCH_CHECK();
-  return SVC_OK;
-}
-
 // Whisper: per-utterance global max of the log10 spectrogram, then clamp/shift -> f16 GEMM operand
 __global__ void rowblock_max_kernel(const float* __restrict__ x, int64_t n_per_utt, float* __restrict__ mx) {
   const int b = blockIdx.x;

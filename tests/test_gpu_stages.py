@@ -49,11 +49,31 @@ def test_mel_energy(engine, cfg, golden):
         ref = OF.mel_spectrogram(torch.from_numpy(wav)[None], cfg)[0]
         assert mel.shape[1] == ref.shape[-1] == OF.mel_frames(len(wav))
         mel = mel[0].cpu().numpy().T
-        # f64 DFT vs torch's f32 FFT: log-mel agrees to 1e-4 where the magnitude is above the 1e-5 clamp
+        # f64 FFT vs torch's f32 FFT: log-mel agrees to 1e-4 where the magnitude is above the 1e-5 clamp
         assert np.max(np.abs(mel - ref.numpy())) < 2e-3
         assert np.mean(np.abs(mel - ref.numpy())) < 3e-5
         ref_en = OF.energy_from_mel(ref[None])[0].numpy()
         np.testing.assert_allclose(en[0].cpu().numpy(), ref_en, rtol=2e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("n_fft,hop", [(512, 128), (2048, 512)])
+def test_mel_energy_other_fft_sizes(n_fft, hop):
+    """The FFT plans the headline config does not use (n/2 = 256: four radix-4 stages; n/2 = 1024: five), through a
+    features-only engine configured with that n_fft / hop / win_length, against the oracle's torch.stft mel."""
+    c = C.load_config()
+    c.n_fft, c.hop_length, c.win_length = n_fft, hop, n_fft
+    e = SVCEngine(c, 0)
+    try:
+        wav = ON.synth_clip(5, 2.0, 24000)
+        mel, en = e.mel_energy(dev(wav[None]))
+        ref = OF.mel_spectrogram(torch.from_numpy(wav)[None], c)[0]
+        mel = mel[0].cpu().numpy().T
+        assert mel.shape == ref.shape
+        assert np.max(np.abs(mel - ref.numpy())) < 2e-3
+        assert np.mean(np.abs(mel - ref.numpy())) < 3e-5
+        np.testing.assert_allclose(en[0].cpu().numpy(), OF.energy_from_mel(ref[None])[0].numpy(), rtol=2e-5, atol=1e-7)
+    finally:
+        e.close()
 
 
 @pytest.mark.parametrize("direct", ["15", "0"])
