@@ -667,11 +667,14 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   if (variant == 15 && tu.gemm4_rmw && conv_gemm4_rmw_form(a, e)) variant = 24;
   SVC_REQUIRE(variant == -1 || (variant >= 10 && variant <= 15) || variant == 20 || variant == 24,
               "gemm_variant %d: -1, 10..15, 20 or 24", variant);
-  if (pair || g.N > 64) {
-    if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), s, variant == 24);
-    if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
-    if (pair) return conv_gemm3(a, e, zero_page(), 5, s);  // v1 has no paired epilogue
+  // N <= 64 (the last BigVGAN up-sampling phases, 48 / 24 channels) also takes conv_gemm3's 128 x 128 tile: 1.9 vs
+  // 3.0 ms per step on gemm.hip's 256 x 64 / 256 x 32 tiles (tools/ab_ups.sh), although 63-81 % of its N is padding
+  if (variant == 20 || variant == 24) {
+    if (pair || g.N > 64) return conv_gemm4(a, e, zero_page(), s, variant == 24);
+    variant = 15;  // conv_gemm4's tiles are 128 wide in N: small-N GEMMs keep conv_gemm3
   }
+  if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
+  if (pair) return conv_gemm3(a, e, zero_page(), 5, s);  // v1 has no paired epilogue
   return conv_gemm(a, e, s);
 }
 

@@ -20,6 +20,8 @@
 namespace svc {
 
 constexpr int F0_MAXC = 16;  // >= max candidates (15 for the parselmouth defaults)
+constexpr int F0_LB = 9;     // autocorrelation lags per thread (register window)
+constexpr int F0_SEG = 4;    // autocorrelation sample segments (partial sums per lag)
 
 struct F0Params {
   int nsp, hnsp, nw, hnw, maxlag, nf, bmax, maxc;
@@ -230,22 +232,27 @@ __global__ void f0_global_kernel(const float* __restrict__ wav, int64_t stride, 
 }
 
 // Hanning window (Praat: 0.5 - 0.5 cos(2 pi i / (nw+1)), i = 1..nw) and its normalised autocorrelation
-__global__ void f0_window_kernel(int nw, int bmax, double* __restrict__ win, double* __restrict__ winR) {
+// Hann window and its normalised autocorrelation winR[lag] = sum_j w[j] w[j + lag] / sum_j w[j]^2, one lag per
+// thread over F0_WIN_WG-thread workgroups (each recomputes the window in LDS); serial sums as the frame kernel's lags
+constexpr int F0_WIN_WG = 64;
+__global__ __launch_bounds__(F0_WIN_WG) void f0_window_kernel(int nw, int bmax, double* __restrict__ win,
+                                                              double* __restrict__ winR) {
   __shared__ double w[2048];
+  __shared__ double r0;
   for (int i = threadIdx.x; i < nw; i += blockDim.x) {
     double v = 0.5 - 0.5 * cos((double)(i + 1) * 2.0 * M_PI / (nw + 1));
     w[i] = v;
-    win[i] = v;
+    if (blockIdx.x == 0) win[i] = v;
   }
   __syncthreads();
-  __shared__ double r0;
   if (threadIdx.x == 0) {
     double s = 0;
     for (int j = 0; j < nw; ++j) s += w[j] * w[j];
     r0 = s;
   }
   __syncthreads();
-  for (int lag = threadIdx.x; lag <= bmax; lag += blockDim.x) {
+  const int lag = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lag <= bmax) {
     double s = 0;
     for (int j = 0; j + lag < nw; ++j) s += w[j] * w[j + lag];
     winR[lag] = s / r0;
@@ -284,11 +291,12 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
                                                        const double* __restrict__ gpeak, F0Out o,
                                                        const F0Utt* __restrict__ utt) {
   extern __shared__ double sm[];
-  double* frame = sm;               // [nw]
-  double* r = frame + P.nw;         // [2*bmax+1], lag L at r[L + bmax]
-  double* red = r + 2 * P.bmax + 1; // [8]
-  double* pkf = red + 8;             // [bmax + 1] first pass: peak frequency at lag i (0 = not a candidate peak)
-  double* pks = pkf + P.bmax + 1;    // [bmax + 1] ... and its sinc(30) strength
+  double* frame = sm;                   // [nw + bmax + 2 F0_LB], zero past nw
+  double* red = frame + P.nw + P.bmax + 2 * F0_LB;  // [8]
+  double* r = red + 8;                  // [2*bmax+1], lag L at r[L + bmax]
+  double* pkf = r + 2 * P.bmax + 1;     // [bmax + 1] first pass: peak frequency at lag i (0 = not a candidate peak)
+  double* pks = pkf + P.bmax + 1;       // [bmax + 1] ... and its sinc(30) strength
+  double* part = r;                     // [F0_SEG - 1][bmax + 1] autocorrelation partial sums (before r is written)
   __shared__ double cf[F0_MAXC], cs[F0_MAXC];
   __shared__ int cim[F0_MAXC];
   __shared__ int ncs;
@@ -304,6 +312,7 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
   const double lmean = block_sum(s, red) / (2.0 * P.nsp);
   const int start = right - P.hnw;  // 1-based
   for (int j = threadIdx.x; j < P.nw; j += blockDim.x) frame[j] = ((double)x[start - 1 + j] - lmean) * win[j];
+  for (int j = P.nw + threadIdx.x; j < P.nw + P.bmax + 2 * F0_LB; j += blockDim.x) frame[j] = 0.0;
   __syncthreads();
   int s0 = P.hnw + 1 - P.hnsp, s1 = P.hnw + P.hnsp;
   if (s0 < 1) s0 = 1;
@@ -324,11 +333,64 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
     }
     return;
   }
-  // autocorrelation for lags 0..bmax (the zero padding to nfft >= 1.5 nw means no circular wrap)
-  for (int lag = threadIdx.x; lag <= P.bmax; lag += blockDim.x) {
-    double a = 0;
-    for (int j = 0; j + lag < P.nw; ++j) a += frame[j] * frame[j + lag];
-    r[P.bmax + lag] = a;
+  // autocorrelation for lags 0..bmax (the zero padding to nfft >= 1.5 nw means no circular wrap): thread (g, sg)
+  // sums lags [F0_LB g, F0_LB (g + 1)) over samples j of segment sg, with the F0_LB frame values x[j + lag] in a
+  // sliding register window (one broadcast and one lane read per F0_LB fmas; zeros past nw stand in for j + lag >= nw)
+  {
+    const int ng = (P.bmax + F0_LB) / F0_LB;  // lag groups
+    const int nseg = min(F0_SEG, (int)blockDim.x / ng);
+    const int seg = (P.nw + nseg - 1) / nseg;
+    const int g = threadIdx.x % ng, sg = threadIdx.x / ng;
+    double acc[F0_LB];
+#pragma unroll
+    for (int q = 0; q < F0_LB; ++q) acc[q] = 0.0;
+    if (sg < nseg) {
+      const int L0 = g * F0_LB, j0 = sg * seg, j1 = min(j0 + seg, P.nw);
+      double wv[F0_LB];
+#pragma unroll
+      for (int q = 0; q < F0_LB; ++q) wv[q] = frame[j0 + L0 + q];
+      int j = j0;
+      for (; j + F0_LB <= j1; j += F0_LB) {
+        double nv[F0_LB];
+#pragma unroll
+        for (int q = 0; q < F0_LB; ++q) nv[q] = frame[j + L0 + F0_LB + q];
+#pragma unroll
+        for (int u = 0; u < F0_LB; ++u) {
+          const double fj = frame[j + u];
+#pragma unroll
+          for (int q = 0; q < F0_LB; ++q) acc[q] = fma(fj, u + q < F0_LB ? wv[u + q] : nv[u + q - F0_LB], acc[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < F0_LB; ++q) wv[q] = nv[q];
+      }
+      for (; j < j1; ++j) {
+        const double fj = frame[j];
+#pragma unroll
+        for (int q = 0; q < F0_LB; ++q) acc[q] = fma(fj, frame[j + L0 + q], acc[q]);
+      }
+      if (sg > 0) {
+#pragma unroll
+        for (int q = 0; q < F0_LB; ++q)
+          if (L0 + q <= P.bmax) part[(sg - 1) * (P.bmax + 1) + L0 + q] = acc[q];
+      }
+    }
+    __syncthreads();
+    if (sg == 0) {
+#pragma unroll
+      for (int q = 0; q < F0_LB; ++q) {
+        const int lag = g * F0_LB + q;
+        if (lag <= P.bmax)
+          for (int t = 1; t < nseg; ++t) acc[q] += part[(t - 1) * (P.bmax + 1) + lag];
+      }
+    }
+    __syncthreads();  // partial sums read before r (which they alias) is written
+    if (sg == 0) {
+#pragma unroll
+      for (int q = 0; q < F0_LB; ++q) {
+        const int lag = g * F0_LB + q;
+        if (lag <= P.bmax) r[P.bmax + lag] = acc[q];
+      }
+    }
   }
   __syncthreads();
   const double ac0 = r[P.bmax];
@@ -603,9 +665,12 @@ int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double
   double* winR = (double*)take((size_t)(P.bmax + 1) * 8);
   hipLaunchKernelGGL(f0_global_kernel, dim3(B), dim3(1024), 0, s, wav, n, utt, gpeak);
   SVC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(f0_window_kernel, dim3(1), dim3(256), 0, s, P.nw, P.bmax, win, winR);
+  hipLaunchKernelGGL(f0_window_kernel, dim3(cdiv(P.bmax + 1, F0_WIN_WG)), dim3(F0_WIN_WG), 0, s, P.nw, P.bmax, win, winR);
   SVC_LAUNCH_CHECK();
-  const size_t lds = (size_t)(P.nw + 2 * P.bmax + 1 + 8 + 2 * (P.bmax + 1)) * sizeof(double);
+  // every lag group needs a thread of the 256-thread workgroup (nw <= 2048: at most 114 groups, >= 2 segments); the
+  // F0_SEG - 1 partial-sum rows fit the r / pkf / pks region (4 bmax + 3 doubles)
+  SVC_REQUIRE((P.bmax + F0_LB) / F0_LB <= 256, "f0: %d lags do not fit the autocorrelation blocking", P.bmax + 1);
+  const size_t lds = (size_t)(P.nw + P.bmax + 2 * F0_LB + 8 + 2 * P.bmax + 1 + 2 * (P.bmax + 1)) * sizeof(double);
   hipLaunchKernelGGL(f0_frame_kernel, dim3(P.nf, B), dim3(256), lds, s, wav, n, P, win, winR, gpeak, o, utt);
   SVC_LAUNCH_CHECK();
   const int pad = pad_of(n, P.nf);
