@@ -385,6 +385,27 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
         if (m >= M) continue;
         const int b = m / a.T_out, t = m - b * a.T_out;
         const int64_t orow = (int64_t)b * e.T_ostore + (int64_t)t * e.ostride + e.ophase;
+        // this row's residual operands for every column group, loaded before any of its stores (which may alias
+        // them, so the compiler cannot move a later group's loads above an earlier group's stores)
+        float4 pr[2][CF::FQN], pq[2][CF::FQN];  // RES32: add_row, acc32; SPLIT: the hi / lo halves as raw bits
+        if constexpr (FORM != G3_F16) {
+#pragma unroll
+          for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int j = 0; j < CF::FQN; ++j) {
+              const int n = min(n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4, a.N - 4);
+              pr[y][j] = pq[y][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+              if constexpr (FORM == G3_SPLIT) {
+                const uint2 h = *reinterpret_cast<const uint2*>(e.acc16_hi + orow * e.ld_acc + n);
+                const uint2 l = *reinterpret_cast<const uint2*>(e.acc16_lo + orow * e.ld_acc + n);
+                pq[y][j] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x),
+                                       __uint_as_float(l.y));
+              } else {
+                if (e.add_row) pr[y][j] = *reinterpret_cast<const float4*>(e.add_row + orow * e.ld_add_row + n);
+                if (e.acc32) pq[y][j] = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
+              }
+            }
+        }
 #pragma unroll
         for (int y = 0; y < 2; ++y)
 #pragma unroll
@@ -416,7 +437,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
             } else {
               if constexpr (FORM == G3_RES32) {
                 if (e.add_row) {
-                  const float4 ar = *reinterpret_cast<const float4*>(e.add_row + orow * e.ld_add_row + n);
+                  const float4 ar = pr[y][j];
                   v.x += ar.x; v.y += ar.y; v.z += ar.z; v.w += ar.w;
                 }
               }
@@ -424,15 +445,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
               bool has_acc = true;
               if constexpr (FORM == G3_SPLIT) {
                 H4 hi, lo;
-                hi.u = *reinterpret_cast<const uint2*>(e.acc16_hi + orow * e.ld_acc + n);
-                lo.u = *reinterpret_cast<const uint2*>(e.acc16_lo + orow * e.ld_acc + n);
+                hi.u = make_uint2(__float_as_uint(pq[y][j].x), __float_as_uint(pq[y][j].y));
+                lo.u = make_uint2(__float_as_uint(pq[y][j].z), __float_as_uint(pq[y][j].w));
                 ac.x = ((float)hi.h[0] + (float)lo.h[0]) - cs[y][j].x;
                 ac.y = ((float)hi.h[1] + (float)lo.h[1]) - cs[y][j].y;
                 ac.z = ((float)hi.h[2] + (float)lo.h[2]) - cs[y][j].z;
                 ac.w = ((float)hi.h[3] + (float)lo.h[3]) - cs[y][j].w;
               } else {
                 has_acc = e.acc32 != nullptr;
-                if (has_acc) ac = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
+                if (has_acc) ac = pq[y][j];
               }
               if (has_acc) {
                 v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
