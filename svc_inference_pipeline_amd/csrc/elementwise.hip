@@ -3,6 +3,8 @@
 // sampler updates (DDPM / PLMS), mel de-normalisation, conv_post+tanh+fade.
 // All tensors are time-major [rows = b*T + t][channels].
 #include <cstdlib>
+#include <type_traits>
+
 #include "common.h"
 
 namespace svc {
@@ -53,21 +55,92 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     }
 }
 
+// D % 256 == 0 (Whisper 1024, HuBERT 768): element c = q * 256 + 4 * lane + k, so every load / store instruction of
+// the wave is one contiguous 1 KiB (f32) / 512 B (f16) run: 16-B loads and 8-B stores instead of 4-B / 2-B ones
+template <typename OutT, bool SPLIT>
+__global__ __launch_bounds__(256) void layernorm_v4_kernel(const float* __restrict__ x, const float* __restrict__ gam,
+                                                           const float* __restrict__ bet, OutT* __restrict__ y,
+                                                           int rows, int D, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * D;
+  const int nq = D / 256;  // <= 4
+  float4 v[4];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < nq) {
+      v[q] = *reinterpret_cast<const float4*>(xr + q * 256 + 4 * lane);
+      s += (v[q].x + v[q].y) + (v[q].z + v[q].w);
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  const float mean = s / (float)D;
+  float ss = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < nq) {
+      const float a = v[q].x - mean, b = v[q].y - mean, c = v[q].z - mean, d = v[q].w - mean;
+      ss += (a * a + b * b) + (c * c + d * d);
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  const float rstd = 1.0f / sqrtf(ss / (float)D + 1e-5f);
+  OutT* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < nq) {
+      const int c = q * 256 + 4 * lane;
+      const float4 g = *reinterpret_cast<const float4*>(gam + c);
+      const float4 bb = *reinterpret_cast<const float4*>(bet + c);
+      const float o[4] = {(v[q].x - mean) * rstd * g.x + bb.x, (v[q].y - mean) * rstd * g.y + bb.y,
+                          (v[q].z - mean) * rstd * g.z + bb.z, (v[q].w - mean) * rstd * g.w + bb.w};
+      if constexpr (std::is_same<OutT, float>::value) {
+        *reinterpret_cast<float4*>(yr + c) = make_float4(o[0], o[1], o[2], o[3]);
+        continue;
+      }
+      union { uint2 u; f16 h[4]; } hi, lo;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) hi.h[k] = (f16)o[k];
+      *reinterpret_cast<uint2*>(yr + c) = hi.u;
+      if constexpr (SPLIT) {  // split-fp16 operand [hi | lo | hi] (ldy >= 3 D)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) lo.h[k] = (f16)(o[k] - (float)hi.h[k]);
+        *reinterpret_cast<uint2*>(yr + D + c) = lo.u;
+        *reinterpret_cast<uint2*>(yr + 2 * D + c) = hi.u;
+      }
+    }
+}
+
 int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int rows, int D, int ldy, hipStream_t s) {
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm: D=%d", D);
-  hipLaunchKernelGGL(layernorm_kernel<f16>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy);
+  if (D % 256 == 0 && ldy % 4 == 0)
+    hipLaunchKernelGGL((layernorm_v4_kernel<f16, false>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D,
+                       ldy);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<f16>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
 int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s) {
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm: D=%d", D);
-  hipLaunchKernelGGL((layernorm_kernel<f16, true>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, 3 * D);
+  if (D % 256 == 0)
+    hipLaunchKernelGGL((layernorm_v4_kernel<f16, true>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D,
+                       3 * D);
+  else
+    hipLaunchKernelGGL((layernorm_kernel<f16, true>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D,
+                       3 * D);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
 int layernorm_f32(const float* x, const float* g, const float* b, float* y, int rows, int D, int ldy, hipStream_t s) {
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm: D=%d", D);
-  hipLaunchKernelGGL(layernorm_kernel<float>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy);
+  if (D % 256 == 0 && ldy % 4 == 0)
+    hipLaunchKernelGGL((layernorm_v4_kernel<float, false>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D,
+                       ldy);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<float>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
