@@ -110,6 +110,10 @@ int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
 bool conv_gemm4_rmw_form(const ConvGemmArgs& a, const EpiArgs& e);
+bool diff_layer_form(const ConvGemmArgs& a);
+int diff_layer(const ConvGemmArgs& a, const float* bias1, const f16* cp, f16* g, const f16* W2, const float* bias2,
+               f16* lo, f16* hi_out, const float* sub, const float* add, float acc_div, const f16* zpage,
+               hipStream_t s, int dbg);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s);
@@ -278,7 +282,8 @@ void Tuning::from_env() {
               {"SVC_AMP_MODE", &amp_mode},         {"SVC_AMP_RUN", &amp_run},           {"SVC_AMP_DBG", &amp_dbg},
               {"SVC_AMP_FUSED", &amp_fused},       {"SVC_AMP_MAXC", &amp_maxc},         {"SVC_WHISPER_STREAMS", &whisper_streams},
               {"SVC_SAMPLER_STREAMS", &sampler_streams}, {"SVC_VOCODER_STREAMS", &vocoder_streams},
-              {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg},             {"SVC_DFT_DBG", &dft_dbg}};
+              {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg},             {"SVC_DFT_DBG", &dft_dbg},
+              {"SVC_DIFF_FUSED", &diff_fused},     {"SVC_DIFF_DBG", &diff_dbg}};
   for (auto& it : ints)
     if (const char* v = getenv(it.env)) *it.v = atoi(v);
   if (const char* v = getenv("SVC_AMP_LDS")) amp_lds_max = v[0] == 'm' ? 1 : 0;
@@ -295,7 +300,7 @@ bool Tuning::set(const char* name, double v) {
               {"amp_dbg", &amp_dbg},           {"amp_fused", &amp_fused},       {"amp_maxc", &amp_maxc},
               {"whisper_streams", &whisper_streams}, {"sampler_streams", &sampler_streams},
               {"vocoder_streams", &vocoder_streams}, {"diff_res32", &diff_res32}, {"f0_dbg", &f0_dbg},
-              {"dft_dbg", &dft_dbg}};
+              {"dft_dbg", &dft_dbg},           {"diff_fused", &diff_fused},     {"diff_dbg", &diff_dbg}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) {
       *it.v = (int)v;
@@ -1886,6 +1891,7 @@ struct DenoiseBufs {
   f16* s16;      // [rows][3C] sum(skip) / sqrt(NL) ([hi | lo | hi] split-fp16 with head_split, else [rows][C])
   f16* u16;      // [rows][3C] relu(skip_projection), same layout
   f16* lo16;     // [rows][C] low half of the split residual stream: x + dproj = y16 + lo16 (default path)
+  f16* y16b;     // [rows][C] the fused layers' second hi buffer (diff_layer reads one and writes the other)
   size_t cp_ls;  // elements between layers of cp16, which is LAYER-major [NL][rows_total][2C]: each layer's gate
                  // epilogue reads one contiguous block (row-major over all layers put 30 KB between its rows)
   size_t g_ls;   // elements between layers of g16, also layer-major [NL][rows_total][C]: the gate GEMM writes and the
@@ -1917,6 +1923,10 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
   if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
+  // Fused layers (diff_layer.hip, default): gate GEMM, output projection and residual update in one launch per layer,
+  // the hi half ping-ponging between y16 and y16b; the last layer (no residual) is the gate GEMM alone.
+  const bool fused = !res32 && tuning().diff_fused && NL > 1;
+  f16* hi_cur = bb.y16;
   for (int i = 0; i < NL; ++i) {
     EpiArgs g = epi();
     g.kind = EPI_GATE;
@@ -1924,7 +1934,23 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     g.ld_cp = 2 * C;
     g.y16 = bb.g16 + (size_t)i * bb.g_ls;
     g.ldy16 = C;
-    if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s, "diffsvc.dilated", tv, 1))) return st;
+    if (fused && i + 1 < NL) {
+      EpiArgs g2 = g;
+      ConvGemmArgs a = gemm_args(c->dil[i], hi_cur, C, C, B, T, T, g2);
+      a.tv = tv;
+      a.tv_mul = 1;
+      if (diff_layer_form(a)) {
+        f16* hi_next = hi_cur == bb.y16 ? bb.y16b : bb.y16;
+        prof_site("diffsvc.layer");
+        if ((st = diff_layer(a, c->dil[i].bias, g.cp, g.y16, c->outres[i].W, c->outres[i].bias, bb.lo16, hi_next,
+                             dp + (size_t)i * C, dp + (size_t)(i + 1) * C, 1.41421356237309515f, zero_page(), s,
+                             tuning().diff_dbg)))
+          return st;
+        hi_cur = hi_next;
+        continue;
+      }
+    }
+    if ((st = run_gemm(c->dil[i], hi_cur, C, C, B, T, T, g, s, "diffsvc.dilated", tv, 1))) return st;
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
     // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step)
     EpiArgs r = epi();
@@ -1935,12 +1961,12 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
       r.out32 = bb.h32;
       r.ld32 = C;
     } else {  // x_i = (y16 + lo16) - dproj_i, and x_{i+1} + dproj_{i+1} goes back split into y16 / lo16
-      r.acc16_hi = bb.y16;
+      r.acc16_hi = hi_cur;
       r.acc16_lo = bb.lo16;
       r.acc_sub = dp + (size_t)i * C;
       r.lo16 = bb.lo16;
     }
-    r.out16 = bb.y16;
+    r.out16 = hi_cur;
     r.ld16 = C;
     r.add16 = dp + (size_t)(i + 1) * C;
     if ((st = run_gemm(c->outres[i], bb.g16 + (size_t)i * bb.g_ls, C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
@@ -1985,13 +2011,14 @@ static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   WS_GET(f16, s16, rows * C * 3);  // [hi | lo | hi] when head_split
   WS_GET(f16, u16, rows * C * 3);
   WS_GET(f16, lo16, rows * C);
-  bb = DenoiseBufs{cp16, h32, y16, g16, s16, u16, lo16, rows * 2 * C, rows * C};
+  WS_GET(f16, y16b, rows * C);
+  bb = DenoiseBufs{cp16, h32, y16, g16, s16, u16, lo16, y16b, rows * 2 * C, rows * C};
   return SVC_OK;
 }
 
 static size_t denoise_bytes(svc_ctx* c, int B, int T) {
   const size_t rows = (size_t)B * T, C = c->C;
-  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 8) + 22 * 4096;
+  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 9) + 24 * 4096;
 }
 
 static int project_cond(svc_ctx* c, const float* cond, int B, int T, const DenoiseBufs& bb, hipStream_t s) {
@@ -2123,7 +2150,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
     const size_t r = u.r0;
     const int C = c->C;
     return DenoiseBufs{bb.cp16 + r * 2 * C, bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * 3 * C,
-                       bb.u16 + r * 3 * C, bb.lo16 + r * C, bb.cp_ls, bb.g_ls};
+                       bb.u16 + r * 3 * C, bb.lo16 + r * C, bb.y16b + r * C, bb.cp_ls, bb.g_ls};
   };
   SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
   for (int h = 0; h < S && S > 1; ++h) SVC_HIP_CHECK(hipStreamWaitEvent(sub[h].s, c->ev_fork, 0));

@@ -161,12 +161,39 @@ def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, tune):
     if variant.startswith("rmw"):
         tune(engine, gemm4_rmw=1, diff_res32=int(variant == "rmw32"))
         variant = "15"
-    tune(engine, gemm_variant=variant)
+    tune(engine, gemm_variant=variant, diff_fused=0)
     eps = engine.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()
     with torch.no_grad():
         ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond),
                                  torch.full((B,), 250, dtype=torch.long), table).numpy()
     assert rel_l2(eps, ref) < 5e-3
+
+
+@pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700), (5, 937)])
+def test_fused_layer_bit_identical(engine, states, cfg, B, T, tune):
+    """diff_layer.hip (dilated conv + gate + residual projection + split-fp16 residual update in ONE launch per layer,
+    the default) against the unfused kernels with the same K order, MFMA operand order and epilogue expressions
+    (conv_gemm4's register gate epilogue + its register residual epilogue): bit-identical eps on row counts that are not
+    multiples of the 128-row tile, utterance boundaries inside tiles and per-utterance frame counts (ragged dilated-conv
+    zero padding); the default unfused path (LDS-staged residual epilogue) within 1e-5, the oracle within 5e-3."""
+    rng = np.random.default_rng(B * 31 + T)
+    cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
+    x = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
+    frames = [max(1, T - 37 * b) for b in range(B)]
+    out = {}
+    for name, sw in (("fused", dict(diff_fused=1)), ("rmw", dict(diff_fused=0, gemm4_rmw=1)),
+                     ("lds", dict(diff_fused=0, gemm4_rmw=0))):
+        tune(engine, **sw)
+        out[name] = (engine.diffsvc_eps(cond, x, 250, frames=frames), engine.diffsvc_eps(cond, x, 7))
+    for k in range(2):
+        assert torch.equal(out["fused"][k], out["rmw"][k]), (k, rel_l2(out["fused"][k].cpu().numpy(),
+                                                                       out["rmw"][k].cpu().numpy()))
+        assert rel_l2(out["fused"][k].cpu().numpy(), out["lds"][k].cpu().numpy()) < 1e-5
+    table = W.step_embedding_table(1000)
+    with torch.no_grad():
+        ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, x.cpu(), cond.cpu(), torch.full((B,), 7, dtype=torch.long),
+                                 table).numpy()
+    assert rel_l2(out["fused"][1].cpu().numpy(), ref) < 5e-3
 
 
 @pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "24"])
@@ -176,7 +203,7 @@ def test_eps_gemm_variants(engine, golden, variant, tune):
     if variant in ("15lds", "15reg"):
         tune(engine, gemm3_direct=0 if variant == "15lds" else 15)
         variant = "15"
-    tune(engine, gemm_variant=variant)
+    tune(engine, gemm_variant=variant, diff_fused=0)
     g = golden("conditioner_diffsvc")
     eps = engine.diffsvc_eps(dev(g["cond"]), dev(g["x_in"]), 500)
     assert rel_l2(eps.cpu().numpy(), g["eps_t500"]) < 5e-3
