@@ -19,6 +19,9 @@
 // and written only by the row's own tile, stays in place).
 // Both GEMMs keep the unfused path's K order (32-deep K-steps in ascending K) and MFMA operand order, and the epilogues
 // are the same expressions, so the layer is bit-identical to conv_gemm4 (gate) + conv_gemm4 (register residual update).
+// Opt-in (tuning diff_fused): 118-125 us per full-batch layer against 71 + 42 us for the two kernels, because with one
+// workgroup per CU the per-tile epilogue traffic (cp 46 MB, residual 92 MB per layer) runs as an un-overlapped burst
+// (DESIGN.md "Fused residual layer, round 2"; tuning diff_dbg splits the time).
 #include <type_traits>
 #include <utility>
 
@@ -70,7 +73,8 @@ struct DiffLayerArgs {
   float acc_div;               // sqrt(2)
   int dbg;                     // diagnostics (tuning diff_dbg): 1 A from the zero page, 2 no GEMM1 MFMAs,
                                // 4 B from one fixed K-step of W_dil, 8 no epilogue HBM traffic (16 no cp loads,
-                               // 32 no residual read-modify-write, 64 no gate-output stores)
+                               // 32 no residual read-modify-write, 64 no gate-output stores, 128 no residual loads,
+                               // 256 no residual stores)
 };
 
 template <typename F, int... K>
@@ -319,6 +323,10 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_layer_kernel(DiffLayerArgs p, c
     DlH4 hi[6], lo[6];
 #pragma unroll
     for (int j = 0; j < 6; ++j) {  // the row's residual operands first: the stores below may alias later loads
+      if (p.dbg & 128) {
+        hi[j].u = lo[j].u = make_uint2(0u, 0u);
+        continue;
+      }
       hi[j].u = *reinterpret_cast<const uint2*>(a.X + (int64_t)m * DL_C + nb + j * 16);
       lo[j].u = *reinterpret_cast<const uint2*>(p.lo + (int64_t)m * DL_C + nb + j * 16);
     }
@@ -343,6 +351,10 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_layer_kernel(DiffLayerArgs p, c
       pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
       lw.h[0] = (f16)(w.x - (float)pk.h[0]); lw.h[1] = (f16)(w.y - (float)pk.h[1]);
       lw.h[2] = (f16)(w.z - (float)pk.h[2]); lw.h[3] = (f16)(w.w - (float)pk.h[3]);
+      if (p.dbg & 256) {
+        if (pk.u.x == 0x12345u && lw.u.y == 0x54321u) p.hi_out[0] = (f16)1.f;  // keep the arithmetic
+        continue;
+      }
       *reinterpret_cast<uint2*>(p.hi_out + (int64_t)m * DL_C + n) = pk.u;
       *reinterpret_cast<uint2*>(p.lo + (int64_t)m * DL_C + n) = lw.u;
     }
