@@ -249,6 +249,8 @@ struct Param {
 struct WBlock {
   float *ln1_g, *ln1_b, *ln2_g, *ln2_b;
   PackedGemm qkv, out, fc1, fc2;
+  PackedGemm v;         // value projection as its own GEMM when its weight split differs from q / k's
+  bool split_v = false;  // (then qkv holds the q and k columns only)
 };
 
 struct HBlock {  // post-LN fairseq TransformerSentenceEncoderLayer
@@ -721,6 +723,10 @@ int build_whisper(svc_ctx* c) {
   // attention linears only; the error enters early and through the attention; DESIGN.md "precision")
   const uint64_t wsplit_attn = (uint64_t)cfgv(c, "content.wsplit_attn", 9007199254740991.0);  // 2^53 - 1: all blocks
   const uint64_t wsplit_mlp = (uint64_t)cfgv(c, "content.wsplit_mlp", 15.0);
+  // finer masks for the attention linears (default: wsplit_attn for each): q / k, v, out
+  const uint64_t wsplit_qk = (uint64_t)cfgv(c, "content.wsplit_qk", (double)wsplit_attn);
+  const uint64_t wsplit_v = (uint64_t)cfgv(c, "content.wsplit_v", (double)wsplit_attn);
+  const uint64_t wsplit_out = (uint64_t)cfgv(c, "content.wsplit_out", (double)wsplit_attn);
   for (int i = 0; i < L; ++i) {
     std::string p = "whisper.encoder.blocks." + std::to_string(i) + ".";
     WBlock& b = c->wblocks[i];
@@ -747,13 +753,21 @@ int build_whisper(svc_ctx* c) {
     auto lin = [&](const Param* w) { return [w](int n, int ci, int) { return w->host[(int64_t)n * (w->shape[1]) + ci]; }; };
     auto bias = [&](const Param* b0) { return [b0](int n) { return b0->host[n]; }; };
     // weight-split mode: "content.wsplit_attn" / "content.wsplit_mlp" (bit i: block i) choose the blocks whose
-    // attention linears (qkv, out) / MLP linears (fc1, fc2) get [W_hi; W_lo]; the others run on plain fp16 weights
+    // attention linears (qkv, out) / MLP linears (fc1, fc2) get [W_hi; W_lo]; the others run on plain fp16 weights.
+    // "content.wsplit_qk" / "content.wsplit_v" / "content.wsplit_out" refine the attention mask per linear (bits 1 /
+    // 16 / 2 of lmode); fc1 / fc2 are bits 4 / 8
     auto lmode = [&](int bit) {
       if (mode != 2) return mode;
-      const uint64_t m = bit <= 2 ? wsplit_attn : wsplit_mlp;
+      const uint64_t m = bit == 1 ? wsplit_qk : bit == 2 ? wsplit_out : bit == 16 ? wsplit_v : wsplit_mlp;
       return ((m >> (i < 53 ? i : 52)) & 1) ? 2 : 0;
     };
-    if ((st = pack_linear_mode(c, b.qkv, 3 * D, D, lmode(1), qkv_w, qkv_b))) return st;
+    b.split_v = lmode(1) != lmode(16);
+    if (!b.split_v) {
+      if ((st = pack_linear_mode(c, b.qkv, 3 * D, D, lmode(1), qkv_w, qkv_b))) return st;
+    } else {  // q | k on one GEMM, v on another, each with its own operand precision
+      if ((st = pack_linear_mode(c, b.qkv, 2 * D, D, lmode(1), qkv_w, qkv_b))) return st;
+      if ((st = pack_linear_mode(c, b.v, D, D, lmode(16), lin(vw), bias(vb)))) return st;
+    }
     // the attention output (A of `out`) is fp16 (the attention kernel's P.V path is fp16 either way): split3 would
     // only split the weights, which the weight-split mode does at 2x
     if ((st = pack_linear_mode(c, b.out, D, D, mode == 2 ? lmode(2) : 0, lin(ow), bias(ob)))) return st;
@@ -1655,6 +1669,12 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
       e.scale_cols = 2 * D;
       e.col_scale = qk_scale;
       if ((st = run_gemm(b.qkv, n16h, D * X3, D * X3, Bh, L, L, e, hs, "whisper.qkv"))) return st;
+      if (b.split_v) {
+        e = epi();
+        e.out16 = qkvh + 2 * D;
+        e.ld16 = 3 * D;
+        if ((st = run_gemm(b.v, n16h, D * X3, D * X3, Bh, L, L, e, hs, "whisper.v"))) return st;
+      }
       if ((st = attention(qkvh, o16h, Bh, L, D, hs))) return st;
       e = epi();
       e.add_row = xh;

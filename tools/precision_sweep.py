@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--wsplit-variants", default="",
                     help="with --gpu, only these weight-split Whisper variants: comma-separated attn_mask:mlp_mask "
+                         "or attn:mlp:qk:v:out masks "
                          "(content.wsplit_attn / content.wsplit_mlp, bit i = block i; e.g. 16777215:0 = attention "
                          "linears of all 24 blocks, no MLP linear)")
     ap.add_argument("--seed", type=int, default=7, help="synthetic clip seed")
@@ -127,9 +128,13 @@ def main():
         if args.wsplit_variants:
             variants = []
             for v in args.wsplit_variants.split(","):
-                att, mlp = (int(x) for x in v.split(":"))
-                variants.append((f"gpu, weight-split attention {att:#x} MLP {mlp:#x} + split-fp16 DiffSVC head", 2, True,
-                                 {"content.wsplit_attn": att, "content.wsplit_mlp": mlp}))
+                f = [int(x, 0) for x in v.split(":")]
+                extra = {"content.wsplit_attn": f[0], "content.wsplit_mlp": f[1]}
+                name = f"gpu, weight-split attention {f[0]:#x} MLP {f[1]:#x}"
+                if len(f) == 5:  # att:mlp:qk:v:out
+                    extra.update({"content.wsplit_qk": f[2], "content.wsplit_v": f[3], "content.wsplit_out": f[4]})
+                    name += f" (qk {f[2]:#x} v {f[3]:#x} out {f[4]:#x})"
+                variants.append((name + " + split-fp16 DiffSVC head", 2, True, extra))
         for name, split, head, extra in variants:
             e = SVCEngine(cfg, 0, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs,
                           content_split=split, head_split=head, config=extra)
