@@ -136,3 +136,41 @@ def test_ragged_sampler_and_vocoder(tiny_engine, fast):
         w1 = e.bigvgan(one)
         assert torch.equal(wav[i, :t * 256], w1[0]), i
         assert not wav[i, t * 256:].any()
+
+
+def test_server_matches_single_clips():
+    """F3 streaming front end (serving.SVCServer): clips submitted one at a time from two threads, batched by the
+    worker into ragged batches, each come back bit-identical to converting that clip alone with its utterance id."""
+    import threading
+
+    from svc_inference_pipeline_amd.serving import SVCServer
+
+    cfg = C.load_config()
+    dims = W.WHISPER_DIMS["tiny-test"]
+    cfg.mapper.input_content_dim["whisper"] = dims["n_audio_state"]
+    e = SVCEngine(cfg, 0, whisper_state=W.make_whisper_state(dims, 0), mapper_state=W.make_mapper_state(cfg.mapper, 0),
+                  vocoder_state=W.make_vocoder_state(cfg.vocoder, 0))
+    try:
+        pipe = SVCPipeline(e)
+        secs = [0.5, 0.62, 0.45, 1.1, 0.55, 0.3]
+        w24 = [dev(ON.synth_clip(90 + i, s, 24000)) for i, s in enumerate(secs)]
+        w16 = [dev(ON.synth_clip_16k_quantised(90 + i, s)) for i, s in enumerate(secs)]
+        futs = {}
+        with SVCServer(pipe, max_batch=4, max_wait_s=0.2, speedup=250, seed=9) as srv:
+            def submit(idx):
+                for i in idx:
+                    futs[i] = srv.submit(w24[i], w16[i], singer=i % 5, utt_id=40 + i)
+            ts = [threading.Thread(target=submit, args=(idx,)) for idx in ([0, 2, 4], [1, 3, 5])]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            outs = {i: f.result(timeout=120) for i, f in futs.items()}
+        assert sorted(u for b in srv.batches for u in b) == [40 + i for i in range(len(secs))]
+        assert any(len(b) > 1 for b in srv.batches)
+        for i in range(len(secs)):
+            one = pipe.convert(w24[i][None], w16[i][None], dev(np.array([i % 5]), torch.int32), speedup=250, seed=9,
+                               utt_ids=dev(np.array([40 + i]), torch.int32)).wav[0]
+            assert torch.equal(outs[i], one), i
+    finally:
+        e.close()
