@@ -369,6 +369,15 @@ def main():
                 (f", {ent['workgroups']}-workgroup launches" if "workgroups" in ent else "") + ")"
             if "rocprof_trace_avg_us" in ent:
                 roof["rocprof_avg_launch_us"] = ent["rocprof_trace_avg_us"]
+    # MFMA utilisation of the roofline kernel's largest grid from the serialised PMC passes (tools/pmc_kernels.sh):
+    # SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE x 1024 SIMDs, per dispatch
+    pmc_k = os.path.join(os.path.dirname(args.pmc_json), "pmc_kernels.json")  # latest tools/pmc_kernels.sh summary
+    if os.path.exists(pmc_k):
+        ents = [v for v in json.load(open(pmc_k)).values() if v.get("kernel") == dom_name and "mfma_busy" in v]
+        if ents:
+            big = max(ents, key=lambda v: v["workgroups"])
+            roof["mfma_busy_pmc"] = round(big["mfma_busy"], 3)
+            roof["mfma_busy_source"] = os.path.relpath(pmc_k, REPO) + f" ({big['workgroups']}-workgroup launches)"
     # per-kernel breakdown of the fully profiled warmup step
     total_flops = sum(v["flops"] for v in prof_all.values())
     kernels = {k: {"ms_per_step": round(v["ms"], 3), "launches_per_step": v["launches"],

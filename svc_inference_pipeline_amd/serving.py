@@ -14,6 +14,7 @@ it (so padding stays bounded: the kernels skip the padded tail, but its rows sti
 carries an utterance id (given, or a running counter) that keys its device noise, so its waveform is bit-identical to
 converting that clip alone with the same id, whatever it was batched with (tests/test_gpu_ragged.py).
 """
+import collections
 import itertools
 import threading
 import time
@@ -54,7 +55,7 @@ class SVCServer:
         self._pending = []
         self._cv = threading.Condition()
         self._closed = False
-        self.batches = []  # (utterance ids of each batch run), for inspection and tests
+        self.batches = collections.deque(maxlen=4096)  # utterance ids of the most recent batches (inspection, tests)
         self._device = getattr(pipeline.engine, "device", None)
         self._worker = threading.Thread(target=self._run, name="svc-server", daemon=True)
         self._worker.start()

@@ -37,7 +37,7 @@ def test_batches_by_length_and_resolves_in_order():
     outs = [f.result(timeout=10) for f in futs]
     srv.close()
     # mel frames 3, 4, 19, 3, 20: the oldest request's batch takes the clips within 2x of its length
-    assert srv.batches == [[0, 1, 3], [2, 4]]
+    assert list(srv.batches) == [[0, 1, 3], [2, 4]]
     for i, (n, o) in enumerate(zip(lens, outs)):
         assert o.shape == (n,) and torch.equal(o, clip(n, 0.5) * (i + 1) + i)
     assert all(kw == dict(fast_inference=True, speedup=250, seed=3) for _, kw in p.calls)
@@ -48,7 +48,7 @@ def test_max_batch_and_explicit_ids():
     with SVCServer(p, max_batch=2, max_wait_s=0.3) as srv:
         futs = [srv.submit(clip(2000), clip(1000), singer=0, utt_id=100 + i) for i in range(5)]
         res = [f.result(timeout=10) for f in futs]
-    assert srv.batches == [[100, 101], [102, 103], [104]]
+    assert list(srv.batches) == [[100, 101], [102, 103], [104]]
     assert [float(r[0]) for r in res] == [101.0, 102.0, 103.0, 104.0, 105.0]
 
 
