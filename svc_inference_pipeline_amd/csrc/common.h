@@ -79,6 +79,21 @@ __device__ __forceinline__ float fast_sigmoid(float x) {
 __device__ __forceinline__ float fast_tanh(float x) {  // 1 - 2 / (1 + e^{2x}): +-1 at the saturated ends
   return 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(2.8853900817779268f * x));
 }
+// The DiffSVC gate sigmoid(a) * tanh(b) (modules/diffsvc.py:226-227) on two v_exp_f32 and ONE v_rcp_f32:
+// tanh(b) = sign(b) (1 - E2) / (1 + E2) with E2 = e^{-2|b|} in [0, 1], sigmoid(a) = 1 / (1 + E1), E1 = e^{-a}, so the
+// product is sign(b) (1 - E2) / ((1 + E1)(1 + E2)). E1's exponent is capped at 2^64 (a < -44: sigmoid < 6e-20, returned
+// as ~5e-20): an infinite E1 times an underflowed E2 would make the denominator NaN, which the PLMS-100 trajectory of
+// random weights reaches. The select keeps a NaN argument NaN; |result| <= 1, so its f16 store needs no saturation.
+// Within 1-2 ulp of sigmoid * tanh (the fp32 oracle with this form tracks the reference's PLMS-100 to 2.4e-7).
+__device__ __forceinline__ float gate_act(float a, float b) {
+  float t1 = -1.4426950408889634f * a;
+  t1 = t1 > 64.0f ? 64.0f : t1;
+  const float e1 = __builtin_amdgcn_exp2f(t1);
+  const float e2 = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(b));
+  const float d1 = 1.0f + e1;
+  const float r = (1.0f - e2) * __builtin_amdgcn_rcpf(fmaf(d1, e2, d1));
+  return copysignf(r, b);
+}
 
 // ------------------------------------------------------------------ implicit-GEMM descriptors
 // Y[m, n] = epilogue( sum_{tap, c} X[in_row(m, tap), c] * Wp[n, tap*Cp + c] )

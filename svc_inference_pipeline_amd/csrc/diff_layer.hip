@@ -260,10 +260,10 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_layer_kernel(DiffLayerArgs p, c
         const float4 f = make_float4(acc[i][j + 2][0] + bfl[j].x, acc[i][j + 2][1] + bfl[j].y,
                                      acc[i][j + 2][2] + bfl[j].z, acc[i][j + 2][3] + bfl[j].w);
         DlH4 pk;
-        pk.h[0] = f16_sat(fast_sigmoid(g.x + (float)cpg[i][j].h[0]) * fast_tanh(f.x + (float)cpf[i][j].h[0]));
-        pk.h[1] = f16_sat(fast_sigmoid(g.y + (float)cpg[i][j].h[1]) * fast_tanh(f.y + (float)cpf[i][j].h[1]));
-        pk.h[2] = f16_sat(fast_sigmoid(g.z + (float)cpg[i][j].h[2]) * fast_tanh(f.z + (float)cpf[i][j].h[2]));
-        pk.h[3] = f16_sat(fast_sigmoid(g.w + (float)cpg[i][j].h[3]) * fast_tanh(f.w + (float)cpf[i][j].h[3]));
+        pk.h[0] = (f16)gate_act(g.x + (float)cpg[i][j].h[0], f.x + (float)cpf[i][j].h[0]);
+        pk.h[1] = (f16)gate_act(g.y + (float)cpg[i][j].h[1], f.y + (float)cpf[i][j].h[1]);
+        pk.h[2] = (f16)gate_act(g.z + (float)cpg[i][j].h[2], f.z + (float)cpf[i][j].h[2]);
+        pk.h[3] = (f16)gate_act(g.w + (float)cpg[i][j].h[3], f.w + (float)cpf[i][j].h[3]);
         const int q = wn * 4 + j * 2 + (fk >> 1);  // 16-B chunk of the pass's 128 channels
         *reinterpret_cast<uint2*>(G + row * 256 + (dl_swg(row, q) << 4) + (fk & 1) * 8) = pk.u;
       }

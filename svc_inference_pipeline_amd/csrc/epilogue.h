@@ -111,10 +111,10 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
       union { uint2 u; f16 h[4]; } pk, c1, c2;  // EPI_GATE
       c1.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n);
       c2.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n + 32);
-      pk.h[0] = f16_sat(fast_sigmoid(v1.x + (float)c1.h[0]) * fast_tanh(v2.x + (float)c2.h[0]));
-      pk.h[1] = f16_sat(fast_sigmoid(v1.y + (float)c1.h[1]) * fast_tanh(v2.y + (float)c2.h[1]));
-      pk.h[2] = f16_sat(fast_sigmoid(v1.z + (float)c1.h[2]) * fast_tanh(v2.z + (float)c2.h[2]));
-      pk.h[3] = f16_sat(fast_sigmoid(v1.w + (float)c1.h[3]) * fast_tanh(v2.w + (float)c2.h[3]));
+      pk.h[0] = (f16)gate_act(v1.x + (float)c1.h[0], v2.x + (float)c2.h[0]);
+      pk.h[1] = (f16)gate_act(v1.y + (float)c1.h[1], v2.y + (float)c2.h[1]);
+      pk.h[2] = (f16)gate_act(v1.z + (float)c1.h[2], v2.z + (float)c2.h[2]);
+      pk.h[3] = (f16)gate_act(v1.w + (float)c1.h[3], v2.w + (float)c2.h[3]);
       *reinterpret_cast<uint2*>(e.y16 + (int64_t)m * e.ldy16 + ch) = pk.u;
     }
   }
