@@ -1,0 +1,8 @@
+# DiffSVC output-projection tile per call site (SVC_SITE_VARIANT), 3-stream PLMS-100 sampler wall time
+set -o pipefail
+mkdir -p gpurun_out
+for v in "" 10 11 12 13 14 24; do
+  if [ -n "$v" ]; then export SVC_SITE_VARIANT="diffsvc.outproj=$v"; else unset SVC_SITE_VARIANT; fi
+  timeout -k 10 120 python3 -u tools/sampler_probe.py "{}" > gpurun_out/ops_$v.log 2>&1 || exit $?
+  echo "variant ${v:-default}: $(grep -m1 wall gpurun_out/ops_$v.log) $(grep -m1 outproj gpurun_out/ops_$v.log)"
+done
