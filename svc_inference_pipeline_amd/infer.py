@@ -3,6 +3,7 @@ converted wav, on one MI355X through libsvc_hip.so.
 
     python -m svc_inference_pipeline_amd.infer --wav test_set/1100000814.wav --singer svcc_CDF1 \\
         --mapper-ckpt mapper.pt --vocoder-ckpt vocoder.pt --whisper-ckpt medium.pt [--fast] [--out gen/x.wav]
+    python -m svc_inference_pipeline_amd.infer --wav a.wav b.wav c.wav ...   # several files: one ragged batch
 
 Same sequence as the reference: acoustic features (mel, energy, Praat F0) -> pitch shift to the target
 singer -> Whisper content features -> DiffSVC sampler (DDPM-1000 by default, PLMS with --fast, as
@@ -58,11 +59,32 @@ def convert_file(engine, cfg, wav_path, singer_name, fast_inference=False, speed
     return res.wav[0].cpu().numpy(), res.mel.shape[1]
 
 
+def convert_files(engine, cfg, wav_paths, singer_name, fast_inference=False, speedup=10, seed=0, device="cuda"):
+    """Several files as ONE ragged batch (SVCPipeline.convert_many, per-utterance lengths through the C-ABI) ->
+    list of (f32 waveform [T_i*hop], T_i); file i uses utterance id i, so file 0 equals convert_file's result."""
+    singers = C.load_singers(cfg)
+    if singer_name not in singers:
+        raise KeyError(f"unknown singer {singer_name!r}; known: {sorted(singers)}")
+    w24, w16 = [], []
+    for p in wav_paths:
+        w = A.load_audio(p, cfg.fs, device=device)
+        if w is None:
+            raise A.AudioError(f"{p}: non-finite samples")
+        w24.append(w)
+        w16.append(A.load_whisper_audio(p, device=device))
+    sid = int(singers[singer_name])
+    wavs = SVCPipeline(engine).convert_many(w24, w16, [sid] * len(w24), fast_inference=fast_inference,
+                                            speedup=speedup, seed=seed)
+    hop = cfg.hop_length
+    return [(w.cpu().numpy(), int(w.shape[0]) // hop) for w in wavs]
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--wav", required=True)
+    ap.add_argument("--wav", required=True, nargs="+",
+                    help="one or more source files; several are converted as one ragged GPU batch")
     ap.add_argument("--singer", default="svcc_CDF1")
-    ap.add_argument("--out", default=None, help="default gen/<wav stem>_<singer>.wav (infer.py:28)")
+    ap.add_argument("--out", default=None, help="default gen/<wav stem>_<singer>.wav (infer.py:28); one file only")
     ap.add_argument("--config", default=None, help="reference-format config.json (default: the packaged one)")
     ap.add_argument("--fast", action="store_true", help="PLMS (fast_inference=True) instead of DDPM-1000")
     ap.add_argument("--speedup", type=int, default=10)
@@ -79,14 +101,21 @@ def main(argv=None):
     vocoder = args.vocoder_ckpt or getattr(cfg, "vocoder_model_path", None)
     print("Loading mapper and vocoder...", flush=True)
     engine = build_engine(cfg, args.device, mapper, vocoder, args.whisper_ckpt, args.random_weights, args.seed)
+    if args.out and len(args.wav) > 1:
+        raise SystemExit("--out names one output file: omit it when converting several files")
     t0 = time.time()
     print("Converting...", flush=True)
-    wav, T = convert_file(engine, cfg, args.wav, args.singer, args.fast, args.speedup, args.seed,
-                          device=f"cuda:{args.device}")
-    print(f"Using time: {time.time() - t0:.3f}s ({T} frames)", flush=True)
-    out = args.out or os.path.join("gen", f"{os.path.splitext(os.path.basename(args.wav))[0]}_{args.singer}.wav")
-    A.save_audio(out, wav, cfg.fs)
-    print("Saving", out, flush=True)
+    dev = f"cuda:{args.device}"
+    if len(args.wav) == 1:
+        results = [convert_file(engine, cfg, args.wav[0], args.singer, args.fast, args.speedup, args.seed, device=dev)]
+    else:
+        results = convert_files(engine, cfg, args.wav, args.singer, args.fast, args.speedup, args.seed, device=dev)
+    print(f"Using time: {time.time() - t0:.3f}s ({sum(T for _, T in results)} frames, {len(results)} file(s))",
+          flush=True)
+    for path, (wav, _) in zip(args.wav, results):
+        out = args.out or os.path.join("gen", f"{os.path.splitext(os.path.basename(path))[0]}_{args.singer}.wav")
+        A.save_audio(out, wav, cfg.fs)
+        print("Saving", out, flush=True)
     engine.close()
     return 0
 
