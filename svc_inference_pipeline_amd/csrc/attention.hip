@@ -13,6 +13,8 @@
 // Softmax VALU work: the key mask only on the last tile, exp2 arguments as one FMA, the row max as a v_max3_f32 tree,
 // and the O rescale skipped when no lane of the wave raised its running max (alpha is then exactly 1, so the result is
 // unchanged). The kernel is VALU-issue bound (PMC: ~9.6 VALU instructions per MFMA, 0.30 MFMA busy).
+#include <type_traits>
+
 #include "common.h"
 
 namespace svc {
@@ -45,11 +47,9 @@ __device__ __forceinline__ float sum_xor32(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// max of three as nested fmaxf with single-use inner results, which the backend folds into one v_max3_f32 (inline asm
+// here would hide MFMA-result read hazards from the compiler's hazard recognizer)
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef float float2v __attribute__((ext_vector_type(2)));
@@ -126,7 +126,10 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
   gload(0);
   lstore(0);
   __syncthreads();
-  for (int kt = 0; kt < ntiles; ++kt) {
+  // one 64-key tile; TAIL (the last tile only, peeled out of the loop) masks the keys past L, so the key compares are
+  // not computed (and hoisted) on every tile
+  auto key_tile = [&](int kt, auto tail_c) {
+    constexpr bool TAIL = decltype(tail_c)::value;
     const int k0 = kt * ATT_KT;
     const f16* Ks = Ksb[kt & 1];
     const f16* Vs = Vsb[kt & 1];
@@ -146,11 +149,11 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
       }
     }
     // ---- online softmax per query column
-    const bool tail = k0 + ATT_KT > L;  // keys past L only in the last tile (wave-uniform)
+    const bool tail = TAIL && k0 + ATT_KT > L;  // keys past L only in the last tile (wave-uniform)
     half8 pb[2][2];  // P^T as B operand: [f][ks'] element j <-> key 32ks' + 4g + (j&3) + 16(j>>2)
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
-      if (tail) {
+      if (TAIL && tail) {
 #pragma unroll
         for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
@@ -160,8 +163,8 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
       // the lane's 16 scores of this query column: a v_max3_f32 tree (8 instructions instead of 16 v_max_f32)
       float m4[4];
 #pragma unroll
-      for (int kf = 0; kf < 4; ++kf) m4[kf] = max3f(max3f(s[kf][f][0], s[kf][f][1], s[kf][f][2]), s[kf][f][3], -INFINITY);
-      float mx = max3f(max3f(m4[0], m4[1], m4[2]), m4[3], -INFINITY);
+      for (int kf = 0; kf < 4; ++kf) m4[kf] = fmaxf(max3f(s[kf][f][0], s[kf][f][1], s[kf][f][2]), s[kf][f][3]);
+      float mx = fmaxf(max3f(m4[0], m4[1], m4[2]), m4[3]);
       mx = max_xor32(max_xor16(mx));
       const float mnew = fmaxf(mrun[f], mx);
       const float msc = mnew * LOG2E;
@@ -209,7 +212,9 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
     }
     if (kt + 1 < ntiles) lstore((kt + 1) & 1);  // that buffer was last read in iteration kt - 1, before its barrier
     __syncthreads();
-  }
+  };
+  for (int kt = 0; kt + 1 < ntiles; ++kt) key_tile(kt, std::false_type{});
+  key_tile(ntiles - 1, std::true_type{});
 
   // ---- normalise and store: lane holds O[q = f*16 + c16][d = df*16 + 4g + r]
 #pragma unroll
