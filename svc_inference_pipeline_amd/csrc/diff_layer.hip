@@ -64,7 +64,8 @@ struct DiffLayerArgs {
   const float* bias1;          // dilated conv bias (packed order)
   const f16* cp;               // conditioner projection of this layer [rows][768] (packed order)
   f16* g;                      // gate output [rows][384] (the layer's block of the skip-sum operand)
-  const f16* W2;               // residual half of output_projection, packed [384][384]
+  const f16* W2;               // residual half of output_projection, packed [384][384] (N = K = Kpad = 384: the
+                               // caller checks its PackedGemm)
   const float* bias2;
   f16* lo;                     // split residual low half [rows][384], updated in place
   f16* hi_out;                 // next layer input hi [rows][384] (NOT a.X)

@@ -1959,7 +1959,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
       ConvGemmArgs a = gemm_args(c->dil[i], hi_cur, C, C, B, T, T, g2);
       a.tv = tv;
       a.tv_mul = 1;
-      if (diff_layer_form(a)) {
+      if (diff_layer_form(a) && c->outres[i].N == C && c->outres[i].Kpad == C && c->outres[i].K == C) {
         f16* hi_next = hi_cur == bb.y16 ? bb.y16b : bb.y16;
         prof_site("diffsvc.layer");
         if ((st = diff_layer(a, c->dil[i].bias, g.cp, g.y16, c->outres[i].W, c->outres[i].bias, bb.lo16, hi_next,
