@@ -228,6 +228,7 @@ struct Tuning {
   int diff_res32 = 0;       // DiffSVC residual stream in f32 (default: split-fp16 hi / lo halves)
   int diff_fused = 0;       // DiffSVC residual layer as one launch (diff_layer.hip; opt-in: measured slower)
   int diff_dbg = 0;         // diff_layer diagnostics (DiffLayerArgs::dbg)
+  int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_layer.hip diff_head)
   int f0_dbg = 0;           // F0 kernel diagnostics
   int dft_dbg = 0;          // DFT / mel kernel diagnostics (1 no DFT loop, 2 no filterbank phase, 3 no frame loads)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only)

@@ -114,6 +114,8 @@ bool diff_layer_form(const ConvGemmArgs& a);
 int diff_layer(const ConvGemmArgs& a, const float* bias1, const f16* cp, f16* g, const f16* W2, const float* bias2,
                f16* lo, f16* hi_out, const float* sub, const float* add, float acc_div, const f16* zpage,
                hipStream_t s, int dbg);
+int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
+              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s);
@@ -285,7 +287,8 @@ void Tuning::from_env() {
               {"SVC_AMP_FUSED", &amp_fused},       {"SVC_AMP_MAXC", &amp_maxc},         {"SVC_WHISPER_STREAMS", &whisper_streams},
               {"SVC_SAMPLER_STREAMS", &sampler_streams}, {"SVC_VOCODER_STREAMS", &vocoder_streams},
               {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg},             {"SVC_DFT_DBG", &dft_dbg},
-              {"SVC_DIFF_FUSED", &diff_fused},     {"SVC_DIFF_DBG", &diff_dbg}};
+              {"SVC_DIFF_FUSED", &diff_fused},     {"SVC_DIFF_DBG", &diff_dbg},
+              {"SVC_DIFF_HEAD", &diff_head}};
   for (auto& it : ints)
     if (const char* v = getenv(it.env)) *it.v = atoi(v);
   if (const char* v = getenv("SVC_AMP_LDS")) amp_lds_max = v[0] == 'm' ? 1 : 0;
@@ -302,7 +305,8 @@ bool Tuning::set(const char* name, double v) {
               {"amp_dbg", &amp_dbg},           {"amp_fused", &amp_fused},       {"amp_maxc", &amp_maxc},
               {"whisper_streams", &whisper_streams}, {"sampler_streams", &sampler_streams},
               {"vocoder_streams", &vocoder_streams}, {"diff_res32", &diff_res32}, {"f0_dbg", &f0_dbg},
-              {"dft_dbg", &dft_dbg},           {"diff_fused", &diff_fused},     {"diff_dbg", &diff_dbg}};
+              {"dft_dbg", &dft_dbg},           {"diff_fused", &diff_fused},     {"diff_dbg", &diff_dbg},
+              {"diff_head", &diff_head}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) {
       *it.v = (int)v;
@@ -2009,6 +2013,12 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     const int rows_sub = B * T;
     if ((st = run_gemm(sk, bb.g16, C, C, 1, NL * sk.tap_mul, rows_sub, e, s, "diffsvc.skipsum"))) return st;
   }
+  // relu(skip_projection) and output_projection in one launch: u never reaches HBM (diff_layer.hip diff_head)
+  if (tuning().diff_head && H3 == 3 && C == 384 && c->skipproj.N == C && c->skipproj.Npad >= C &&
+      c->skipproj.K == 3 * C && c->skipproj.Kpad == 3 * C && c->outproj.K == 3 * C && c->outproj.Kpad == 3 * C &&
+      c->outproj.Npad >= 128 && c->outproj.N <= 128 && c->n_mel % 4 == 0)
+    return diff_head(bb.s16, c->skipproj.W, c->skipproj.bias, C, 3 * C, c->outproj.W, c->outproj.bias, c->outproj.N,
+                     3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s);
   e = epi();
   e.act = ACT_RELU;
   e.out16 = bb.u16;

@@ -172,7 +172,7 @@ def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, tune):
 @pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700), (5, 937)])
 def test_fused_layer_bit_identical(engine, states, cfg, B, T, tune):
     """diff_layer.hip (dilated conv + gate + residual projection + split-fp16 residual update in ONE launch per layer,
-    the default) against the unfused kernels with the same K order, MFMA operand order and epilogue expressions
+    opt-in) against the unfused kernels with the same K order, MFMA operand order and epilogue expressions
     (conv_gemm4's register gate epilogue + its register residual epilogue): bit-identical eps on row counts that are not
     multiples of the 128-row tile, utterance boundaries inside tiles and per-utterance frame counts (ragged dilated-conv
     zero padding); the default unfused path (LDS-staged residual epilogue) within 1e-5, the oracle within 5e-3."""
@@ -194,6 +194,37 @@ def test_fused_layer_bit_identical(engine, states, cfg, B, T, tune):
         ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, x.cpu(), cond.cpu(), torch.full((B,), 7, dtype=torch.long),
                                  table).numpy()
     assert rel_l2(out["fused"][1].cpu().numpy(), ref) < 5e-3
+
+
+@pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700), (5, 937)])
+def test_fused_head(engine, states, cfg, B, T, tune):
+    """diff_layer.hip diff_head (relu(skip_projection) + output_projection in one launch, u kept on chip) against the
+    two unfused GEMMs: the same products, output_projection's K segments summed in another order (hi.W_hi, hi.W_lo,
+    lo.W_hi), so within 1e-6 (f32 rounding order only); the oracle within 5e-3; ragged row counts."""
+    rng = np.random.default_rng(B * 13 + T)
+    cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
+    x = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
+    out = {}
+    for name, v in (("fused", 1), ("unfused", 0)):
+        tune(engine, diff_head=v)
+        out[name] = (engine.diffsvc_eps(cond, x, 250), engine.diffsvc_eps(cond, x, 7))
+    for k in range(2):
+        assert torch.isfinite(out["fused"][k]).all()
+        assert rel_l2(out["fused"][k].cpu().numpy(), out["unfused"][k].cpu().numpy()) < 1e-6
+    table = W.step_embedding_table(1000)
+    with torch.no_grad():
+        ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, x.cpu(), cond.cpu(), torch.full((B,), 7, dtype=torch.long),
+                                 table).numpy()
+    assert rel_l2(out["fused"][1].cpu().numpy(), ref) < 5e-3
+
+
+def test_fused_head_plms(engine, golden, tune):
+    """The fused head through PLMS-4 against the reference-generated golden (same bound as test_plms_and_ddpm)."""
+    g = golden("samplers")
+    cond = dev(golden("conditioner_diffsvc")["cond"])
+    tune(engine, diff_head=1)
+    x4 = engine.diffsvc_sample(cond, fast_inference=True, speedup=250, x_T=dev(g["x_T"]))
+    assert rel_l2(x4[0].cpu().numpy().T, g["plms4"]) < 1e-3
 
 
 @pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "24"])
