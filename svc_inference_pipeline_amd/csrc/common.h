@@ -203,6 +203,17 @@ struct StageRing {
 
 int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
 
+// One PLMS update x' = x + d (A x - Bc e'), e' = (sum_k c_k e_k) / div (modules/diffsvcrepo_inference.py:91-130;
+// engine.hip svc_diffsvc_sample):
+// plms_update (elementwise.hip) or fused into the DiffSVC head's epilogue (diff_layer.hip diff_head).
+struct PlmsArgs {
+  const float* e[4]; float c[4]; int ne; float div;
+  float d, A, Bc;
+  const float* xin;  // x the update is applied to
+  float* xout; f16* x16; int ld16;
+  float* e_avg_out;  // optional: store e' (used for the first PLMS step's x_pred path)
+};
+
 // Kernel-selection switches: the measured production choices by default, other values select the earlier or
 // alternative kernel forms that the parity tests cover and the A/B benches compare (DESIGN.md records each result).
 // A context copies the defaults at creation, where an SVC_<NAME> environment variable overrides each (so a whole
@@ -229,6 +240,7 @@ struct Tuning {
   int diff_fused = 0;       // DiffSVC residual layer as one launch (diff_layer.hip; opt-in: measured slower)
   int diff_dbg = 0;         // diff_layer diagnostics (DiffLayerArgs::dbg)
   int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_layer.hip diff_head)
+  int plms_fused = 1;       // the PLMS update in diff_head's epilogue instead of its own launch
   int f0_dbg = 0;           // F0 kernel diagnostics
   int dft_dbg = 0;          // DFT / mel kernel diagnostics (1 no DFT loop, 2 no filterbank phase, 3 no frame loads)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only)

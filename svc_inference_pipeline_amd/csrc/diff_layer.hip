@@ -389,7 +389,40 @@ struct DiffHeadArgs {
   const float* bout;
   float* eps;        // [rows][ld_eps]
   int ld_eps, n_out, M;
+  int plms;          // apply pl in the epilogue (the PLMS update that follows this eps, elementwise.hip plms4_kernel)
+  PlmsArgs pl;
 };
+
+// plms4_kernel's update of 4 channels (flat index i, row r = m, column c = n) with the freshly computed eps in
+// registers: the same expressions in the same order, so x / x16 are those plms_update would write
+__device__ __forceinline__ void head_plms(const PlmsArgs& p, const float* self, float4 e0v, int64_t i, int64_t r,
+                                          int c) {
+  auto ld = [&](const float* q) { return q == self ? e0v : *reinterpret_cast<const float4*>(q + i); };
+  const float4 v0 = ld(p.e[0]);
+  float e[4] = {p.c[0] * v0.x, p.c[0] * v0.y, p.c[0] * v0.z, p.c[0] * v0.w};
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    if (p.ne > k) {
+      const float4 v = ld(p.e[k]);
+      e[0] = e[0] + p.c[k] * v.x;
+      e[1] = e[1] + p.c[k] * v.y;
+      e[2] = e[2] + p.c[k] * v.z;
+      e[3] = e[3] + p.c[k] * v.w;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) e[k] = e[k] / p.div;
+  if (p.e_avg_out) *reinterpret_cast<float4*>(p.e_avg_out + i) = make_float4(e[0], e[1], e[2], e[3]);
+  const float4 x = *reinterpret_cast<const float4*>(p.xin + i);
+  const float4 xn = make_float4(x.x + p.d * (p.A * x.x - p.Bc * e[0]), x.y + p.d * (p.A * x.y - p.Bc * e[1]),
+                                x.z + p.d * (p.A * x.z - p.Bc * e[2]), x.w + p.d * (p.A * x.w - p.Bc * e[3]));
+  *reinterpret_cast<float4*>(p.xout + i) = xn;
+  if (p.x16) {
+    union { uint2 u; f16 h[4]; } pk;
+    pk.h[0] = f16_sat(xn.x); pk.h[1] = f16_sat(xn.y); pk.h[2] = f16_sat(xn.z); pk.h[3] = f16_sat(xn.w);
+    *reinterpret_cast<uint2*>(p.x16 + r * p.ld16 + c) = pk.u;
+  }
+}
 
 __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, const f16* zpage) {
   extern __shared__ __align__(16) unsigned char sm[];
@@ -550,14 +583,18 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm * 64 + i * 16 + fr;
       if (m >= M) continue;
-      *reinterpret_cast<float4*>(p.eps + (int64_t)m * p.ld_eps + n) =
+      const float4 ev =
           make_float4(acc2[i][j][0] + bi.x, acc2[i][j][1] + bi.y, acc2[i][j][2] + bi.z, acc2[i][j][3] + bi.w);
+      const int64_t idx = (int64_t)m * p.ld_eps + n;
+      *reinterpret_cast<float4*>(p.eps + idx) = ev;
+      if (p.plms) head_plms(p.pl, p.eps, ev, idx, m, n);
     }
   }
 }
 
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
-              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s) {
+              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
+              const PlmsArgs* plms) {
   SVC_REQUIRE(Nsp == DL_C && Ksp == 3 * DL_C && Kout == 3 * DL_C && Nout >= 1 && Nout <= 128 && Nout % 4 == 0 &&
                   Npad_out >= 128 && ld_eps % 4 == 0,
               "diff_head: shape (Nsp %d Ksp %d Nout %d Kout %d)", Nsp, Ksp, Nout, Kout);
@@ -565,7 +602,18 @@ int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp
   for (const void* q : ptrs) SVC_REQUIRE(q && ((uintptr_t)q & 15) == 0, "diff_head: operand not 16-B aligned");
   const int64_t grid = cdiv64(M, DL_BM);
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "diff_head: bad grid");
-  DiffHeadArgs p{s16, Wsp, bsp, Wout, bout, eps, ld_eps, Nout, M};
+  DiffHeadArgs p{s16, Wsp, bsp, Wout, bout, eps, ld_eps, Nout, M, 0, PlmsArgs{}};
+  if (plms) {  // the update's flat index is the eps index: rows of ld_eps == Nout channels, 16-B aligned operands
+    SVC_REQUIRE(ld_eps == Nout && plms->ne >= 1 && plms->ne <= 4 && (!plms->x16 || plms->ld16 % 4 == 0),
+                "diff_head: PLMS update shape (ld_eps %d Nout %d ne %d)", ld_eps, Nout, plms->ne);
+    auto al = [](const void* q, uintptr_t a) { return ((uintptr_t)q & (a - 1)) == 0; };  // null passes
+    bool ok = plms->xin && plms->xout && al(plms->xin, 16) && al(plms->xout, 16) && al(plms->x16, 8) &&
+              al(plms->e_avg_out, 16);
+    for (int k = 0; k < plms->ne; ++k) ok = ok && plms->e[k] && al(plms->e[k], 16);
+    SVC_REQUIRE(ok, "diff_head: PLMS operand missing or misaligned");
+    p.plms = 1;
+    p.pl = *plms;
+  }
   static bool attr = false;
   if (!attr) {
     SVC_HIP_CHECK(hipFuncSetAttribute((const void*)diff_head_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

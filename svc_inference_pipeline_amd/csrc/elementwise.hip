@@ -336,13 +336,6 @@ int bucketize(const double* f0, const float* en, const float* mbins, const float
 // ============================================================================ samplers
 // x, eps, hist: f32 [rows][100]; x16: f16 copy [rows][ld16] for the next mel_preprocess GEMM.
 // PLMS (modules/diffsvcrepo_inference.py:91-151): e' = sum_i c_i * e_i / div ; x = x + d*(A*x - Bc*e')
-struct PlmsArgs {
-  const float* e[4]; float c[4]; int ne; float div;
-  float d, A, Bc;
-  const float* xin;  // x the update is applied to
-  float* xout; f16* x16; int ld16;
-  float* e_avg_out;  // optional: store e' (used for the first PLMS step's x_pred path)
-};
 
 __global__ void plms_kernel(PlmsArgs p, int rows, int C) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

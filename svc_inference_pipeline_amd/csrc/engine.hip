@@ -83,13 +83,6 @@ int denorm_mel(const float* x, f16* y, float* y32, int ldy, int rows, int C, con
 int content_map(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst, hipStream_t s);
 int bucketize(const double* f0, const float* en, const float* mbins, const float* ebins, int nb, int* im, int* ie,
               int n, hipStream_t s);
-struct PlmsArgs {
-  const float* e[4]; float c[4]; int ne; float div;
-  float d, A, Bc;
-  const float* xin;
-  float* xout; f16* x16; int ld16;
-  float* e_avg_out;
-};
 int plms_update(const PlmsArgs& p, int rows, int C, hipStream_t s);
 struct DdpmArgs {
   float sra, srm1, c1, c2, sigma;
@@ -115,7 +108,8 @@ int diff_layer(const ConvGemmArgs& a, const float* bias1, const f16* cp, f16* g,
                f16* lo, f16* hi_out, const float* sub, const float* add, float acc_div, const f16* zpage,
                hipStream_t s, int dbg);
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
-              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s);
+              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
+              const PlmsArgs* plms);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s);
@@ -288,7 +282,8 @@ void Tuning::from_env() {
               {"SVC_SAMPLER_STREAMS", &sampler_streams}, {"SVC_VOCODER_STREAMS", &vocoder_streams},
               {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg},             {"SVC_DFT_DBG", &dft_dbg},
               {"SVC_DIFF_FUSED", &diff_fused},     {"SVC_DIFF_DBG", &diff_dbg},
-              {"SVC_DIFF_HEAD", &diff_head}};
+              {"SVC_DIFF_HEAD", &diff_head},
+              {"SVC_PLMS_FUSED", &plms_fused}};
   for (auto& it : ints)
     if (const char* v = getenv(it.env)) *it.v = atoi(v);
   if (const char* v = getenv("SVC_AMP_LDS")) amp_lds_max = v[0] == 'm' ? 1 : 0;
@@ -306,7 +301,7 @@ bool Tuning::set(const char* name, double v) {
               {"whisper_streams", &whisper_streams}, {"sampler_streams", &sampler_streams},
               {"vocoder_streams", &vocoder_streams}, {"diff_res32", &diff_res32}, {"f0_dbg", &f0_dbg},
               {"dft_dbg", &dft_dbg},           {"diff_fused", &diff_fused},     {"diff_dbg", &diff_dbg},
-              {"diff_head", &diff_head}};
+              {"diff_head", &diff_head},       {"plms_fused", &plms_fused}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) {
       *it.v = (int)v;
@@ -1925,8 +1920,10 @@ struct DenoiseBufs {
 
 
 // tv (device, optional): ragged batches, utterance b has tv[b] valid frames; only the dilated convs look across frames
+// plms (optional): the PLMS update that consumes this eps, applied in the head's epilogue when the fused head runs
+// (tuning plms_fused), else as its own launch after it
 static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s,
-                   const int* tv) {
+                   const int* tv, const PlmsArgs* plms = nullptr) {
   const int C = c->C, NL = c->n_layers, rows = B * T;
   const int ldx16 = (int)round_up(c->n_mel, 8);
   const float* dp = c->dproj + (size_t)t * NL * C;
@@ -2016,9 +2013,14 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   // relu(skip_projection) and output_projection in one launch: u never reaches HBM (diff_layer.hip diff_head)
   if (tuning().diff_head && H3 == 3 && C == 384 && c->skipproj.N == C && c->skipproj.Npad >= C &&
       c->skipproj.K == 3 * C && c->skipproj.Kpad == 3 * C && c->outproj.K == 3 * C && c->outproj.Kpad == 3 * C &&
-      c->outproj.Npad >= 128 && c->outproj.N <= 128 && c->n_mel % 4 == 0)
-    return diff_head(bb.s16, c->skipproj.W, c->skipproj.bias, C, 3 * C, c->outproj.W, c->outproj.bias, c->outproj.N,
-                     3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s);
+      c->outproj.Npad >= 128 && c->outproj.N <= 128 && c->n_mel % 4 == 0) {
+    const bool fuse = plms && tuning().plms_fused;
+    if ((st = diff_head(bb.s16, c->skipproj.W, c->skipproj.bias, C, 3 * C, c->outproj.W, c->outproj.bias,
+                        c->outproj.N, 3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s,
+                        fuse ? plms : nullptr)))
+      return st;
+    return plms && !fuse ? plms_update(*plms, rows, c->n_mel, s) : SVC_OK;
+  }
   e = epi();
   e.act = ACT_RELU;
   e.out16 = bb.u16;
@@ -2028,8 +2030,8 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e = epi();
   e.out32 = eps;
   e.ld32 = c->n_mel;
-  (void)rows;
-  return run_gemm(c->outproj, bb.u16, C * H3, C * H3, B, T, T, e, s, "diffsvc.eps_out");
+  if ((st = run_gemm(c->outproj, bb.u16, C * H3, C * H3, B, T, T, e, s, "diffsvc.eps_out"))) return st;
+  return plms ? plms_update(*plms, rows, c->n_mel, s) : SVC_OK;
 }
 
 static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
@@ -2232,7 +2234,6 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
       const int urows = u.B * T;
       const DenoiseBufs ub = sub_bufs(u);
       float* ecur = hist[head] + r * nm;
-      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr))) return st;
       PlmsArgs p{};
       p.d = d;
       p.A = A;
@@ -2242,6 +2243,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
       p.x16 = x16 + r * ld16;
       p.ld16 = ld16;
       auto H = [&](int back) { return hist[((head - back) % 5 + 5) % 5] + r * nm; };
+      // each update runs in (or right after) the denoise whose eps it consumes (denoise's plms argument)
       if (nh == 0) {
         PlmsArgs q = p;
         q.e[0] = ecur;
@@ -2250,15 +2252,16 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         q.div = 1.0f;
         q.xout = xp + r * nm;
         q.x16 = xp16 + r * ld16;
-        if ((st = plms_update(q, urows, nm, u.s))) return st;
+        if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &q))) return st;
         float* eprev = hist[(head + 1) % 5] + r * nm;
-        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s, tv ? tv + u.b0 : nullptr))) return st;
         p.e[0] = ecur;
         p.e[1] = eprev;
         p.c[0] = 1.0f;
         p.c[1] = 1.0f;
         p.ne = 2;
         p.div = 2.0f;
+        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s, tv ? tv + u.b0 : nullptr, &p))) return st;
+        continue;
       } else if (nh == 1) {
         p.e[0] = ecur;
         p.e[1] = H(1);
@@ -2287,7 +2290,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         p.ne = 4;
         p.div = 24.0f;
       }
-      if ((st = plms_update(p, urows, nm, u.s))) return st;
+      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &p))) return st;
     }
     head = (head + 1) % 5;
     nh = nh < 4 ? nh + 1 : 4;

@@ -227,6 +227,27 @@ def test_fused_head_plms(engine, golden, tune):
     assert rel_l2(x4[0].cpu().numpy().T, g["plms4"]) < 1e-3
 
 
+@pytest.mark.parametrize("B,T,speedup", [(1, None, 250), (1, None, 10), (3, 211, 25)])
+def test_plms_fused_bit_identical(engine, golden, tune, B, T, speedup):
+    """The PLMS update applied in diff_head's epilogue (tuning plms_fused, the default) against its own launch after
+    the head: the same expressions in the same order, so the sampled mel is bit-identical (first-step predictor pair,
+    AB2-AB4, sub-batches on several streams)."""
+    if T is None:
+        cond = dev(golden("conditioner_diffsvc")["cond"])
+        x_T = dev(golden("samplers")["x_T"])
+    else:
+        rng = np.random.default_rng(B * 5 + T)
+        cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
+        x_T = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
+    frames = None if T is None else [T - 41 * b for b in range(B)]
+    out = []
+    for v in (1, 0):
+        tune(engine, plms_fused=v)
+        out.append(engine.diffsvc_sample(cond, fast_inference=True, speedup=speedup, x_T=x_T, frames=frames))
+    assert torch.isfinite(out[0]).all()
+    assert torch.equal(out[0], out[1]), rel_l2(out[0].cpu().numpy(), out[1].cpu().numpy())
+
+
 @pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "24"])
 def test_eps_gemm_variants(engine, golden, variant, tune):
     """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path); 15lds:
