@@ -213,6 +213,13 @@ struct PlmsArgs {
   float* xout; f16* x16; int ld16;
   float* e_avg_out;  // optional: store e' (used for the first PLMS step's x_pred path)
 };
+// The next denoise's input projection h = relu(x16 . W + b) + dproj_0(t_next) -> split-fp16 (y16, lo16), computed in
+// the DiffSVC head from the x the fused PLMS update just produced (diff_layer.hip diff_head, tuning melpre_fused).
+struct MelNext {
+  const f16* W; const float* bias; int N, K, Kpad;  // the packed diffsvc.melpre GEMM ([Npad][Kpad])
+  const float* dp;                                  // dproj row of layer 0 at t_next [N]
+  f16* y16; f16* lo16;                              // [rows][N]
+};
 
 // Kernel-selection switches: the measured production choices by default, other values select the earlier or
 // alternative kernel forms that the parity tests cover and the A/B benches compare (DESIGN.md records each result).
@@ -240,7 +247,8 @@ struct Tuning {
   int diff_fused = 0;       // DiffSVC residual layer as one launch (diff_layer.hip; opt-in: measured slower)
   int diff_dbg = 0;         // diff_layer diagnostics (DiffLayerArgs::dbg)
   int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_layer.hip diff_head)
-  int plms_fused = 1;       // the PLMS update in diff_head's epilogue instead of its own launch
+  int plms_fused = 0;       // the PLMS update in diff_head's epilogue instead of its own launch (opt-in: slower)
+  int melpre_fused = 0;     // with it, the next denoise's input projection in diff_head too (opt-in: slower)
   int f0_dbg = 0;           // F0 kernel diagnostics
   int dft_dbg = 0;          // DFT / mel kernel diagnostics (1 no DFT loop, 2 no filterbank phase, 3 no frame loads)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only)

@@ -391,12 +391,14 @@ struct DiffHeadArgs {
   int ld_eps, n_out, M;
   int plms;          // apply pl in the epilogue (the PLMS update that follows this eps, elementwise.hip plms4_kernel)
   PlmsArgs pl;
+  int mel;           // then the next denoise's input projection from the updated x (GEMM C)
+  MelNext mn;
 };
 
 // plms4_kernel's update of 4 channels (flat index i, row r = m, column c = n) with the freshly computed eps in
 // registers: the same expressions in the same order, so x / x16 are those plms_update would write
-__device__ __forceinline__ void head_plms(const PlmsArgs& p, const float* self, float4 e0v, int64_t i, int64_t r,
-                                          int c) {
+__device__ __forceinline__ float4 head_plms(const PlmsArgs& p, const float* self, float4 e0v, int64_t i, int64_t r,
+                                            int c) {
   auto ld = [&](const float* q) { return q == self ? e0v : *reinterpret_cast<const float4*>(q + i); };
   const float4 v0 = ld(p.e[0]);
   float e[4] = {p.c[0] * v0.x, p.c[0] * v0.y, p.c[0] * v0.z, p.c[0] * v0.w};
@@ -422,6 +424,7 @@ __device__ __forceinline__ void head_plms(const PlmsArgs& p, const float* self, 
     pk.h[0] = f16_sat(xn.x); pk.h[1] = f16_sat(xn.y); pk.h[2] = f16_sat(xn.z); pk.h[3] = f16_sat(xn.w);
     *reinterpret_cast<uint2*>(p.x16 + r * p.ld16 + c) = pk.u;
   }
+  return xn;
 }
 
 __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, const f16* zpage) {
@@ -573,28 +576,95 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
         acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc2[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   }
-  // ---- eps = acc + b_out, columns < n_out
+  // ---- eps = acc + b_out, columns < n_out (+ the PLMS update; + the next input projection's A image of f16(x'))
+  constexpr int DH_XIMG = 0, DH_WMEL = 32 * 1024;  // GEMM C: x' image [128 rows][256 B], W_mel [384 rows][256 B]
+  if (p.mel) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    dl_barrier();  // every wave finished GEMM B: the u image and ring B are free
+#pragma unroll
+    for (int v = 0; v < 12; ++v) {  // W_mel, 1 KiB = 4 rows per DMA, granules swizzled at the source
+      const int row = (wave * 12 + v) * 4 + (lane >> 4);
+      dl_dma(p.mn.W + (int64_t)row * 128 + dl_swg(row, lane & 15) * 8, sm + DH_WMEL + (wave * 12 + v) * 1024);
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = wn * 32 + j * 16 + fk * 4;
-    if (n >= p.n_out) continue;
-    const float4 bi = *reinterpret_cast<const float4*>(p.bout + n);
+    const bool col = n < p.n_out;
+    const float4 bi = col ? *reinterpret_cast<const float4*>(p.bout + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + fr;
+      const int m = m0 + row;
+      float4 xn = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (col && m < M) {
+        const float4 ev =
+            make_float4(acc2[i][j][0] + bi.x, acc2[i][j][1] + bi.y, acc2[i][j][2] + bi.z, acc2[i][j][3] + bi.w);
+        const int64_t idx = (int64_t)m * p.ld_eps + n;
+        *reinterpret_cast<float4*>(p.eps + idx) = ev;
+        if (p.plms) xn = head_plms(p.pl, p.eps, ev, idx, m, n);
+      }
+      if (p.mel) {
+        DlH4 pk;
+        pk.h[0] = f16_sat(xn.x); pk.h[1] = f16_sat(xn.y); pk.h[2] = f16_sat(xn.z); pk.h[3] = f16_sat(xn.w);
+        *reinterpret_cast<uint2*>(sm + DH_XIMG + row * 256 + (dl_swg(row, n >> 3) << 4) + ((n >> 2) & 1) * 8) = pk.u;
+      }
+    }
+  }
+  if (!p.mel) return;
+  // ---- GEMM C: h = relu(x' . W_mel + b_mel) + dproj_0(t_next) as split-fp16, 4 K-steps of 32 (Kpad 128)
+  dl_vmwait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  dl_barrier();
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    half8 af[4], bf[6];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = wm * 64 + i * 16 + fr;
+      af[i] = *reinterpret_cast<const half8*>(sm + DH_XIMG + row * 256 + (dl_swg(row, ks * 4 + fk) << 4));
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int row = wn * 96 + j * 16 + fr;
+      bf[j] = *reinterpret_cast<const half8*>(sm + DH_WMEL + row * 256 + (dl_swg(row, ks * 4 + fk) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+  }
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const int n = nb + j * 16;
+    const float4 bi = *reinterpret_cast<const float4*>(p.mn.bias + n);
+    const float4 ad = *reinterpret_cast<const float4*>(p.mn.dp + n);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm * 64 + i * 16 + fr;
       if (m >= M) continue;
-      const float4 ev =
-          make_float4(acc2[i][j][0] + bi.x, acc2[i][j][1] + bi.y, acc2[i][j][2] + bi.z, acc2[i][j][3] + bi.w);
-      const int64_t idx = (int64_t)m * p.ld_eps + n;
-      *reinterpret_cast<float4*>(p.eps + idx) = ev;
-      if (p.plms) head_plms(p.pl, p.eps, ev, idx, m, n);
+      // conv_gemm3's epilogue expressions: v = relu(acc + b); w = v + add16; hi = f16_sat(w); lo = f16(w - hi)
+      const float w[4] = {fmaxf(acc[i][j][0] + bi.x, 0.f) + ad.x, fmaxf(acc[i][j][1] + bi.y, 0.f) + ad.y,
+                          fmaxf(acc[i][j][2] + bi.z, 0.f) + ad.z, fmaxf(acc[i][j][3] + bi.w, 0.f) + ad.w};
+      DlH4 hi, lo;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hi.h[r] = f16_sat(w[r]);
+        lo.h[r] = (f16)(w[r] - (float)hi.h[r]);
+      }
+      *reinterpret_cast<uint2*>(p.mn.y16 + (int64_t)m * p.mn.N + n) = hi.u;
+      *reinterpret_cast<uint2*>(p.mn.lo16 + (int64_t)m * p.mn.N + n) = lo.u;
     }
   }
 }
 
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
               int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
-              const PlmsArgs* plms) {
+              const PlmsArgs* plms, const MelNext* mel) {
   SVC_REQUIRE(Nsp == DL_C && Ksp == 3 * DL_C && Kout == 3 * DL_C && Nout >= 1 && Nout <= 128 && Nout % 4 == 0 &&
                   Npad_out >= 128 && ld_eps % 4 == 0,
               "diff_head: shape (Nsp %d Ksp %d Nout %d Kout %d)", Nsp, Ksp, Nout, Kout);
@@ -602,7 +672,7 @@ int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp
   for (const void* q : ptrs) SVC_REQUIRE(q && ((uintptr_t)q & 15) == 0, "diff_head: operand not 16-B aligned");
   const int64_t grid = cdiv64(M, DL_BM);
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "diff_head: bad grid");
-  DiffHeadArgs p{s16, Wsp, bsp, Wout, bout, eps, ld_eps, Nout, M, 0, PlmsArgs{}};
+  DiffHeadArgs p{s16, Wsp, bsp, Wout, bout, eps, ld_eps, Nout, M, 0, PlmsArgs{}, 0, MelNext{}};
   if (plms) {  // the update's flat index is the eps index: rows of ld_eps == Nout channels, 16-B aligned operands
     SVC_REQUIRE(ld_eps == Nout && plms->ne >= 1 && plms->ne <= 4 && (!plms->x16 || plms->ld16 % 4 == 0),
                 "diff_head: PLMS update shape (ld_eps %d Nout %d ne %d)", ld_eps, Nout, plms->ne);
@@ -613,6 +683,14 @@ int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp
     SVC_REQUIRE(ok, "diff_head: PLMS operand missing or misaligned");
     p.plms = 1;
     p.pl = *plms;
+  }
+  if (mel) {
+    SVC_REQUIRE(plms && mel->N == DL_C && mel->Kpad == 128 && mel->K <= 128 && Nout <= mel->K,
+                "diff_head: next input projection shape (N %d K %d Kpad %d)", mel->N, mel->K, mel->Kpad);
+    const void* mp[] = {mel->W, mel->bias, mel->dp, mel->y16, mel->lo16};
+    for (const void* q : mp) SVC_REQUIRE(q && ((uintptr_t)q & 15) == 0, "diff_head: input-projection operand");
+    p.mel = 1;
+    p.mn = *mel;
   }
   static bool attr = false;
   if (!attr) {

@@ -109,7 +109,7 @@ int diff_layer(const ConvGemmArgs& a, const float* bias1, const f16* cp, f16* g,
                hipStream_t s, int dbg);
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
               int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
-              const PlmsArgs* plms);
+              const PlmsArgs* plms, const MelNext* mel);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s);
@@ -283,7 +283,8 @@ void Tuning::from_env() {
               {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg},             {"SVC_DFT_DBG", &dft_dbg},
               {"SVC_DIFF_FUSED", &diff_fused},     {"SVC_DIFF_DBG", &diff_dbg},
               {"SVC_DIFF_HEAD", &diff_head},
-              {"SVC_PLMS_FUSED", &plms_fused}};
+              {"SVC_PLMS_FUSED", &plms_fused},
+              {"SVC_MELPRE_FUSED", &melpre_fused}};
   for (auto& it : ints)
     if (const char* v = getenv(it.env)) *it.v = atoi(v);
   if (const char* v = getenv("SVC_AMP_LDS")) amp_lds_max = v[0] == 'm' ? 1 : 0;
@@ -301,7 +302,8 @@ bool Tuning::set(const char* name, double v) {
               {"whisper_streams", &whisper_streams}, {"sampler_streams", &sampler_streams},
               {"vocoder_streams", &vocoder_streams}, {"diff_res32", &diff_res32}, {"f0_dbg", &f0_dbg},
               {"dft_dbg", &dft_dbg},           {"diff_fused", &diff_fused},     {"diff_dbg", &diff_dbg},
-              {"diff_head", &diff_head},       {"plms_fused", &plms_fused}};
+              {"diff_head", &diff_head},       {"plms_fused", &plms_fused},
+              {"melpre_fused", &melpre_fused}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) {
       *it.v = (int)v;
@@ -1921,9 +1923,12 @@ struct DenoiseBufs {
 
 // tv (device, optional): ragged batches, utterance b has tv[b] valid frames; only the dilated convs look across frames
 // plms (optional): the PLMS update that consumes this eps, applied in the head's epilogue when the fused head runs
-// (tuning plms_fused), else as its own launch after it
+// and tuning plms_fused is set (opt-in, measured slower: DESIGN.md), else as its own launch after it. t_next >= 0: the next denoise of these buffers runs at step
+// t_next on the updated x; the head then also computes that denoise's input projection (tuning melpre_fused) and sets
+// *h_next, and that call passes h_ready = true to skip its own.
 static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s,
-                   const int* tv, const PlmsArgs* plms = nullptr) {
+                   const int* tv, const PlmsArgs* plms = nullptr, int t_next = -1, bool h_ready = false,
+                   bool* h_next = nullptr) {
   const int C = c->C, NL = c->n_layers, rows = B * T;
   const int ldx16 = (int)round_up(c->n_mel, 8);
   const float* dp = c->dproj + (size_t)t * NL * C;
@@ -1943,7 +1948,9 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.out16 = bb.y16;
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
-  if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
+  if (h_next) *h_next = false;
+  if (!(h_ready && !res32))
+    if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
   // Fused layers (diff_layer.hip, default): gate GEMM, output projection and residual update in one launch per layer,
   // the hi half ping-ponging between y16 and y16b; the last layer (no residual) is the gate GEMM alone.
   const bool fused = !res32 && tuning().diff_fused && NL > 1;
@@ -2015,10 +2022,18 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
       c->skipproj.K == 3 * C && c->skipproj.Kpad == 3 * C && c->outproj.K == 3 * C && c->outproj.Kpad == 3 * C &&
       c->outproj.Npad >= 128 && c->outproj.N <= 128 && c->n_mel % 4 == 0) {
     const bool fuse = plms && tuning().plms_fused;
+    MelNext mn{};
+    const bool mel = fuse && t_next >= 0 && !res32 && tuning().melpre_fused && plms->x16 && c->melpre.N == C &&
+                     c->melpre.Kpad == 128 && c->melpre.K <= 128 && c->melpre.Npad >= C && c->n_mel <= c->melpre.K;
+    if (mel) {
+      mn = MelNext{c->melpre.W, c->melpre.bias, C, c->melpre.K, c->melpre.Kpad,
+                   c->dproj + (size_t)t_next * NL * C, bb.y16, bb.lo16};
+    }
     if ((st = diff_head(bb.s16, c->skipproj.W, c->skipproj.bias, C, 3 * C, c->outproj.W, c->outproj.bias,
                         c->outproj.N, 3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s,
-                        fuse ? plms : nullptr)))
+                        fuse ? plms : nullptr, mel ? &mn : nullptr)))
       return st;
+    if (h_next) *h_next = mel;
     return plms && !fuse ? plms_update(*plms, rows, c->n_mel, s) : SVC_OK;
   }
   e = epi();
@@ -2219,6 +2234,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
   }
   // PLMS: history ring of 4 epsilons + the first step's predictor buffers (the ring position is shared)
   int nh = 0, head = 0;  // hist slots: newest at hist[(head - 1) mod 5]
+  bool h_ready[kMaxSubStreams] = {};  // per sub-batch: the last head already computed the next denoise's input projection
   const std::vector<float>& ac = c->alphas_cumprod_f32;
   for (int i = ((c->steps - 1) / interval) * interval; i >= 0; i -= interval) {
     const int tp = i - interval > 0 ? i - interval : 0;
@@ -2228,6 +2244,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
     const float A = 1.0f / (a_t_sq * (a_t_sq + a_prev_sq));
     const float Bc = 1.0f / (a_t_sq * (sqrtf((1.0f - a_prev) * a_t) + sqrtf((1.0f - a_t) * a_prev)));
     const float d = a_prev - a_t;
+    const int t_next = i - interval >= 0 ? i - interval : -1;  // the next loop step's denoise
     for (int h = 0; h < S; ++h) {
       const Sub& u = sub[h];
       const size_t r = u.r0;
@@ -2252,7 +2269,9 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         q.div = 1.0f;
         q.xout = xp + r * nm;
         q.x16 = xp16 + r * ld16;
-        if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &q))) return st;
+        if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &q, tp, h_ready[h],
+                          &h_ready[h])))
+          return st;
         float* eprev = hist[(head + 1) % 5] + r * nm;
         p.e[0] = ecur;
         p.e[1] = eprev;
@@ -2260,7 +2279,9 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         p.c[1] = 1.0f;
         p.ne = 2;
         p.div = 2.0f;
-        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s, tv ? tv + u.b0 : nullptr, &p))) return st;
+        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s, tv ? tv + u.b0 : nullptr, &p, t_next,
+                          h_ready[h], &h_ready[h])))
+          return st;
         continue;
       } else if (nh == 1) {
         p.e[0] = ecur;
@@ -2290,7 +2311,9 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         p.ne = 4;
         p.div = 24.0f;
       }
-      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &p))) return st;
+      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &p, t_next, h_ready[h],
+                        &h_ready[h])))
+        return st;
     }
     head = (head + 1) % 5;
     nh = nh < 4 ? nh + 1 : 4;

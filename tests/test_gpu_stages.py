@@ -229,9 +229,9 @@ def test_fused_head_plms(engine, golden, tune):
 
 @pytest.mark.parametrize("B,T,speedup", [(1, None, 250), (1, None, 10), (3, 211, 25)])
 def test_plms_fused_bit_identical(engine, golden, tune, B, T, speedup):
-    """The PLMS update applied in diff_head's epilogue (tuning plms_fused, the default) against its own launch after
-    the head: the same expressions in the same order, so the sampled mel is bit-identical (first-step predictor pair,
-    AB2-AB4, sub-batches on several streams)."""
+    """The PLMS update applied in diff_head's epilogue (tuning plms_fused, opt-in), and with it the next denoise's
+    input projection (melpre_fused), against separate launches: the same expressions, K order and MFMA operand order,
+    so the sampled mel is bit-identical (first-step predictor pair, AB2-AB4, ragged sub-batches on several streams)."""
     if T is None:
         cond = dev(golden("conditioner_diffsvc")["cond"])
         x_T = dev(golden("samplers")["x_T"])
@@ -241,11 +241,12 @@ def test_plms_fused_bit_identical(engine, golden, tune, B, T, speedup):
         x_T = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
     frames = None if T is None else [T - 41 * b for b in range(B)]
     out = []
-    for v in (1, 0):
-        tune(engine, plms_fused=v)
+    for sw in (dict(plms_fused=1, melpre_fused=1), dict(plms_fused=1, melpre_fused=0), dict(plms_fused=0)):
+        tune(engine, **sw)
         out.append(engine.diffsvc_sample(cond, fast_inference=True, speedup=speedup, x_T=x_T, frames=frames))
     assert torch.isfinite(out[0]).all()
-    assert torch.equal(out[0], out[1]), rel_l2(out[0].cpu().numpy(), out[1].cpu().numpy())
+    for k in (0, 1):
+        assert torch.equal(out[k], out[2]), (k, rel_l2(out[k].cpu().numpy(), out[2].cpu().numpy()))
 
 
 @pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "24"])
