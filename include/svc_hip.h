@@ -58,8 +58,8 @@ svc_status svc_ctx_destroy(svc_ctx* ctx);
 /* numeric configuration (config.json keys): e.g. "mapper.residual_layer_num", "fs", "vocoder.n_stages".
    "tune.<name>" keys set a kernel switch of this context at any time (gemm_variant, gemm3_direct, gemm4_rmw,
    gemm4_gate, gemm_halo, act_variant, amp_mode, amp_run, amp_lds_max, amp_dbg, amp_fused, amp_maxc, whisper_streams,
-   sampler_streams, vocoder_streams, diff_res32, diff_fused, diff_dbg, diff_head, plms_fused, melpre_fused, f0_dbg, dft_dbg; "tune.reset" restores the
-   creation-time values). Defaults are
+   sampler_streams, vocoder_streams, diff_res32, diff_fused, diff_dbg, diff_head, plms_fused, melpre_fused, f0_dbg,
+   dft_dbg; "tune.reset" restores the creation-time values). Defaults are
    the measured production kernels; at creation an SVC_<NAME> environment variable overrides each. ctx may be NULL for
    "tune.*" keys: the switches of the op-level entry points (svc_op_*, svc_gemm_bench). */
 svc_status svc_ctx_set_config(svc_ctx* ctx, const char* key, double value);

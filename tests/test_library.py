@@ -62,3 +62,17 @@ def test_kernel_switches_are_per_context_config():
         _lib.tune(None, no_such_switch=1)
     with pytest.raises(_lib.SVCError, match="null context"):
         _lib.call("svc_ctx_set_config", None, b"mapper.n_mel", 100.0)
+
+
+def test_every_documented_kernel_switch_is_accepted():
+    """Every "tune.<name>" key the header documents (include/svc_hip.h, svc_ctx_set_config) is a switch the library
+    knows (op-level context, no GPU call); the context is reset afterwards."""
+    text = open(os.path.join(REPO, "include", "svc_hip.h")).read()
+    block = re.search(r"kernel switch of this context at any time \(([^;]*);", text).group(1)
+    names = [n.strip() for n in block.split(",")]
+    assert len(names) >= 20 and "diff_head" in names and "melpre_fused" in names
+    try:
+        for n in names:
+            _lib.tune(None, **{n: 0})
+    finally:
+        _lib.tune(None, reset=1)
