@@ -42,7 +42,11 @@ def main():
             ms = ctypes.c_double()
             # GEMM_BENCH_COLD=1: each launch after a 1 GiB memset (operands not cache-resident, as in the sampler)
             iters = -10 if os.environ.get("GEMM_BENCH_COLD") == "1" else 10
-            _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, iters, ctypes.byref(ms))
+            try:
+                _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, iters, ctypes.byref(ms))
+            except _lib.SVCError:  # the library rejects this (variant, epilogue) pair before launching
+                row.append(f"v{v}: {'n/a':>27s}")
+                continue
             tf = 2.0 * M * N * Cin * taps / (ms.value * 1e-3) / 1e12
             row.append(f"v{v}: {ms.value * 1000:8.1f} us {tf:7.1f} TF")
         if os.environ.get("GEMM_BENCH_TORCH", "1") == "1":
