@@ -283,10 +283,10 @@ def main():
     dom_site = max((n for n in prof_all if n.split("@")[0] == dom_name), key=lambda n: prof_all[n]["ms"])
     dom_site = dom_site.split("@")[1] if "@" in dom_site else ""
 
-    # The sampler runs utterance-aligned sub-batches on concurrent streams (kernel switch sampler_streams, default 3,
+    # The sampler runs utterance-aligned sub-batches on concurrent streams (kernel switch sampler_streams, default 2,
     # SVC_SAMPLER_STREAMS), so a launch's HIP-event duration includes time shared with the other streams' kernels. One
     # extra untimed step with the sampler on a single stream gives the dominant call site's isolated per-launch rate.
-    streams = int(os.environ.get("SVC_SAMPLER_STREAMS", "3"))
+    streams = int(os.environ.get("SVC_SAMPLER_STREAMS", "2"))
     isolated = None
     if streams > 1 and dom_site.startswith("diffsvc."):
         eng.tune(sampler_streams=1)

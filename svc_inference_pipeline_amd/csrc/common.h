@@ -241,7 +241,7 @@ struct Tuning {
   int amp_fused = 1;        // BigVGAN small-C fused activation + conv (0: activation1d + GEMM everywhere)
   int amp_maxc = 48;        // widest channel count that takes the fused kernel
   int whisper_streams = 1;  // Whisper encoder sub-batch streams
-  int sampler_streams = 3;  // DiffSVC sampler sub-batch streams
+  int sampler_streams = 2;  // DiffSVC sampler sub-batch streams
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
   int diff_res32 = 0;       // DiffSVC residual stream in f32 (default: split-fp16 hi / lo halves)
   int diff_fused = 0;       // DiffSVC residual layer as one launch (diff_layer.hip; opt-in: measured slower)

@@ -2178,8 +2178,8 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
   // Utterance-aligned sub-batches on their own streams, issued kernel by kernel in alternation: their
   // launches overlap on the GPU, so one sub-batch's epilogue / prologue phases (HBM-bound, ~40 % of a
   // denoiser GEMM launch at this size) run beside the other's MFMA phases. Utterances are independent,
-  // so results are identical to a single stream. Default 3 (measured best with the caller stream on the 4
-  // hardware queues; 2: -4 %, 4: -13 %); sampler_streams = 1 disables the split.
+  // so results are identical to a single stream. Default 2 (round-2 final code, alternating A/B on two boxes:
+  // +0.9 % over 3, 4: -15 %; profiles/r02zf_streams_ab.txt); sampler_streams = 1 disables the split.
   const int S = std::max(1, std::min(std::min(tuning().sampler_streams, B), (int)kMaxSubStreams));
   struct Sub {
     int B, b0;
