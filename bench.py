@@ -116,6 +116,19 @@ def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads, hs=None, fast=True,
                       f"{t_call * 1e3:.0f} ms timed denoiser calls (DDPM-1000 extrapolated), torch-CPU fp32, {threads} threads"}
 
 
+# algorithmic FLOPs of one 10 s clip (T = 937 mel frames) per component; the frame-proportional parts
+# scale with T, Whisper / HuBERT run on their fixed 30 s / 10 s input
+SURVEY_TF = {"whisper": 1.138, "contentvec": 0.128, "cond": 0.0007 + 0.011, "denoise_call": 0.04464, "bigvgan": 1.718}
+
+
+def survey_algorithmic_tflops(clips, T, calls, content="whisper"):
+    """§8(d)'s algorithmic work of a step (TFLOP): the reference's model FLOPs, without the split-fp16 / weight-split
+    duplicate MFMA work this build executes for precision (reported separately as executed_tflops_per_step)."""
+    r = T / 937.0
+    return clips * (SURVEY_TF[content] + r * (SURVEY_TF["cond"] + calls * SURVEY_TF["denoise_call"] +
+                                              SURVEY_TF["bigvgan"]))
+
+
 def family(prof):
     """{"kernel@site": rec} -> {kernel: summed rec}"""
     out = {}
@@ -175,7 +188,13 @@ def dry_run(args, dist):
     dist.barrier()
     t0 = time.time()
     out = None
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        if args.fault and dist.rank == args.fault_rank and i == min(1, args.steps - 1):
+            # fault injection (tests/test_parallel.py): this rank fails mid-run, by an exception or by hanging
+            # without exiting; the peers must not wait forever in the gather
+            if args.fault == "raise":
+                raise RuntimeError(f"injected fault on rank {dist.rank} at step {i}")
+            time.sleep(3600)
         out, lens = dist.gather_waveforms(wav, return_lengths=True)
     dist.barrier()
     per_rank = [r[0] for r in dist.all_gather_floats([time.time() - t0])]
@@ -197,6 +216,11 @@ def main():
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo identity conversion: exercises the rank spawn, sharding and gather only")
     ap.add_argument("--dump", default=None, help="(--dry-run) save rank 0's gathered waveforms to this .npy")
+    ap.add_argument("--fault", choices=["raise", "hang"], default=None,
+                    help="(--dry-run) rank --fault-rank raises / hangs at the second step (failure-path tests)")
+    ap.add_argument("--fault-rank", type=int, default=1)
+    ap.add_argument("--dist-timeout", type=float, default=None,
+                    help="collective timeout in seconds (default SVC_DIST_TIMEOUT_S or 600)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32, help="clips per GPU")
@@ -226,9 +250,9 @@ def main():
     if env_world is not None and int(env_world) != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
     if args.dry_run:
-        return dry_run(args, DistContext.from_env(backend="gloo"))
+        return dry_run(args, DistContext.from_env(backend="gloo", timeout_s=args.dist_timeout))
 
-    dist = DistContext.from_env()
+    dist = DistContext.from_env(timeout_s=args.dist_timeout)
     torch.cuda.set_device(dist.local_rank)
     cfg = C.load_config()
     t_setup = time.time()
@@ -283,10 +307,10 @@ def main():
     dom_site = max((n for n in prof_all if n.split("@")[0] == dom_name), key=lambda n: prof_all[n]["ms"])
     dom_site = dom_site.split("@")[1] if "@" in dom_site else ""
 
-    # The sampler runs utterance-aligned sub-batches on concurrent streams (kernel switch sampler_streams, default 2,
-    # SVC_SAMPLER_STREAMS), so a launch's HIP-event duration includes time shared with the other streams' kernels. One
+    # The sampler runs utterance-aligned sub-batches on concurrent streams (kernel switch sampler_streams, read back
+    # from the library), so a launch's HIP-event duration includes time shared with the other streams' kernels. One
     # extra untimed step with the sampler on a single stream gives the dominant call site's isolated per-launch rate.
-    streams = int(os.environ.get("SVC_SAMPLER_STREAMS", "2"))
+    streams = int(eng.get_config("tune.sampler_streams"))
     isolated = None
     if streams > 1 and dom_site.startswith("diffsvc."):
         eng.tune(sampler_streams=1)
@@ -378,8 +402,29 @@ def main():
             big = max(ents, key=lambda v: v["workgroups"])
             roof["mfma_busy_pmc"] = round(big["mfma_busy"], 3)
             roof["mfma_busy_source"] = os.path.relpath(pmc_k, REPO) + f" ({big['workgroups']}-workgroup launches)"
+    # the production sub-batch launches of the dominant call site (sampler_streams concurrent sub-batches): their
+    # rocprof per-dispatch average from the committed trace summary, when it holds that grid
+    if os.path.exists(args.pmc_json) and dom_site.startswith("diffsvc.") and streams > 1:
+        pmc = json.load(open(args.pmc_json))
+        ent = pmc.get("kernels", {}).get(dom_name)
+        T_frames = int((d24.shape[1] + 768 - 1024) // 256 + 1)
+        sub_rows = -(-B // streams) * T_frames  # the largest sub-batch
+        wg = -(-sub_rows // 128) * 6           # 128 x 128 tiles over the 768 packed gate / filter columns
+        g = ent.get("by_grid", {}).get(str(wg * 256)) if ent else None
+        if g and "rocprof_trace_avg_us" in g:
+            fl = 2.0 * sub_rows * 768 * 1152
+            tf = fl / (g["rocprof_trace_avg_us"] * 1e-6) / 1e12
+            roof["production"] = {"sub_batch_rows": sub_rows, "workgroups": wg,
+                                  "rocprof_avg_launch_us": round(g["rocprof_trace_avg_us"], 2),
+                                  "achieved": round(tf, 2), "frac": round(tf / PEAK_F16_TFLOPS, 4),
+                                  "hbm_bytes_per_launch": g.get("hbm_bytes_per_launch"),
+                                  "source": os.path.relpath(args.pmc_json, REPO) + " (" + pmc.get("source_run", "?") +
+                                  f", {wg}-workgroup launches, {streams} concurrent sampler streams)"}
     # per-kernel breakdown of the fully profiled warmup step
     total_flops = sum(v["flops"] for v in prof_all.values())
+    calls = (1000 // args.speedup + 1) if fast else 1000
+    alg_tf = survey_algorithmic_tflops(dist.world * B, int((d24.shape[1] + 768 - 1024) // 256 + 1), calls,
+                                       "whisper" if hs is None else "contentvec")
     kernels = {k: {"ms_per_step": round(v["ms"], 3), "launches_per_step": v["launches"],
                    "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 1) if v["flops"] else None,
                    "gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1) if v["bytes"] else None}
@@ -410,8 +455,13 @@ def main():
                        "global_batch": dist.world * B, "seq_len_frames": int((d24.shape[1] + 768 - 1024) // 256 + 1),
                        "parallelism": f"dp{dist.world} (per-utterance shards, RCCL gather)"},
             "roofline": roof, "cpu_baseline": cpu,
-            "algorithmic_tflops_per_step": round(total_flops / 1e12, 2),
-            "sustained_tflops": round(total_flops / 1e12 / (ms_per_step / 1000.0), 1),
+            # SURVEY.md §8(d) algorithmic work (the reference's model FLOPs) and the end-to-end fraction of the MFMA
+            # peak it sustains; executed_* counts the MFMA work actually issued (split-fp16 / weight-split duplicates)
+            "algorithmic_tflops_per_step": round(alg_tf, 2),
+            "sustained_tflops": round(alg_tf / (ms_per_step / 1000.0), 1),
+            "sustained_frac": round(alg_tf / (ms_per_step / 1000.0) / PEAK_F16_TFLOPS, 4),
+            "executed_tflops_per_step": round(total_flops * dist.world / 1e12, 2),
+            "executed_sustained_tflops": round(total_flops * dist.world / 1e12 / (ms_per_step / 1000.0), 1),
             "kernels_profiled_step": "last warmup step, every launch bracketed by HIP events (sampler sub-batches on "
                                      f"{streams} concurrent streams: their per-launch times overlap)",
             "kernels": kernels,

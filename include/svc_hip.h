@@ -33,8 +33,9 @@
  *     batch length. Each utterance is then computed exactly as a clip of its own length (its own reflect / zero /
  *     replicate padding, STFT frames, Praat frame grid, fade-out): outputs are bit-identical to converting it alone,
  *     and the rows past its end are written as zeros. Whisper needs no lengths: pad its 16 kHz input with zeros (as
- *     pad_or_trim does). The tables are staged to the device stream-ordered (a ring of 8 slots per stage group), so
- *     calls of one entry point must be ordered on one stream.
+ *     pad_or_trim does). The tables are staged to the device through a ring of 8 slots per stage group; a slot is
+ *     reused only after every kernel of the call that read it has finished (its event is re-recorded on the call's
+ *     stream after the call's last launch), so calls may use any streams.
  */
 #ifndef SVC_HIP_H
 #define SVC_HIP_H
@@ -55,14 +56,19 @@ int svc_abi_version(void);
 
 svc_status svc_ctx_create(int device, svc_ctx** out);
 svc_status svc_ctx_destroy(svc_ctx* ctx);
-/* numeric configuration (config.json keys): e.g. "mapper.residual_layer_num", "fs", "vocoder.n_stages".
-   "tune.<name>" keys set a kernel switch of this context at any time (gemm_variant, gemm3_direct, gemm4_rmw,
-   gemm4_gate, gemm_halo, act_variant, amp_mode, amp_run, amp_lds_max, amp_dbg, amp_fused, amp_maxc, whisper_streams,
-   sampler_streams, vocoder_streams, diff_res32, diff_fused, diff_dbg, diff_head, plms_fused, melpre_fused, f0_dbg,
-   dft_dbg; "tune.reset" restores the creation-time values). Defaults are
-   the measured production kernels; at creation an SVC_<NAME> environment variable overrides each. ctx may be NULL for
-   "tune.*" keys: the switches of the op-level entry points (svc_op_*, svc_gemm_bench). */
+/* numeric configuration (config.json keys, flattened: "fs", "mapper.residual_layer_num", "vocoder.upsample_rates.0",
+   ...; and the precision keys "content.split", "content.wsplit_attn" / _mlp / _qk / _v / _out, "mapper.head_split",
+   "hubert.output_layer"). An unknown key is SVC_ERR_INVALID (a misspelt key must not leave a default in place).
+   "tune.<name>" keys set a kernel switch of this context at any time (gemm_variant, gemm3_direct, whisper_streams,
+   sampler_streams, vocoder_streams, diff_head, amp_maxc; "tune.reset" restores the creation-time values). Defaults
+   are the measured production kernels; at creation an SVC_<NAME> environment variable overrides each. ctx may be
+   NULL for "tune.*" keys: the switches of the op-level entry points (svc_op_*, svc_gemm_bench). */
 svc_status svc_ctx_set_config(svc_ctx* ctx, const char* key, double value);
+/* the value of a configuration key set on this context, or of a kernel switch ("tune.<name>"; ctx NULL: the
+   op-level context's); a key that was never set is SVC_ERR_INVALID */
+svc_status svc_ctx_get_config(svc_ctx* ctx, const char* key, double* value);
+/* host-only: 1 when `key` is a configuration key svc_ctx_set_config accepts (not "tune.*"), else 0 */
+int svc_config_key_known(const char* key);
 svc_status svc_ctx_add_param(svc_ctx* ctx, const char* name, const float* host, int ndim, const int64_t* shape);
 svc_status svc_ctx_finalize(svc_ctx* ctx);
 /* bytes of device memory held by packed weights / by the workspace arena */
@@ -186,9 +192,10 @@ svc_status svc_profile_filter(const char* kernel_prefix);
 svc_status svc_profile_read(int idx, char* name, int name_len, double* total_ms, int64_t* launches, double* flops,
                             double* bytes, int* n_kernels);
 /* GEMM microbenchmark on synthetic operands: average ms per launch of one implicit-GEMM configuration
-   (variant -1 = first-generation kernel, 10-14 = conv_gemm3 tiles, 15 = the production choice, 20 / 24 =
-   conv_gemm4 with the LDS-staged / register epilogue; see run_gemm in engine.hip); epi 0 = f16 store, 1 = paired
-   gate, 2 / 6 = f32 / split-fp16 residual read-modify-write */
+   (10-14 = conv_gemm3 tiles, 15 = the production choice, 20 / 24 = conv_gemm4 with the LDS-staged / register
+   gate epilogue; see run_gemm in engine.hip); epi 0 = f16 store, 1 = paired gate, 2 / 6 = f32 / split-fp16 residual
+   read-modify-write, 3-5 = gate diagnostics (variant 24: 3 no cp read and no store, 4 no cp read, 5 no store);
+   iters < 0: |iters| launches, each after a 1 GiB memset (operands evicted from the caches) */
 svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi, int variant, int iters, double* ms_out);
 /* slaney mel filterbank (librosa.filters.mel, htk=False, norm='slaney') computed natively, host output */
 svc_status svc_mel_filterbank(int sr, int n_fft, int n_mels, double fmin, double fmax, float* out_host);

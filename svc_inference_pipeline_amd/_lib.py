@@ -16,6 +16,8 @@ PROTOTYPES = {
     "svc_ctx_create": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "svc_ctx_destroy": (c_int, [c_void_p]),
     "svc_ctx_set_config": (c_int, [c_void_p, ctypes.c_char_p, c_double]),
+    "svc_ctx_get_config": (c_int, [c_void_p, ctypes.c_char_p, ctypes.POINTER(c_double)]),
+    "svc_config_key_known": (c_int, [ctypes.c_char_p]),
     "svc_ctx_add_param": (c_int, [c_void_p, ctypes.c_char_p, c_void_p, c_int, ctypes.POINTER(c_int64)]),
     "svc_ctx_finalize": (c_int, [c_void_p]),
     "svc_ctx_memory": (c_int, [c_void_p, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64)]),
@@ -55,7 +57,8 @@ PROTOTYPES = {
     "svc_mel_filterbank": (c_int, [c_int, c_int, c_int, c_double, c_double, c_void_p]),
 }
 
-ABI_VERSION = 2  # svc_abi_version() of the library these prototypes describe (2: ragged-batch length tables)
+ABI_VERSION = 3  # svc_abi_version() of the library these prototypes describe (2: ragged-batch length tables,
+#                  3: svc_ctx_get_config, unknown configuration keys rejected)
 
 _lib = None
 
@@ -98,6 +101,13 @@ def tune(ctx=None, **switches):
     op-level entry points' context; tune(ctx, reset=1) restores the values the context was created with."""
     for k, v in switches.items():
         call("svc_ctx_set_config", ctx, f"tune.{k}".encode(), float(v))
+
+
+def get_config(ctx, key):
+    """svc_ctx_get_config: a configuration key's value, or a kernel switch's ("tune.<name>"; ctx None: op level)."""
+    v = c_double()
+    call("svc_ctx_get_config", ctx, key.encode(), ctypes.byref(v))
+    return v.value
 
 
 def profile_enable(on=True):

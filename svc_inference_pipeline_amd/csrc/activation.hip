@@ -4,9 +4,6 @@
 //   u[2q+1] = 2 * sum_{a=0..5} x[clamp(q-2+a)] * f[10-2a]
 //   s[j]    = u + 1/(exp(beta)+1e-9) * sin(u*exp(alpha))^2
 //   y[t]    = sum_{k=0..11} f[k] * s[clamp(2t+k-5, 0, 2L-1)]   (LowPassFilter1d: replicate pad (5,6), stride 2)
-// A workgroup owns 64 outputs x CG groups of 4 channels of one utterance; each thread keeps one channel
-// group (float4 loads, 8-byte fp16 stores) and walks time. x rows [t0-6, t0+70) and the 140 needed s
-// values live in LDS, so every x element is read once and every s once per 64 outputs.
 // sin uses v_sin_f32 after an explicit reduction to [-0.5, 0.5] revolutions: its error (~|u|*6e-8) is the
 // size of the f32 rounding of the argument u*alpha that the reference itself incurs.
 #include "common.h"
@@ -14,93 +11,8 @@
 
 namespace svc {
 
-constexpr int A2_TT = 64;
-
-template <int CG>
-__global__ __launch_bounds__(256) void activation1d_v2_kernel(const float* __restrict__ x, f16* __restrict__ y, int L,
-                                                              int C, int ldy, const float* __restrict__ alpha_log,
-                                                              const float* __restrict__ beta_log,
-                                                              const float* __restrict__ filt, const int* __restrict__ tv,
-                                                              int tv_mul) {
-  constexpr int NL = 256 / CG;  // time lanes
-  __shared__ float4 xs[(A2_TT + 12) * CG];
-  __shared__ float4 ss[(2 * A2_TT + 12) * CG];
-  const int tid = threadIdx.x;
-  if (tid >= NL * CG) return;  // (no barrier is skipped: idle threads leave before the first one)
-  const int g = tid % CG, tl = tid / CG;
-  const int t0 = blockIdx.x * A2_TT;
-  const int c = blockIdx.y * (4 * CG) + 4 * g;
-  const int b = blockIdx.z;
-  const bool cok = c < C;
-  const float* xb = x + (int64_t)b * L * C;
-  // ragged batches: the sequence ends at Lb (replicate padding there); rows keep the batch stride L
-  const int Lb = tv ? min(L, tv[b] * tv_mul) : L;
-  if (t0 >= Lb) return;
-  float f[12];
-#pragma unroll
-  for (int k = 0; k < 12; ++k) f[k] = filt[k];
-  float4 as = make_float4(1.f, 1.f, 1.f, 1.f), ib = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (cok) {
-    as = make_float4(expf(alpha_log[c]), expf(alpha_log[c + 1]), expf(alpha_log[c + 2]), expf(alpha_log[c + 3]));
-    ib = make_float4(1.0f / (expf(beta_log[c]) + 0.000000001f), 1.0f / (expf(beta_log[c + 1]) + 0.000000001f),
-                     1.0f / (expf(beta_log[c + 2]) + 0.000000001f), 1.0f / (expf(beta_log[c + 3]) + 0.000000001f));
-  }
-  for (int r = tl; r < A2_TT + 12; r += NL) {
-    int t = t0 - 6 + r;
-    t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
-    xs[r * CG + g] = cok ? *reinterpret_cast<const float4*>(xb + (int64_t)t * C + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  __syncthreads();
-  for (int jj = tl; jj < 2 * A2_TT + 12; jj += NL) {
-    int j = 2 * t0 - 5 + jj;
-    j = j < 0 ? 0 : (j >= 2 * Lb ? 2 * Lb - 1 : j);
-    const int qq = j >> 1;
-    const int odd = j & 1;
-    float4 u = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int a = 0; a < 6; ++a) {
-      int xt = qq - 3 + odd + a;
-      xt = xt < 0 ? 0 : (xt >= Lb ? Lb - 1 : xt);
-      const float w = f[11 - odd - 2 * a];
-      const float4 xv = xs[(xt - (t0 - 6)) * CG + g];
-      u.x += xv.x * w;
-      u.y += xv.y * w;
-      u.z += xv.z * w;
-      u.w += xv.w * w;
-    }
-    u.x *= 2.0f;
-    u.y *= 2.0f;
-    u.z *= 2.0f;
-    u.w *= 2.0f;
-    float sx = sin_rev(u.x * as.x), sy = sin_rev(u.y * as.y), sz = sin_rev(u.z * as.z), sw = sin_rev(u.w * as.w);
-    ss[jj * CG + g] = make_float4(u.x + ib.x * (sx * sx), u.y + ib.y * (sy * sy), u.z + ib.z * (sz * sz),
-                                  u.w + ib.w * (sw * sw));
-  }
-  __syncthreads();
-  if (!cok) return;
-  for (int r = tl; r < A2_TT; r += NL) {
-    const int t = t0 + r;
-    if (t >= Lb) break;
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-    for (int k = 0; k < 12; ++k) {
-      const float4 sv = ss[(2 * r + k) * CG + g];
-      acc.x += f[k] * sv.x;
-      acc.y += f[k] * sv.y;
-      acc.z += f[k] * sv.z;
-      acc.w += f[k] * sv.w;
-    }
-    union { uint2 u; f16 h[4]; } pk;
-    pk.h[0] = f16_sat(acc.x);
-    pk.h[1] = f16_sat(acc.y);
-    pk.h[2] = f16_sat(acc.z);
-    pk.h[3] = f16_sat(acc.w);
-    *reinterpret_cast<uint2*>(y + ((int64_t)b * L + t) * ldy + c) = pk.u;
-  }
-}
-
 // ---------------------------------------------------------------------------------------------------
-// Register-streaming form (default). A thread owns VEC adjacent channels of one utterance and walks a run
+// Register-streaming form. A thread owns VEC adjacent channels of one utterance and walks a run
 // of R outputs in blocks of P. It keeps sliding windows in registers: xw = x[t-5 .. t+P+4] (10 carried +
 // P loaded per block) and sw = s[2t-5 .. 2t+2P+4] (10 carried + 2P computed per block). No LDS, no
 // barriers; loads are coalesced across lanes (adjacent lanes = adjacent channel groups). Window values
@@ -233,26 +145,9 @@ int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const flo
   SVC_REQUIRE(L >= 1 && C >= 4 && C % 4 == 0 && ldy % 4 == 0, "activation1d: L=%d C=%d ldy=%d", L, C, ldy);
   SVC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "activation1d: alignment");
   const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * (4 + 2), s);
-  // tuning act_variant (A/B runs, tests): 0 = LDS-tiled kernel, 1..4 = register streaming
-  const int variant = tuning().act_variant;
-  if (variant == 1) {
-    launch_rs<4, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
-  } else if (variant == 2) {
-    launch_rs<2, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
-  } else if (variant == 3) {
-    launch_rs<4, 4, 64>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
-  } else if (variant == 4) {
-    launch_rs<1, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
-  } else if (C % 64 == 0) {
-    hipLaunchKernelGGL(activation1d_v2_kernel<16>, dim3(cdiv(L, A2_TT), C / 64, B), dim3(256), 0, s, x, y, L, C, ldy,
-                       alpha_log, beta_log, filt, tv, tv_mul);
-  } else if (C % 48 == 0) {
-    hipLaunchKernelGGL(activation1d_v2_kernel<12>, dim3(cdiv(L, A2_TT), C / 48, B), dim3(256), 0, s, x, y, L, C, ldy,
-                       alpha_log, beta_log, filt, tv, tv_mul);
-  } else {
-    hipLaunchKernelGGL(activation1d_v2_kernel<6>, dim3(cdiv(L, A2_TT), cdiv(C, 24), B), dim3(256), 0, s, x, y, L, C,
-                       ldy, alpha_log, beta_log, filt, tv, tv_mul);
-  }
+  // 2 channels per thread, 8-output blocks, 128-output runs: the fastest of the register-streaming shapes and of an
+  // LDS-tiled form measured in rounds 1-2 (4.0-4.1 TB/s; the others were removed in round 3)
+  launch_rs<2, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;

@@ -13,8 +13,6 @@ struct AmpConvArgs {
   const f16* W;       // packed weights [Npad][Kpad], K index = tap*C + ci (pack_conv1d with Cp = C)
   int Kpad;
   const float* bias;
-  int dbg;  // diagnostics (tools/amp_bench.py, SVC_AMP_DBG): 1 = skip the activation phase, 2 = skip the conv phase
-  int run_adapt = 0;  // activation runs sized for one task per thread (SVC_AMP_RUN, default on)
   const int* tv = nullptr;  // ragged batches: utterance b has min(L, tv[b] * tv_mul) rows (NULL = all L)
   int tv_mul = 1;
 };

@@ -31,23 +31,18 @@ struct AmpCfg {
   // the epilogue works in registers (operand-swapped MFMAs, see below), so LDS holds only the activation image:
   // C = 48: 34 KiB -> 4 workgroups per CU (3 with the former 48 KiB C staging), C = 24: 15 KiB
   static constexpr int LDS = A_BYTES;
-  // activation tasks: VEC channels x RUN rows per thread for MODE 0 / 1 (MODE 2 / 3 use channel pairs in 4-row blocks;
-  // the earlier VEC 2 / RUN 32 / 8-row-block form for C = 48 measured 18 % slower: 137 VGPRs + AGPRs, 3 waves)
-  static constexpr int VEC = 1;
-  static constexpr int RUN = C == 24 ? 32 : 16;  // C = 24: 24 x 10 runs = 240 tasks (611 -> 562-585 us / launch)
   static_assert(C % 8 == 0 && LDA % 8 == 0, "16-B fragment rows");
 };
 
 constexpr int AMP_NT = 256;
 
-// MODE 0: launch bounds with no occupancy target (the compiler then splits the register file into 64-119 VGPRs +
-// 32-48 AGPRs); MODE 1: a 4-waves-per-SIMD target, under which it keeps the accumulators in the unified VGPR file
-// (C = 24: 67 registers, 7 waves per SIMD instead of 5; C = 48: LDS-limited to 4 either way); MODE 2: as 1, with
-// C = 48's activation on channel pairs (packed f32 FMAs, 4-row blocks to fit the same registers); MODE 3 (default):
-// as 2 for C = 24 too (79 registers, 6 waves per SIMD). Per launch, B = 32 x 10 s (tools/amp_bench.py): C = 48
-// 7-20 % and C = 24 7-12 % faster than MODE 0; end to end +0.5 % (2 -> 0) and +0.3 % (3 -> 2)
-template <int C, int MODE>
-__global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
+// Launch bound: 4 waves per SIMD, under which the compiler keeps the accumulators in the unified VGPR file (C = 24:
+// 79 registers, 6 waves per SIMD; without an occupancy target it split the file into VGPRs + AGPRs at 5 waves).
+// The activation of C <= 48 runs on channel pairs with packed f32 FMAs (v_pk_fma_f32) in 4-row blocks, C = 96 on
+// single channels in 8-row blocks. Round 1 measured these forms 7-20 % faster per launch than the unbounded
+// single-channel form (tools/amp_bench.py); the earlier forms were removed in round 3.
+template <int C>
+__global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
   using CF = AmpCfg<C>;
   extern __shared__ __align__(16) unsigned char amp_sm[];
   f16* As = reinterpret_cast<f16*>(amp_sm);
@@ -63,20 +58,18 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
   const int rows = CF::BT + 2 * P;
 
   // ------------------------------------------------------------------ 1. SnakeBeta -> LDS (f16)
-  if (p.dbg == 1) {
-    for (int i = tid; i < rows * CF::LDA; i += AMP_NT) As[i] = (f16)0.0f;
-  } else {
-    constexpr bool PK = (MODE == 2 && C == 48) || (MODE == 3 && C <= 48);
-    constexpr int VEC = PK ? 2 : CF::VEC, BLK = PK ? 4 : 8;
+  {
+    constexpr bool PK = C <= 48;
+    constexpr int VEC = PK ? 2 : 1, BLK = PK ? 4 : 8;
     using V = ActVec<VEC>;
     float f[12];
 #pragma unroll
     for (int q = 0; q < 12; ++q) f[q] = p.filt[q];
     const int ngrp = C / VEC;
-    // run length: with p.run_adapt, the shortest multiple of BLK that gives every (channel, run) task to its own
-    // thread (one exposed load latency per thread: a run's sliding window prefetches its next block), else CF::RUN
+    // run length: the shortest multiple of BLK that gives every (channel, run) task to its own thread (one exposed
+    // load latency per thread: a run's sliding window prefetches its next block across the whole run)
     const int nr_fit = max(1, AMP_NT / ngrp);
-    const int RUN = p.run_adapt ? ((rows + nr_fit - 1) / nr_fit + BLK - 1) / BLK * BLK : CF::RUN;
+    const int RUN = ((rows + nr_fit - 1) / nr_fit + BLK - 1) / BLK * BLK;
     const int nruns = (rows + RUN - 1) / RUN;
     const float* xb = p.x + (int64_t)b * L * C;
     for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
@@ -196,7 +189,7 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
   for (int i = 0; i < MW; ++i)
 #pragma unroll
     for (int j = 0; j < CF::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-  const int ks = p.dbg == 2 ? 0 : (p.k * C + 31) / 32;
+  const int ks = (p.k * C + 31) / 32;
   const int fr = lane & 15, fk = lane >> 4;
   const f16* wrow = p.W + (int64_t)fr * p.Kpad + fk * 8;
   half8 bn[CF::FN];  // weight fragments of the next k-step, loaded one step ahead (L2 latency off the MFMA path)
@@ -261,12 +254,12 @@ __global__ __launch_bounds__(AMP_NT, MODE == 0 ? 1 : 4) void amp_conv_kernel(Amp
   }
 }
 
-template <int C, int MODE>
-static int launch_amp_mode(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
+template <int C>
+static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   using CF = AmpCfg<C>;
   static bool attr = false;
   if (!attr) {
-    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)amp_conv_kernel<C, MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)amp_conv_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                       CF::LDS));
     attr = true;
   }
@@ -278,22 +271,13 @@ static int launch_amp_mode(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s
   const char* tag = C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>");
   const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
   // the activation image needs BT + 2P rows, not BT + 2 MAXP: sized per launch, C = 48 fits 5 workgroups per CU
-  // (instead of 4) for every conv with P <= 15 (tuning amp_lds_max keeps the worst-case size, A/B runs)
+  // (instead of 4) for every conv with P <= 15
   const int P = (p.k - 1) / 2 * p.d;
-  const int lds = tuning().amp_lds_max ? CF::LDS : (CF::BT + 2 * P) * CF::LDA * 2;
-  hipLaunchKernelGGL((amp_conv_kernel<C, MODE>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, p, e);
+  const int lds = (CF::BT + 2 * P) * CF::LDA * 2;
+  hipLaunchKernelGGL((amp_conv_kernel<C>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, p, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
-}
-
-template <int C>
-static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
-  const int mode = tuning().amp_mode;  // A/B runs of the register / packed-activation forms
-  if (mode == 0) return launch_amp_mode<C, 0>(p, e, s);
-  if (mode == 1) return launch_amp_mode<C, 1>(p, e, s);
-  if (mode == 2) return launch_amp_mode<C, 2>(p, e, s);
-  return launch_amp_mode<C, 3>(p, e, s);
 }
 
 bool amp_conv_supported(int C, int k, int d) {
@@ -308,18 +292,6 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
                   (!e.acc32 || e.ld_acc == C) && !e.add16 && e.act == ACT_NONE && e.kind == EPI_GENERIC,
               "amp_conv: epilogue must be contiguous rows of C channels (bias / add_row / acc32 / out32 / out16)");
   SVC_REQUIRE(((uintptr_t)p.x & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "amp_conv: alignment");
-  if (tuning().amp_run && !p.run_adapt) {  // amp_run 0: the fixed run length (A/B runs)
-    AmpConvArgs q = p;
-    q.run_adapt = 1;
-    return amp_conv(q, C, e, s);
-  }
-  if (tuning().amp_dbg && !p.dbg) {
-    AmpConvArgs q = p;
-    q.dbg = tuning().amp_dbg;
-    if (C == 24) return launch_amp<24>(q, e, s);
-    if (C == 48) return launch_amp<48>(q, e, s);
-    return launch_amp<96>(q, e, s);
-  }
   if (C == 24) return launch_amp<24>(p, e, s);
   if (C == 48) return launch_amp<48>(p, e, s);
   return launch_amp<96>(p, e, s);

@@ -11,8 +11,8 @@
 // A operand is read with gfx950's transposing ds_read_b64_tr_b16 (a 16-lane group reads 4 keys x 16 head columns and
 // each lane receives its column), from an image whose 16-B chunks are XOR-swizzled so those reads are conflict-free.
 // Softmax VALU work: the key mask only on the last tile, exp2 arguments as one FMA, the row max as a v_max3_f32 tree,
-// and the O rescale skipped when no lane of the wave raised its running max (alpha is then exactly 1, so the result is
-// unchanged). The kernel is VALU-issue bound (PMC: ~9.6 VALU instructions per MFMA, 0.30 MFMA busy).
+// and the O rescale skipped when no lane of the wave raised its running max (alpha is then exactly 1 by
+// construction, so the result is unchanged). The kernel is VALU-issue bound (PMC: ~9.6 VALU instructions per MFMA, 0.30 MFMA busy).
 #include <type_traits>
 
 #include "common.h"
@@ -168,8 +168,10 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
       mx = max_xor32(max_xor16(mx));
       const float mnew = fmaxf(mrun[f], mx);
       const float msc = mnew * LOG2E;
-      const float alpha = __builtin_amdgcn_exp2f(fmaf(mrun[f], LOG2E, -msc));  // v_exp_f32 (arguments <= 0)
       const bool grew = mnew != mrun[f];
+      // v_exp_f32 (arguments <= 0); exactly 1 where the max did not grow (exp2 of msc's rounding error otherwise is
+      // not), so the skipped O rescale below and the row sum's factor agree
+      const float alpha = grew ? __builtin_amdgcn_exp2f(fmaf(mrun[f], LOG2E, -msc)) : 1.0f;
       mrun[f] = mnew;
       // exponent arguments, row sum and f16 conversion on packed f32 pairs (v_pk_fma_f32, v_pk_add_f32,
       // v_cvt_pk_f16_f32): half the VALU issue slots of the scalar forms; only v_exp_f32 stays per element

@@ -112,7 +112,6 @@ struct ConvGemmArgs {
   int B, T_out;
   int N;         // valid (packed) output columns
   int ntiles_n;
-  int halo;      // conv_gemm3 tap-reuse mode: max |tap shift| (0 = off); set by conv_gemm3 itself
   // ragged batches: utterance b has min(T_in, tv[b] * tv_mul) valid input rows (NULL = all T_in); rows past it read
   // as zero, exactly the Conv1d zero padding of a clip of that length (its own rows keep the batch stride T_in)
   const int* tv;
@@ -163,8 +162,10 @@ struct EpiArgs {
 };
 
 // Per-call host tables (ragged-batch lengths) staged to the device, stream-ordered: a ring of pinned host + device
-// slots, so a table is never rewritten while an earlier copy (or a kernel reading an earlier table) may still be in
-// flight. Each slot's event marks its last copy; a slot is reused only after that copy, kRing calls ago, finished.
+// slots, so a table is never rewritten while an earlier copy, or a kernel reading an earlier table, may still be in
+// flight. put() records the slot's event after the copy; the entry point that consumed the table re-records it with
+// retire() on its stream after its last launch (RingRetire below), so a slot is reused only after every kernel of
+// the call that read it has finished, whichever stream the next call of another entry point runs on.
 struct StageRing {
   static constexpr int kRing = 8;
   void* h[kRing] = {};
@@ -172,6 +173,7 @@ struct StageRing {
   size_t cap[kRing] = {};
   hipEvent_t ev[kRing] = {};
   int next = 0;
+  int last = -1;  // slot handed out by the latest put(), until retire()
   // copies `bytes` from `src` to device memory owned by the ring; *dev receives it
   int put(const void* src, size_t bytes, hipStream_t s, void** dev) {
     const int k = next;
@@ -189,8 +191,14 @@ struct StageRing {
     memcpy(h[k], src, bytes);
     SVC_HIP_CHECK(hipMemcpyAsync(d[k], h[k], bytes, hipMemcpyHostToDevice, s));
     SVC_HIP_CHECK(hipEventRecord(ev[k], s));
+    last = k;
     *dev = d[k];
     return SVC_OK;
+  }
+  // the latest table's readers are all enqueued on s (sub-streams joined back): its slot waits for them
+  void retire(hipStream_t s) {
+    if (last >= 0) (void)hipEventRecord(ev[last], s);
+    last = -1;
   }
   void release() {
     for (int k = 0; k < kRing; ++k) {
@@ -200,12 +208,17 @@ struct StageRing {
     }
   }
 };
-
-int conv_gemm(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
+// scope guard of an entry point that stages a table: retires it on the entry point's stream when the call returns
+// (after its last launch, on every return path)
+struct RingRetire {
+  StageRing& r;
+  hipStream_t s;
+  RingRetire(StageRing& ring, hipStream_t stream) : r(ring), s(stream) { r.last = -1; }
+  ~RingRetire() { r.retire(s); }
+};
 
 // One PLMS update x' = x + d (A x - Bc e'), e' = (sum_k c_k e_k) / div (modules/diffsvcrepo_inference.py:91-130;
-// engine.hip svc_diffsvc_sample):
-// plms_update (elementwise.hip) or fused into the DiffSVC head's epilogue (diff_layer.hip diff_head).
+// engine.hip svc_diffsvc_sample, elementwise.hip plms_update).
 struct PlmsArgs {
   const float* e[4]; float c[4]; int ne; float div;
   float d, A, Bc;
@@ -213,14 +226,6 @@ struct PlmsArgs {
   float* xout; f16* x16; int ld16;
   float* e_avg_out;  // optional: store e' (used for the first PLMS step's x_pred path)
 };
-// The next denoise's input projection h = relu(x16 . W + b) + dproj_0(t_next) -> split-fp16 (y16, lo16), computed in
-// the DiffSVC head from the x the fused PLMS update just produced (diff_layer.hip diff_head, tuning melpre_fused).
-struct MelNext {
-  const f16* W; const float* bias; int N, K, Kpad;  // the packed diffsvc.melpre GEMM ([Npad][Kpad])
-  const float* dp;                                  // dproj row of layer 0 at t_next [N]
-  f16* y16; f16* lo16;                              // [rows][N]
-};
-
 // Kernel-selection switches: the measured production choices by default, other values select the earlier or
 // alternative kernel forms that the parity tests cover and the A/B benches compare (DESIGN.md records each result).
 // A context copies the defaults at creation, where an SVC_<NAME> environment variable overrides each (so a whole
@@ -228,32 +233,19 @@ struct MelNext {
 // (ctx NULL: the op-level entry points' context). Launchers read the switches of the context whose entry point is
 // running (tuning(), set per call by TuningScope) instead of the environment.
 struct Tuning {
-  int gemm_variant = 15;    // GEMM kernel: -1 gemm.hip, 10..14 conv_gemm3 tile, 15 fitted choice, 20 / 24 conv_gemm4
+  int gemm_variant = 15;    // GEMM kernel: 15 fitted choice (conv_gemm3 tile by pick3; the DiffSVC gate GEMM on
+                            // conv_gemm4 with its register gate epilogue), 10..14 a fixed conv_gemm3 tile, 20 / 24
+                            // conv_gemm4 with the LDS-staged / register epilogue where N > 64
   int gemm3_direct = 3;     // conv_gemm3 register-epilogue forms in use (mask, gemm3.hip direct_form3)
-  int gemm4_rmw = 0;        // DiffSVC output projection on conv_gemm4's register read-modify-write epilogue
-  int gemm4_gate = 1;       // DiffSVC gate GEMM on conv_gemm4's register gate epilogue (0: LDS-staged, variant 20)
-  int gemm_halo = 0;        // conv_gemm3 tap-reuse operand image
-  int act_variant = 2;      // activation1d kernel form (0 LDS-tiled, 1..4 register streaming)
-  int amp_mode = 3;         // amp_conv form (0..3)
-  int amp_run = 1;          // amp_conv activation runs sized one task per thread (0: fixed runs)
-  int amp_lds_max = 0;      // amp_conv worst-case activation image (1) instead of per-launch sizing
-  int amp_dbg = 0;          // amp_conv diagnostics (1 no activation phase, 2 no conv phase)
-  int amp_fused = 1;        // BigVGAN small-C fused activation + conv (0: activation1d + GEMM everywhere)
-  int amp_maxc = 48;        // widest channel count that takes the fused kernel
   int whisper_streams = 1;  // Whisper encoder sub-batch streams
   int sampler_streams = 2;  // DiffSVC sampler sub-batch streams
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
-  int diff_res32 = 0;       // DiffSVC residual stream in f32 (default: split-fp16 hi / lo halves)
-  int diff_fused = 0;       // DiffSVC residual layer as one launch (diff_layer.hip; opt-in: measured slower)
-  int diff_dbg = 0;         // diff_layer diagnostics (DiffLayerArgs::dbg)
-  int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_layer.hip diff_head)
-  int plms_fused = 0;       // the PLMS update in diff_head's epilogue instead of its own launch (opt-in: slower)
-  int melpre_fused = 0;     // with it, the next denoise's input projection in diff_head too (opt-in: slower)
-  int f0_dbg = 0;           // F0 kernel diagnostics
-  int dft_dbg = 0;          // DFT / mel kernel diagnostics (1 no DFT loop, 2 no filterbank phase, 3 no frame loads)
-  std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only)
+  int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip)
+  int amp_maxc = 48;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none)
+  std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only, A/B runs)
   void from_env();
   bool set(const char* name, double v);  // false: unknown name ("reset" restores the creation-time values)
+  bool get(const char* name, double* v) const;
 };
 const Tuning& tuning();
 struct TuningScope {

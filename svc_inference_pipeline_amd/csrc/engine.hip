@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <ctype.h>
 
 #include <algorithm>
 #include <map>
@@ -102,14 +103,8 @@ int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
-bool conv_gemm4_rmw_form(const ConvGemmArgs& a, const EpiArgs& e);
-bool diff_layer_form(const ConvGemmArgs& a);
-int diff_layer(const ConvGemmArgs& a, const float* bias1, const f16* cp, f16* g, const f16* W2, const float* bias2,
-               f16* lo, f16* hi_out, const float* sub, const float* add, float acc_div, const f16* zpage,
-               hipStream_t s, int dbg);
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
-              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
-              const PlmsArgs* plms, const MelNext* mel);
+              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s);
@@ -271,45 +266,41 @@ struct VStage {
 // ---------------------------------------------------------------------------- kernel switches
 static thread_local const Tuning* t_tuning = nullptr;
 
-void Tuning::from_env() {
+// the switches by name: (tune.<name>, SVC_<NAME> environment override at context creation)
+template <typename T>
+static int* tuning_field(T& t, const char* name) {
   struct {
-    const char* env;
+    const char* name;
     int* v;
-  } ints[] = {{"SVC_GEMM_VARIANT", &gemm_variant}, {"SVC_GEMM3_DIRECT", &gemm3_direct}, {"SVC_GEMM4_RMW", &gemm4_rmw},
-              {"SVC_GEMM4_GATE", &gemm4_gate},     {"SVC_GEMM_HALO", &gemm_halo},       {"SVC_ACT_VARIANT", &act_variant},
-              {"SVC_AMP_MODE", &amp_mode},         {"SVC_AMP_RUN", &amp_run},           {"SVC_AMP_DBG", &amp_dbg},
-              {"SVC_AMP_FUSED", &amp_fused},       {"SVC_AMP_MAXC", &amp_maxc},         {"SVC_WHISPER_STREAMS", &whisper_streams},
-              {"SVC_SAMPLER_STREAMS", &sampler_streams}, {"SVC_VOCODER_STREAMS", &vocoder_streams},
-              {"SVC_DIFF_RES32", &diff_res32},     {"SVC_F0_DBG", &f0_dbg},             {"SVC_DFT_DBG", &dft_dbg},
-              {"SVC_DIFF_FUSED", &diff_fused},     {"SVC_DIFF_DBG", &diff_dbg},
-              {"SVC_DIFF_HEAD", &diff_head},
-              {"SVC_PLMS_FUSED", &plms_fused},
-              {"SVC_MELPRE_FUSED", &melpre_fused}};
+  } ints[] = {{"gemm_variant", &t.gemm_variant},       {"gemm3_direct", &t.gemm3_direct},
+              {"whisper_streams", &t.whisper_streams}, {"sampler_streams", &t.sampler_streams},
+              {"vocoder_streams", &t.vocoder_streams}, {"diff_head", &t.diff_head},
+              {"amp_maxc", &t.amp_maxc}};
   for (auto& it : ints)
-    if (const char* v = getenv(it.env)) *it.v = atoi(v);
-  if (const char* v = getenv("SVC_AMP_LDS")) amp_lds_max = v[0] == 'm' ? 1 : 0;
+    if (strcmp(it.name, name) == 0) return it.v;
+  return nullptr;
+}
+
+void Tuning::from_env() {
+  for (const char* name : {"gemm_variant", "gemm3_direct", "whisper_streams", "sampler_streams", "vocoder_streams",
+                           "diff_head", "amp_maxc"}) {
+    std::string env = "SVC_";
+    for (const char* q = name; *q; ++q) env += (char)toupper((unsigned char)*q);
+    if (const char* v = getenv(env.c_str())) *tuning_field(*this, name) = atoi(v);
+  }
   if (const char* v = getenv("SVC_SITE_VARIANT")) site_variant = v;
 }
 
 bool Tuning::set(const char* name, double v) {
-  struct {
-    const char* name;
-    int* v;
-  } ints[] = {{"gemm_variant", &gemm_variant}, {"gemm3_direct", &gemm3_direct}, {"gemm4_rmw", &gemm4_rmw},
-              {"gemm4_gate", &gemm4_gate},     {"gemm_halo", &gemm_halo},       {"act_variant", &act_variant},
-              {"amp_mode", &amp_mode},         {"amp_run", &amp_run},           {"amp_lds_max", &amp_lds_max},
-              {"amp_dbg", &amp_dbg},           {"amp_fused", &amp_fused},       {"amp_maxc", &amp_maxc},
-              {"whisper_streams", &whisper_streams}, {"sampler_streams", &sampler_streams},
-              {"vocoder_streams", &vocoder_streams}, {"diff_res32", &diff_res32}, {"f0_dbg", &f0_dbg},
-              {"dft_dbg", &dft_dbg},           {"diff_fused", &diff_fused},     {"diff_dbg", &diff_dbg},
-              {"diff_head", &diff_head},       {"plms_fused", &plms_fused},
-              {"melpre_fused", &melpre_fused}};
-  for (auto& it : ints)
-    if (strcmp(it.name, name) == 0) {
-      *it.v = (int)v;
-      return true;
-    }
-  return false;
+  int* f = tuning_field(*this, name);
+  if (f) *f = (int)v;
+  return f != nullptr;
+}
+
+bool Tuning::get(const char* name, double* v) const {
+  int* f = tuning_field(const_cast<Tuning&>(*this), name);
+  if (f) *v = *f;
+  return f != nullptr;
 }
 
 const Tuning& tuning() {
@@ -652,15 +643,10 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   a.tv = tv;
   a.tv_mul = tv_mul;
   const bool pair = e.kind == EPI_GATE;
-  // gemm_variant: -1 = v1 (gemm.hip) for plain GEMMs; 10..14 = conv_gemm3 tile,
-  // 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired epilogue, K = 1152)
-  // which runs conv_gemm4 with its register gate epilogue (24; 3-9 % faster than conv_gemm3); 20 = conv_gemm4,
-  // 24 = conv_gemm4 with its register epilogues (gate; residual read-modify-write) where the epilogue has that form.
-  // (The round-1 conv_gemm2 tiles and conv_gemm5 ring variants were measured slower and removed.)
+  // gemm_variant: 15 (default) = conv_gemm3 with the fitted tile choice, except the DiffSVC gate GEMM (paired
+  // epilogue, K = 1152) which runs conv_gemm4 with its register gate epilogue (24; 3-9 % faster than conv_gemm3);
+  // 10..14 = a fixed conv_gemm3 tile; 20 / 24 = conv_gemm4 with the LDS-staged / register gate epilogue.
   int variant = tu.gemm_variant;
-  // gemm4_rmw = 1: the output projection on conv_gemm4's register epilogue too. Alone it is 12 % faster per sampler
-  // sub-batch launch (tools/gemm_bench.py), but beside the other sampler streams the whole step measured 1.5 % slower
-  // (703 vs 713 audio-s/s, same box), so it is opt-in.
   // site_variant = "site=variant,...": per-call-site override (tile / kernel A/B runs, e.g. diffsvc.outproj=20)
   if (!tu.site_variant.empty()) {
     const char* senv = tu.site_variant.c_str();
@@ -671,19 +657,16 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
         break;
       }
   }
-  if (variant == 15 && pair) variant = tu.gemm4_gate ? 24 : 20;
-  if (variant == 15 && tu.gemm4_rmw && conv_gemm4_rmw_form(a, e)) variant = 24;
-  SVC_REQUIRE(variant == -1 || (variant >= 10 && variant <= 15) || variant == 20 || variant == 24,
-              "gemm_variant %d: -1, 10..15, 20 or 24", variant);
-  // N <= 64 (the last BigVGAN up-sampling phases, 48 / 24 channels) also takes conv_gemm3's 128 x 128 tile: 1.9 vs
-  // 3.0 ms per step on gemm.hip's 256 x 64 / 256 x 32 tiles (tools/ab_ups.sh), although 63-81 % of its N is padding
+  if (variant == 15 && pair) variant = 24;
+  SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24, "gemm_variant %d: 10..15, 20 or 24",
+              variant);
+  // N <= 64 (the last BigVGAN up-sampling phases, 48 / 24 channels) takes conv_gemm3's 128 x 128 tile: 1.9 vs
+  // 3.0 ms per step on the round-1 256 x 64 / 256 x 32 tiles (tools/ab_ups.sh), although 63-81 % of its N is padding
   if (variant == 20 || variant == 24) {
     if (pair || g.N > 64) return conv_gemm4(a, e, zero_page(), s, variant == 24);
     variant = 15;  // conv_gemm4's tiles are 128 wide in N: small-N GEMMs keep conv_gemm3
   }
-  if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, s);
-  if (pair) return conv_gemm3(a, e, zero_page(), 5, s);  // v1 has no paired epilogue
-  return conv_gemm(a, e, s);
+  return conv_gemm3(a, e, zero_page(), variant - 10, s);
 }
 
 EpiArgs epi() {
@@ -1292,7 +1275,7 @@ extern "C" {
 
 const char* svc_last_error(void) { return get_error(); }
 // 2: ragged-batch length tables (utt_samples / frames) in the stage entry points
-int svc_abi_version(void) { return 2; }
+int svc_abi_version(void) { return 3; }
 
 svc_status svc_ctx_create(int device, svc_ctx** out) {
   SVC_REQUIRE(out, "svc_ctx_create: null out");
@@ -1328,6 +1311,38 @@ svc_status svc_ctx_destroy(svc_ctx* c) {
 
 static int op_ws(svc_ctx** tmp);
 
+// the configuration keys the context reads (config.json's, flattened as SVCEngine._set_config writes them, and the
+// precision keys): a misspelt or obsolete key fails instead of silently leaving its default in place
+static bool known_config_key(const char* key) {
+  static const char* exact[] = {
+      "fs", "n_fft", "hop_length", "win_length", "n_mels", "fmin", "fmax", "f0_min", "f0_max",
+      "mapper.residual_channels", "mapper.residual_layer_num", "mapper.n_mel", "mapper.diffusion_fc_size",
+      "mapper.dilation_cycle_length", "mapper.residual_kernel_size", "mapper.noise_schedule_factors.0",
+      "mapper.noise_schedule_factors.1", "mapper.head_split", "content.split", "content.wsplit_attn",
+      "content.wsplit_mlp", "content.wsplit_qk", "content.wsplit_v", "content.wsplit_out", "hubert.output_layer",
+      "vocoder.n_stages", "vocoder.n_kernels", "vocoder.upsample_initial_channel", "vocoder.input_dim",
+      "vocoder.resblock", "vocoder.snake", "vocoder.snake_logscale"};
+  for (const char* k : exact)
+    if (strcmp(key, k) == 0) return true;
+  // indexed lists: <prefix><i> or, for the dilations, <prefix><j>.n / <prefix><j>.<l>
+  static const char* indexed[] = {"vocoder.upsample_rates.", "vocoder.upsample_kernel_sizes.",
+                                  "vocoder.resblock_kernel_sizes.", "vocoder.resblock_dilation_sizes."};
+  for (int i = 0; i < 4; ++i) {
+    const size_t n = strlen(indexed[i]);
+    if (strncmp(key, indexed[i], n) != 0) continue;
+    const char* p = key + n;
+    if (!isdigit((unsigned char)*p)) return false;
+    while (isdigit((unsigned char)*p)) ++p;
+    if (i < 3) return *p == 0;
+    if (*p++ != '.') return false;
+    if (strcmp(p, "n") == 0) return true;
+    if (!isdigit((unsigned char)*p)) return false;
+    while (isdigit((unsigned char)*p)) ++p;
+    return *p == 0;
+  }
+  return false;
+}
+
 svc_status svc_ctx_set_config(svc_ctx* c, const char* key, double value) {
   SVC_REQUIRE(key, "set_config: null key");
   if (strncmp(key, "tune.", 5) == 0) {  // kernel switches (Tuning); NULL context: the op-level entry points'
@@ -1340,7 +1355,24 @@ svc_status svc_ctx_set_config(svc_ctx* c, const char* key, double value) {
     return SVC_OK;
   }
   SVC_REQUIRE(c, "set_config: null context");
+  SVC_REQUIRE(known_config_key(key), "set_config: unknown configuration key %s", key);
   c->cfg[key] = value;
+  return SVC_OK;
+}
+
+int svc_config_key_known(const char* key) { return key && known_config_key(key) ? 1 : 0; }
+
+svc_status svc_ctx_get_config(svc_ctx* c, const char* key, double* value) {
+  SVC_REQUIRE(key && value, "get_config: null argument");
+  if (strncmp(key, "tune.", 5) == 0) {
+    if (!c) op_ws(&c);
+    SVC_REQUIRE(c->tune.get(key + 5, value), "get_config: unknown kernel switch %s", key);
+    return SVC_OK;
+  }
+  SVC_REQUIRE(c, "get_config: null context");
+  auto it = c->cfg.find(key);
+  SVC_REQUIRE(it != c->cfg.end(), "get_config: %s is not set", key);
+  *value = it->second;
   return SVC_OK;
 }
 
@@ -1523,6 +1555,7 @@ svc_status svc_mel_energy(svc_ctx* c, const float* wav, int B, int64_t n, const 
   const int64_t* nb_dev;
   const int* Tb_dev;
   std::vector<int> Tb_host;
+  RingRetire retire_(c->lens_feat, s);
   int st0 = stage_samples(c, c->lens_feat, n_samples, B, n, s, &nb_dev, &Tb_dev, &Tb_host);
   if (st0) return st0;
   int st;
@@ -1566,6 +1599,7 @@ svc_status svc_f0_ac(svc_ctx* c, const float* wav, int B, int64_t n, const int64
     Tb.resize(B);
     for (int b = 0; b < B; ++b) Tb[b] = (int)mel_frames_of(c, n_samples[b]);
   }
+  RingRetire retire_(c->lens_feat, (hipStream_t)stream);
   return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->auxws.base, c->auxws.cap,
                      (hipStream_t)stream, n_samples, n_samples ? Tb.data() : nullptr, &c->lens_feat);
 }
@@ -1906,13 +1940,11 @@ svc_status svc_condition(svc_ctx* c, const void* content16, const double* f0, co
 // ---------------------------------------------------------------------------- DiffSVC denoiser
 struct DenoiseBufs {
   f16* cp16;     // [rows][NL*2C] conditioner projections of every layer (hoisted out of the sampler loop)
-  float* h32;    // [rows][C] residual stream (f32, tuning diff_res32)
-  f16* y16;      // [rows][C] next layer input x + diffusion_projection
+  f16* y16;      // [rows][C] next layer input x + diffusion_projection (the high half of the split residual stream)
   f16* g16;      // [rows][NL*C] gate outputs of every layer (A operand of the skip GEMM)
   f16* s16;      // [rows][3C] sum(skip) / sqrt(NL) ([hi | lo | hi] split-fp16 with head_split, else [rows][C])
   f16* u16;      // [rows][3C] relu(skip_projection), same layout
-  f16* lo16;     // [rows][C] low half of the split residual stream: x + dproj = y16 + lo16 (default path)
-  f16* y16b;     // [rows][C] the fused layers' second hi buffer (diff_layer reads one and writes the other)
+  f16* lo16;     // [rows][C] low half of the split residual stream: x + dproj = y16 + lo16
   size_t cp_ls;  // elements between layers of cp16, which is LAYER-major [NL][rows_total][2C]: each layer's gate
                  // epilogue reads one contiguous block (row-major over all layers put 30 KB between its rows)
   size_t g_ls;   // elements between layers of g16, also layer-major [NL][rows_total][C]: the gate GEMM writes and the
@@ -1922,39 +1954,23 @@ struct DenoiseBufs {
 
 
 // tv (device, optional): ragged batches, utterance b has tv[b] valid frames; only the dilated convs look across frames
-// plms (optional): the PLMS update that consumes this eps, applied in the head's epilogue when the fused head runs
-// and tuning plms_fused is set (opt-in, measured slower: DESIGN.md), else as its own launch after it. t_next >= 0: the next denoise of these buffers runs at step
-// t_next on the updated x; the head then also computes that denoise's input projection (tuning melpre_fused) and sets
-// *h_next, and that call passes h_ready = true to skip its own.
+// plms (optional): the PLMS update that consumes this eps, launched right after the head
 static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int T, int t, float* eps, hipStream_t s,
-                   const int* tv, const PlmsArgs* plms = nullptr, int t_next = -1, bool h_ready = false,
-                   bool* h_next = nullptr) {
+                   const int* tv, const PlmsArgs* plms = nullptr) {
   const int C = c->C, NL = c->n_layers, rows = B * T;
   const int ldx16 = (int)round_up(c->n_mel, 8);
   const float* dp = c->dproj + (size_t)t * NL * C;
   int st;
-  // Residual stream x: by default split-fp16 storage (x + dproj_l = y16 + lo16, ~22 significand bits in 4 bytes):
-  // the layer's GEMM operand y16 is its high half, so each residual update moves 10 instead of 12 bytes per element.
-  // tuning diff_res32 = 1 keeps x in f32 (h32).
-  const bool res32 = tuning().diff_res32 == 1;
+  // Residual stream x in split-fp16 storage (x + dproj_l = y16 + lo16, ~22 significand bits in 4 bytes): the layer's
+  // GEMM operand y16 is its high half, so each residual update moves 10 instead of 12 bytes per element (an f32
+  // residual stream measured 1.1 % slower end to end at the same mel-L1, round 1; removed in round 3).
   EpiArgs e = epi();
   e.act = ACT_RELU;
-  if (res32) {
-    e.out32 = bb.h32;
-    e.ld32 = C;
-  } else {
-    e.lo16 = bb.lo16;
-  }
+  e.lo16 = bb.lo16;
   e.out16 = bb.y16;
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
-  if (h_next) *h_next = false;
-  if (!(h_ready && !res32))
-    if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
-  // Fused layers (diff_layer.hip, default): gate GEMM, output projection and residual update in one launch per layer,
-  // the hi half ping-ponging between y16 and y16b; the last layer (no residual) is the gate GEMM alone.
-  const bool fused = !res32 && tuning().diff_fused && NL > 1;
-  f16* hi_cur = bb.y16;
+  if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
   for (int i = 0; i < NL; ++i) {
     EpiArgs g = epi();
     g.kind = EPI_GATE;
@@ -1962,39 +1978,18 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     g.ld_cp = 2 * C;
     g.y16 = bb.g16 + (size_t)i * bb.g_ls;
     g.ldy16 = C;
-    if (fused && i + 1 < NL) {
-      EpiArgs g2 = g;
-      ConvGemmArgs a = gemm_args(c->dil[i], hi_cur, C, C, B, T, T, g2);
-      a.tv = tv;
-      a.tv_mul = 1;
-      if (diff_layer_form(a) && c->outres[i].N == C && c->outres[i].Kpad == C && c->outres[i].K == C) {
-        f16* hi_next = hi_cur == bb.y16 ? bb.y16b : bb.y16;
-        prof_site("diffsvc.layer");
-        if ((st = diff_layer(a, c->dil[i].bias, g.cp, g.y16, c->outres[i].W, c->outres[i].bias, bb.lo16, hi_next,
-                             dp + (size_t)i * C, dp + (size_t)(i + 1) * C, 1.41421356237309515f, zero_page(), s,
-                             tuning().diff_dbg)))
-          return st;
-        hi_cur = hi_next;
-        continue;
-      }
-    }
-    if ((st = run_gemm(c->dil[i], hi_cur, C, C, B, T, T, g, s, "diffsvc.dilated", tv, 1))) return st;
+    if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s, "diffsvc.dilated", tv, 1))) return st;
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
-    // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step)
+    // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step):
+    // x_i = (y16 + lo16) - dproj_i, and x_{i+1} + dproj_{i+1} goes back split into y16 / lo16
     EpiArgs r = epi();
     r.ld_acc = C;
     r.acc_div = 1.41421356237309515f;
-    if (res32) {
-      r.acc32 = bb.h32;
-      r.out32 = bb.h32;
-      r.ld32 = C;
-    } else {  // x_i = (y16 + lo16) - dproj_i, and x_{i+1} + dproj_{i+1} goes back split into y16 / lo16
-      r.acc16_hi = hi_cur;
-      r.acc16_lo = bb.lo16;
-      r.acc_sub = dp + (size_t)i * C;
-      r.lo16 = bb.lo16;
-    }
-    r.out16 = hi_cur;
+    r.acc16_hi = bb.y16;
+    r.acc16_lo = bb.lo16;
+    r.acc_sub = dp + (size_t)i * C;
+    r.lo16 = bb.lo16;
+    r.out16 = bb.y16;
     r.ld16 = C;
     r.add16 = dp + (size_t)(i + 1) * C;
     if ((st = run_gemm(c->outres[i], bb.g16 + (size_t)i * bb.g_ls, C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
@@ -2017,24 +2012,14 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     const int rows_sub = B * T;
     if ((st = run_gemm(sk, bb.g16, C, C, 1, NL * sk.tap_mul, rows_sub, e, s, "diffsvc.skipsum"))) return st;
   }
-  // relu(skip_projection) and output_projection in one launch: u never reaches HBM (diff_layer.hip diff_head)
+  // relu(skip_projection) and output_projection in one launch: u never reaches HBM (diff_head.hip)
   if (tuning().diff_head && H3 == 3 && C == 384 && c->skipproj.N == C && c->skipproj.Npad >= C &&
       c->skipproj.K == 3 * C && c->skipproj.Kpad == 3 * C && c->outproj.K == 3 * C && c->outproj.Kpad == 3 * C &&
       c->outproj.Npad >= 128 && c->outproj.N <= 128 && c->n_mel % 4 == 0) {
-    const bool fuse = plms && tuning().plms_fused;
-    MelNext mn{};
-    const bool mel = fuse && t_next >= 0 && !res32 && tuning().melpre_fused && plms->x16 && c->melpre.N == C &&
-                     c->melpre.Kpad == 128 && c->melpre.K <= 128 && c->melpre.Npad >= C && c->n_mel <= c->melpre.K;
-    if (mel) {
-      mn = MelNext{c->melpre.W, c->melpre.bias, C, c->melpre.K, c->melpre.Kpad,
-                   c->dproj + (size_t)t_next * NL * C, bb.y16, bb.lo16};
-    }
     if ((st = diff_head(bb.s16, c->skipproj.W, c->skipproj.bias, C, 3 * C, c->outproj.W, c->outproj.bias,
-                        c->outproj.N, 3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s,
-                        fuse ? plms : nullptr, mel ? &mn : nullptr)))
+                        c->outproj.N, 3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s)))
       return st;
-    if (h_next) *h_next = mel;
-    return plms && !fuse ? plms_update(*plms, rows, c->n_mel, s) : SVC_OK;
+    return plms ? plms_update(*plms, rows, c->n_mel, s) : SVC_OK;
   }
   e = epi();
   e.act = ACT_RELU;
@@ -2052,20 +2037,18 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
 static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   const size_t rows = (size_t)B * T, C = c->C;
   WS_GET(f16, cp16, rows * c->n_layers * 2 * C);
-  WS_GET(float, h32, rows * C);
   WS_GET(f16, y16, rows * C);
   WS_GET(f16, g16, rows * c->n_layers * C);
   WS_GET(f16, s16, rows * C * 3);  // [hi | lo | hi] when head_split
   WS_GET(f16, u16, rows * C * 3);
   WS_GET(f16, lo16, rows * C);
-  WS_GET(f16, y16b, rows * C);
-  bb = DenoiseBufs{cp16, h32, y16, g16, s16, u16, lo16, y16b, rows * 2 * C, rows * C};
+  bb = DenoiseBufs{cp16, y16, g16, s16, u16, lo16, rows * 2 * C, rows * C};
   return SVC_OK;
 }
 
 static size_t denoise_bytes(svc_ctx* c, int B, int T) {
   const size_t rows = (size_t)B * T, C = c->C;
-  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * (4 + 2 * 9) + 24 * 4096;
+  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * 2 * 8 + 24 * 4096;
 }
 
 static int project_cond(svc_ctx* c, const float* cond, int B, int T, const DenoiseBufs& bb, hipStream_t s) {
@@ -2107,6 +2090,7 @@ svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B,
   SVC_REQUIRE(t >= 0 && t < c->steps, "eps: t=%d", t);
   hipStream_t s = (hipStream_t)stream;
   const int* tv;
+  RingRetire retire_(c->lens_main, s);
   if (int st0 = stage_frames(c->lens_main, frames, B, T, s, &tv)) return st0;
   const int rows = B * T, ld16 = (int)round_up(c->n_mel, 8);
   int st;
@@ -2132,6 +2116,7 @@ svc_status svc_diffsvc_sample(svc_ctx* c, const float* cond, int B, int T, const
   CTX_READY(c);
   hipStream_t s = (hipStream_t)stream;
   const int* tv;
+  RingRetire retire_(c->lens_main, s);
   int st = stage_frames(c->lens_main, frames, B, T, s, &tv);
   if (st || (st = sample_impl(c, cond, B, T, tv, mode, interval, x_T, noise, seed, utt_ids, x0, s))) return st;
   // frames past an utterance's end hold no sample: zero them
@@ -2196,8 +2181,8 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
   auto sub_bufs = [&](const Sub& u) {
     const size_t r = u.r0;
     const int C = c->C;
-    return DenoiseBufs{bb.cp16 + r * 2 * C, bb.h32 + r * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * 3 * C,
-                       bb.u16 + r * 3 * C, bb.lo16 + r * C, bb.y16b + r * C, bb.cp_ls, bb.g_ls};
+    return DenoiseBufs{bb.cp16 + r * 2 * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * 3 * C, bb.u16 + r * 3 * C,
+                       bb.lo16 + r * C, bb.cp_ls, bb.g_ls};
   };
   SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
   for (int h = 0; h < S && S > 1; ++h) SVC_HIP_CHECK(hipStreamWaitEvent(sub[h].s, c->ev_fork, 0));
@@ -2234,7 +2219,6 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
   }
   // PLMS: history ring of 4 epsilons + the first step's predictor buffers (the ring position is shared)
   int nh = 0, head = 0;  // hist slots: newest at hist[(head - 1) mod 5]
-  bool h_ready[kMaxSubStreams] = {};  // per sub-batch: the last head already computed the next denoise's input projection
   const std::vector<float>& ac = c->alphas_cumprod_f32;
   for (int i = ((c->steps - 1) / interval) * interval; i >= 0; i -= interval) {
     const int tp = i - interval > 0 ? i - interval : 0;
@@ -2244,7 +2228,6 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
     const float A = 1.0f / (a_t_sq * (a_t_sq + a_prev_sq));
     const float Bc = 1.0f / (a_t_sq * (sqrtf((1.0f - a_prev) * a_t) + sqrtf((1.0f - a_t) * a_prev)));
     const float d = a_prev - a_t;
-    const int t_next = i - interval >= 0 ? i - interval : -1;  // the next loop step's denoise
     for (int h = 0; h < S; ++h) {
       const Sub& u = sub[h];
       const size_t r = u.r0;
@@ -2269,8 +2252,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         q.div = 1.0f;
         q.xout = xp + r * nm;
         q.x16 = xp16 + r * ld16;
-        if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &q, tp, h_ready[h],
-                          &h_ready[h])))
+        if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &q)))
           return st;
         float* eprev = hist[(head + 1) % 5] + r * nm;
         p.e[0] = ecur;
@@ -2279,8 +2261,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         p.c[1] = 1.0f;
         p.ne = 2;
         p.div = 2.0f;
-        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s, tv ? tv + u.b0 : nullptr, &p, t_next,
-                          h_ready[h], &h_ready[h])))
+        if ((st = denoise(c, ub, xp16 + r * ld16, u.B, T, tp, eprev, u.s, tv ? tv + u.b0 : nullptr, &p)))
           return st;
         continue;
       } else if (nh == 1) {
@@ -2311,8 +2292,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         p.ne = 4;
         p.div = 24.0f;
       }
-      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &p, t_next, h_ready[h],
-                        &h_ready[h])))
+      if ((st = denoise(c, ub, x16 + r * ld16, u.B, T, i, ecur, u.s, tv ? tv + u.b0 : nullptr, &p)))
         return st;
     }
     head = (head + 1) % 5;
@@ -2330,6 +2310,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
   // ragged batches: utterance b has frames[b] mel frames; at a point where the signal is `mul` times the mel rate
   // its valid length is tv[b] * mul, and every conv / activation / the fade-out ends there
   const int* tv;
+  RingRetire retire_(c->lens_main, s);
   if (int st0 = stage_frames(c->lens_main, frames, B, T, s, &tv)) return st0;
   for (int b = 0; frames && b < B; ++b)
     SVC_REQUIRE(frames[b] * c->hop_out >= c->nfade, "bigvgan: utterance %d (%d frames) shorter than the fade-out", b,
@@ -2354,8 +2335,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
   WS_GET(float, XS, big);
   WS_GET(f16, a16, big);
   WS_GET(f16, next16, big);
-  const bool use_amp = tuning().amp_fused != 0;  // 0 = unfused activation1d + GEMM everywhere (A/B runs)
-  // amp_maxc: widest channel count that takes the fused kernel. C = 96 measured 1.2 % faster end to end as
+  // amp_maxc: widest channel count that takes the fused kernel (0: activation1d + GEMM everywhere). C = 96 measured 1.2 % faster end to end as
   // activation1d + conv_gemm3 (736 vs 727 audio-s/s, same box); C = 48 unfused is 9 % slower (its N = 48 GEMMs are too
   // narrow for the MFMA tiles)
   const int amp_maxc = tuning().amp_maxc;
@@ -2432,7 +2412,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
           const int d2 = rb2 ? S.rd[j][l] : 1;
           const float* act_in = rb2 ? src : tmph;  // input of the activation before the second (or only) conv
           // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
-          const bool fuse = use_amp && ch <= amp_maxc && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
+          const bool fuse = ch <= amp_maxc && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
           if (!rb2) {
             EpiArgs e1 = epi();
             e1.out32 = tmph;
@@ -2695,6 +2675,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters != 0, "gemm_bench: bad args");
   SVC_REQUIRE(epi_kind < 3 || epi_kind == 6 || variant == 24,
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
+  SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24, "gemm_bench: variant %d", variant);
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float *bias, *R = nullptr;
@@ -2743,8 +2724,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   if (cold) SVC_HIP_CHECK(hipMalloc(&flush, flush_bytes));
   auto run = [&]() {
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
-    if (variant >= 10) return conv_gemm3(a, e, zero_page(), variant - 10, 0);
-    return conv_gemm(a, e, 0);
+    return conv_gemm3(a, e, zero_page(), variant - 10, 0);
   };
   for (int w = 0; w < 2 && !st; ++w) st = run();
   float ms = 0;

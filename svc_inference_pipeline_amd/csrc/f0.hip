@@ -25,7 +25,6 @@ constexpr int F0_SEG = 4;    // autocorrelation sample segments (partial sums pe
 
 struct F0Params {
   int nsp, hnsp, nw, hnw, maxlag, nf, bmax, maxc;
-  int dbg;  // diagnostics (SVC_F0_DBG): 1 = stop after the autocorrelation, 2 = skip the Brent refinement
   double dx, t1, x1, ts, floor_hz, ceiling, voicing, silence, octave_cost, octave_jump, vuv_cost;
 };
 
@@ -402,7 +401,6 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
   }
   if (threadIdx.x == 0) r[P.bmax] = 1.0;
   __syncthreads();
-  if (P.dbg == 1) return;
   const int rn = 2 * P.bmax + 1;
   const int iend = P.maxlag < P.bmax ? P.maxlag : P.bmax;
   // first pass, in parallel over lags: local maxima above half the voicing threshold and their sinc(30) strengths
@@ -456,7 +454,7 @@ __global__ __launch_bounds__(256) void f0_frame_kernel(const float* __restrict__
   const int k = threadIdx.x;
   // second pass: sinc(70) maximum by Brent, one WAVE per candidate (the sinc sums spread over its lanes)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int kc = 1 + wave; kc < nc && P.dbg != 2; kc += (int)(blockDim.x >> 6)) {
+  for (int kc = 1 + wave; kc < nc; kc += (int)(blockDim.x >> 6)) {
     const int ixmid = cim[kc] + P.bmax + 1;
     double xmid, ymid;
     if (ixmid <= 1) {
@@ -641,7 +639,6 @@ int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double
   }
   SVC_REQUIRE(P.nw <= 2048 && P.maxc <= F0_MAXC, "f0: window %d / candidates %d too large", P.nw, P.maxc);
   P.voicing = voicing;
-  P.dbg = tuning().f0_dbg;
   P.silence = 0.03;
   P.octave_cost = 0.01;
   P.octave_jump = 0.35;

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(FftPlan<N>::TPF * FftPlan<N>::FR) void dft_mel_kern
   double* zf = reinterpret_cast<double*>(zs + fr * N);
   for (int j = t; j < n; j += P::TPF) {
     float x = 0.f;
-    if (fr < nf && a.dbg != 3) {
+    if (fr < nf) {
       int64_t idx = (int64_t)(f0 + fr) * a.hop + j - a.pad;
       if (idx < 0) idx = -idx;
       if (idx >= n_logical) idx = 2 * (n_logical - 1) - idx;
@@ -205,7 +205,7 @@ __global__ __launch_bounds__(FftPlan<N>::TPF * FftPlan<N>::FR) void dft_mel_kern
   }
   __syncthreads();
   // 2. FFT
-  if (a.dbg != 1) P::run(zs + fr * N, tw, t);
+  P::run(zs + fr * N, tw, t);
   // 3. real-input split and magnitudes
   const double2* Z = zs + fr * N;
   for (int k = t; k <= N; k += P::TPF) {
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(FftPlan<N>::TPF * FftPlan<N>::FR) void dft_mel_kern
   }
   __syncthreads();
   const int64_t row0 = (int64_t)b * a.n_frames + f0;
-  for (int i = tid; i < (a.dbg == 2 ? 0 : nf * a.n_mels); i += NT) {
+  for (int i = tid; i < nf * a.n_mels; i += NT) {
     const int f = i / a.n_mels, m = i - f * a.n_mels;
     const int lo = a.band[3 * m], hi = a.band[3 * m + 1];
     const float* fbm = fbs + a.band[3 * m + 2] - lo;
@@ -255,7 +255,6 @@ static int launch_dft_mel(const DftArgs& a, int B, hipStream_t s) {
     attr = true;
   }
   DftArgs p = a;
-  p.dbg = tuning().dft_dbg;
   dim3 grid(cdiv(a.n_frames, P::FR), B);
   hipLaunchKernelGGL(dft_mel_kernel<N>, grid, dim3(P::TPF * P::FR), lds, s, p);
   SVC_LAUNCH_CHECK();

@@ -19,14 +19,8 @@
 //     dummy DMAs from the zero page so the counts stay uniform.
 //   * When Cp % 64 == 0 a K-tile lies inside one conv tap: the tap shift is wave-uniform and the
 //     A-operand address is a per-lane base plus a scalar offset (one compare + select per DMA).
-//   * HALO (tap reuse, multi-tap same-length convs with Cp % 64 == 0): K-tiles run channel-chunk-major,
-//     tap-minor, and the A operand of a 64-channel chunk is staged ONCE as an image of BM + 2H rows
-//     (H = max |tap shift| <= 32, padded to a multiple of 64 rows) that every tap of the chunk reads at
-//     its row offset; a fragment whose source row leaves its utterance reads zero (per-lane select).
-//     Operand bytes per tile drop from taps x (BM + BN) to (BM + 2H) + taps x BN rows per chunk — the
-//     lever on gfx950, where these short-K GEMMs run at the L2 -> LDS fill rate (~12 B/clk/CU measured)
-//     rather than the MFMA rate. Schedule: B halves as above (P0, P1); the next chunk's image is issued in
-//     P2 of the chunk's second-to-last tap and retired by the P3 wait of its last tap.
+//   (A tap-reuse form that staged a 64-channel chunk's A rows once for every tap moved ~40 % fewer operand bytes on
+//    the multi-tap convs yet ran 5-10 % slower; it was removed in round 3, DESIGN.md.)
 #include <cstdio>
 #include <cstdlib>
 #include "common.h"
@@ -34,15 +28,13 @@
 
 namespace svc {
 
-template <int BM, int BN, bool HALO = false>
+template <int BM, int BN>
 struct G3 {
   static constexpr int NT = 512;
-  static constexpr int BMH = HALO ? BM + 64 : BM;    // A image rows (halo of <= 32 rows each side)
-  static constexpr int AI = BMH / 64;                // DMA instructions per wave for one A image
   static constexpr int WTM = BM / 2, WTN = BN / 4;   // wave tile
   static constexpr int QM = WTM / 2, QN = WTN / 2;   // quadrant (one phase)
   static constexpr int FQM = QM / 16, FQN = QN / 16; // 16x16 fragments per quadrant
-  static constexpr int TILE = (BMH + BN) * 128;      // bytes of one K-tile image (A rows, then B rows)
+  static constexpr int TILE = (BM + BN) * 128;       // bytes of one K-tile image (A rows, then B rows)
   static constexpr int RING = 2 * TILE;
   static constexpr int AH = BM / 128;                // DMA instructions per wave per A half-tile
   static constexpr int BH = BN / 128;
@@ -55,8 +47,7 @@ struct G3 {
 };
 
 // 16-B chunk swizzle of the 128-B-row LDS images: conflict-free ds_read_b128 fragment reads (16 consecutive
-// rows per lane group) for EVERY starting row, which the tap-reuse mode needs (it reads the A image at
-// arbitrary tap offsets; the former kv ^ ((row >> 1) & 7) went 2-way unless the start was a multiple of 4).
+// rows per lane group) for every starting row.
 __device__ __forceinline__ int sw3(int row, int kv) { return kv ^ (row & 6); }
 
 template <int N>
@@ -78,7 +69,7 @@ __device__ __forceinline__ void g3_dma(const void* src, unsigned char* lds) {
 // every W rows: rows w*W + h*Q + [0, Q)
 __device__ __forceinline__ int half_row(int i, int h, int Q, int W) { return (i / Q) * W + h * Q + (i % Q); }
 
-// Register epilogue forms (FORM > 0, !PAIR, !HALO): the MFMAs run with A and B swapped, so a lane's accumulator holds
+// Register epilogue forms (FORM > 0, !PAIR): the MFMAs run with A and B swapped, so a lane's accumulator holds
 // 4 consecutive columns of one output row and the epilogue reads and writes HBM straight from registers (no C tile
 // through LDS, no extra barriers). Each form is the epilogue_pass arithmetic, in the same order, for one family:
 //   G3_F16  : act(acc + bias) (* col_scale for n < scale_cols) -> out16 (+ split16 lo / hi copies)
@@ -86,12 +77,11 @@ __device__ __forceinline__ int half_row(int i, int h, int Q, int W) { return (i 
 //   G3_SPLIT: acc + bias, ((acc16_hi + acc16_lo) - acc_sub + v) / acc_div -> out16 = hi(v + add16), lo16 = lo
 enum { G3_LDS = 0, G3_F16 = 1, G3_RES32 = 2, G3_SPLIT = 3 };
 
-template <int BM, int BN, bool CP64, bool PAIR, bool HALO, int FORM = G3_LDS>
+template <int BM, int BN, bool CP64, bool PAIR, int FORM = G3_LDS>
 __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage,
                                                            float inv_cp) {
-  static_assert(!HALO || CP64, "tap reuse needs whole-tap K-tiles");
-  static_assert(FORM == G3_LDS || (!PAIR && !HALO), "register epilogues: generic, per-tap schedule only");
-  using CF = G3<BM, BN, HALO>;
+  static_assert(FORM == G3_LDS || !PAIR, "register epilogues: generic epilogues only");
+  using CF = G3<BM, BN>;
   extern __shared__ __align__(16) unsigned char sm3[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -145,42 +135,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
       b_p[h][v] = a.W + (int64_t)(n0 + row) * a.Kpad + sw3(row, lane & 7) * 8;
     }
 
-  auto a_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE; };  // HALO: indexed by chunk, not K-tile
-  auto b_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE + CF::BMH * 128; };
-  // ---- HALO: taps per chunk, image DMA slots (image row R <-> flattened input row m0 - H + R), and the
-  // utterance-local time of every A-fragment row this lane reads (for the per-tap validity select)
-  const int taps = HALO ? a.K / a.Cp : 1;
-  const int H = a.halo;
-  const f16* im_p[HALO ? CF::AI : 1];
-  int im_off[HALO ? CF::AI : 1];
-  int frag_t[2][CF::FQM];
-  bool need_mask = true;  // wave-uniform: some fragment row's tap source may leave its utterance
-  if constexpr (HALO) {
-    const int b0 = m0 / a.T_out, t0 = m0 - b0 * a.T_out;
-    need_mask = m0 + BM > M || t0 < H || t0 + BM - 1 + H >= a.T_out;
-#pragma unroll
-    for (int v = 0; v < CF::AI; ++v) {
-      const int R = v * 64 + wave * 8 + (lane >> 3);
-      const int g = m0 - H + R;
-      im_off[v] = (v * 64 + wave * 8) * 128;
-      im_p[v] = (g >= 0 && g < M) ? a.X + (int64_t)g * a.ldx + sw3(R, lane & 7) * 8 : nullptr;
-    }
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int i = 0; i < CF::FQM; ++i) {
-        const int m = m0 + wm * CF::WTM + x * CF::QM + i * 16 + (lane & 15);
-        frag_t[x][i] = m < M ? m - (m / a.T_out) * a.T_out : -(1 << 29);
-      }
-  }
-  auto issue_img = [&](int c) {  // A image of channel chunk c into A buffer c & 1
-    unsigned char* dst = sm3 + (c & 1) * CF::TILE;
-    const bool live = c * taps < nk;
-#pragma unroll
-    for (int v = 0; v < CF::AI; ++v)
-      g3_dma(live && im_p[v] ? (const void*)(im_p[v] + c * 64) : (const void*)zsrc, dst + im_off[v]);
-  };
-
+  auto a_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE; };
+  auto b_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE + BM * 128; };
   auto issue_a = [&](int h, int kt) {
     unsigned char* dst = a_img(kt);
     if constexpr (CP64) {
@@ -213,10 +169,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
       }
     }
   };
-  auto issue_b = [&](int h, int kt, int c = 0, int j = 0) {
+  auto issue_b = [&](int h, int kt) {
     unsigned char* dst = b_img(kt);
-    int koff = kt * 64;
-    if constexpr (HALO) koff = j * a.Cp + c * 64;  // K-tile kt = (chunk c, tap j): weight columns tap * Cp + chunk * 64
+    const int koff = kt * 64;
 #pragma unroll
     for (int v = 0; v < CF::BH; ++v) g3_dma(kt < nk ? (const void*)(b_p[h][v] + koff) : (const void*)zsrc, dst + b_rb[h][v] * 128);
   };
@@ -235,44 +190,19 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   const int fr = lane & 15, fk = lane >> 4;
 
   // one phase: quadrant (QMI, QNI) of K-tile kt
-  // phase of K-tile kt; HALO: kt = kc * taps + kj (chunk, tap), and (nc, nj) of K-tile kt + 1 (counters, no division)
-  auto phase = [&](auto QMI_, auto QNI_, int kt, int kc, int kj, int nc, int nj) {
+  auto phase = [&](auto QMI_, auto QNI_, int kt) {
     constexpr int QMI = decltype(QMI_)::value, QNI = decltype(QNI_)::value;
     constexpr int P = QMI * 2 + QNI;
-    const unsigned char* Ab = a_img(kc);
+    const unsigned char* Ab = a_img(kt);
     const unsigned char* Bb = b_img(kt);
     // ---- L section: this quadrant's fragments (A reused between phases 0/1 and 2/3)
     if constexpr (QNI == 0) {
-      if constexpr (HALO) {
-        const int shift = kj * a.tap_mul + a.tap_add;
-        if (!need_mask) {  // tile inside one utterance, >= H rows from its ends: every source row is valid
 #pragma unroll
-          for (int i = 0; i < CF::FQM; ++i) {
-            const int row = H + wm * CF::WTM + QMI * CF::QM + i * 16 + fr + shift;
+      for (int i = 0; i < CF::FQM; ++i) {
+        const int row = wm * CF::WTM + QMI * CF::QM + i * 16 + fr;
 #pragma unroll
-            for (int s = 0; s < 2; ++s)
-              af[i][s] = *reinterpret_cast<const half8*>(Ab + row * 128 + (sw3(row, s * 4 + fk) << 4));
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < CF::FQM; ++i) {
-            const int row = H + wm * CF::WTM + QMI * CF::QM + i * 16 + fr + shift;
-            const bool ok = (unsigned)(frag_t[QMI][i] + shift) < (unsigned)a.T_in;
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const half8 v = *reinterpret_cast<const half8*>(Ab + row * 128 + (sw3(row, s * 4 + fk) << 4));
-              af[i][s] = ok ? v : half8{};
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < CF::FQM; ++i) {
-          const int row = wm * CF::WTM + QMI * CF::QM + i * 16 + fr;
-#pragma unroll
-          for (int s = 0; s < 2; ++s)
-            af[i][s] = *reinterpret_cast<const half8*>(Ab + row * 128 + (sw3(row, s * 4 + fk) << 4));
-        }
+        for (int s = 0; s < 2; ++s)
+          af[i][s] = *reinterpret_cast<const half8*>(Ab + row * 128 + (sw3(row, s * 4 + fk) << 4));
       }
     }
 #pragma unroll
@@ -283,21 +213,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
         bf[j][s] = *reinterpret_cast<const half8*>(Bb + row * 128 + (sw3(row, s * 4 + fk) << 4));
     }
     // restage one half-tile; keep the 3 youngest half-tiles in flight
-    if constexpr (HALO) {
-      // B halves as below; the next chunk's A image in P2 of the second-to-last tap. Waits: P0 retires B-hi(k)
-      // (keeping an image issued in the previous K-tile in flight), P3 retires B-lo(k+1) (keeping B-hi(k+1) and
-      // an image issued in P2); the last tap's P3 retires the image before the next chunk's first read.
-      if constexpr (P == 0) {
-        issue_b(0, kt + 1, nc, nj);
-        if (kj == taps - 1) vm_wait<CF::BH + CF::AI>(); else vm_wait<CF::BH>();
-      } else if constexpr (P == 1) {
-        issue_b(1, kt + 1, nc, nj);
-      } else if constexpr (P == 2) {
-        if (kj == taps - 2) issue_img(kc + 1);
-      } else {
-        if (kj == taps - 2) vm_wait<CF::BH + CF::AI>(); else vm_wait<CF::BH>();
-      }
-    } else if constexpr (P == 0) {
+    if constexpr (P == 0) {
       issue_b(0, kt + 1);
       vm_wait<CF::BH + 2 * CF::AH>();
     } else if constexpr (P == 1) {
@@ -328,37 +244,21 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   };
 
   // ---- prologue: A-lo(0), B-lo(0), B-hi(0), A-hi(0), A-lo(1) in flight; retire the first two
-  // (HALO: image(0), B-lo(0), B-hi(0); retire the first two)
-  if constexpr (HALO) {
-    issue_img(0);
-    issue_b(0, 0);
-    issue_b(1, 0);
-    vm_wait<CF::BH>();
-  } else {
-    issue_a(0, 0);
-    issue_b(0, 0);
-    issue_b(1, 0);
-    issue_a(1, 0);
-    issue_a(0, 1);
-    vm_wait<2 * CF::AH + CF::BH>();
-  }
+  issue_a(0, 0);
+  issue_b(0, 0);
+  issue_b(1, 0);
+  issue_a(1, 0);
+  issue_a(0, 1);
+  vm_wait<2 * CF::AH + CF::BH>();
   g3_barrier();
   if (wm == 1) g3_barrier();  // stagger: group 1 runs one barrier behind group 0
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
-  for (int kt = 0, kc = 0, kj = 0; kt < nk; ++kt) {
-    int nc = kc, nj = kj + 1;
-    if (HALO && nj == taps) {
-      nj = 0;
-      ++nc;
-    }
-    if constexpr (!HALO) kc = kt;
-    phase(I0{}, I0{}, kt, kc, kj, nc, nj);
-    phase(I0{}, I1{}, kt, kc, kj, nc, nj);
-    phase(I1{}, I0{}, kt, kc, kj, nc, nj);
-    phase(I1{}, I1{}, kt, kc, kj, nc, nj);
-    kc = nc;
-    kj = nj;
+  for (int kt = 0; kt < nk; ++kt) {
+    phase(I0{}, I0{}, kt);
+    phase(I0{}, I1{}, kt);
+    phase(I1{}, I0{}, kt);
+    phase(I1{}, I1{}, kt);
   }
   if (wm == 0) g3_barrier();
   vm_wait<0>();  // trailing dummy DMAs land before the ring is reused for C staging (or the workgroup ends)
@@ -512,18 +412,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   }
 }
 
-// tap reuse applies to same-length stride-1 multi-tap convs whose K-tiles are whole taps, with |shift| <= 32
-// Opt-in (tuning gemm_halo = 1): measured on MI355X it moves ~40 % fewer operand bytes yet runs 5-10 % SLOWER than
-// the per-tap schedule on the DiffSVC / BigVGAN shapes (tools/gemm_bench.py), so these GEMMs are not
-// bound by the L2 -> LDS byte rate; kept, parity-tested, for the next schedule revision.
-static int halo_of(const ConvGemmArgs& a) {
-  if (tuning().gemm_halo != 1 || a.tv) return 0;  // (the halo image masks by the uniform T_in only)
-  const int taps = a.Cp > 0 ? a.K / a.Cp : 0;
-  if (!(a.Cp % 64 == 0 && a.K == a.Kpad && taps >= 2 && a.istride == 1 && a.T_in == a.T_out)) return 0;
-  const int h = std::max(std::abs(a.tap_add), std::abs((taps - 1) * a.tap_mul + a.tap_add));
-  return h >= 1 && h <= 32 ? h : 0;
-}
-
 // Register epilogue form of a generic epilogue (G3_LDS when it has none). tuning gemm3_direct is a mask of the forms in
 // use: 1 = G3_F16, 2 = G3_RES32, 4 = G3_SPLIT, 8 = also inside the DiffSVC sampler (run_gemm sets no_reg_epi there
 // otherwise); default 3, 0 = the LDS epilogue everywhere. Alone every form is as fast or faster (Whisper fc1 12 %,
@@ -543,31 +431,6 @@ static int direct_form3(const ConvGemmArgs& a, const EpiArgs& e) {
 template <int BM, int BN, bool PAIR>
 static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipStream_t s, const char* tag) {
   ConvGemmArgs a = a0;
-  a.halo = halo_of(a);
-  if (a.halo) {
-    using CH = G3<BM, BN, true>;
-    const int M = a.B * a.T_out;
-    a.ntiles_n = cdiv(a.N, BN);
-    const int64_t grid = (int64_t)cdiv(M, BM) * a.ntiles_n;
-    SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm3: bad grid");
-    SVC_REQUIRE((int64_t)a.ntiles_n * BN <= std::max(round_up(a.N, 256), round_up(a.N, 384)),
-                "conv_gemm3: weights not padded for BN=%d", BN);
-    static bool attr_h = false;
-    if (!attr_h) {
-      SVC_HIP_CHECK(hipFuncSetAttribute((const void*)conv_gemm3_kernel<BM, BN, true, PAIR, true>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, CH::LDS));
-      attr_h = true;
-    }
-    const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
-    char htag[64];
-    snprintf(htag, sizeof htag, "%s+halo", tag);
-    const int tok = prof_begin(htag, 2.0 * M * (double)a.N * kreal, 0.0, s);
-    hipLaunchKernelGGL((conv_gemm3_kernel<BM, BN, true, PAIR, true>), dim3((unsigned)grid), dim3(CH::NT), CH::LDS, s,
-                       a, e, zpage, 1.0f / (float)a.Cp);
-    prof_end(tok, s);
-    SVC_LAUNCH_CHECK();
-    return SVC_OK;
-  }
   using CF = G3<BM, BN>;
   const int M = a.B * a.T_out;
   const int form = PAIR ? G3_LDS : direct_form3(a, e);
@@ -578,14 +441,14 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
               "conv_gemm3: weights not padded for BN=%d", BN);
   const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
   const void* fns[2][4] = {
-      {(const void*)conv_gemm3_kernel<BM, BN, false, PAIR, false, G3_LDS>,
-       (const void*)conv_gemm3_kernel<BM, BN, false, false, false, G3_F16>,
-       (const void*)conv_gemm3_kernel<BM, BN, false, false, false, G3_RES32>,
-       (const void*)conv_gemm3_kernel<BM, BN, false, false, false, G3_SPLIT>},
-      {(const void*)conv_gemm3_kernel<BM, BN, true, PAIR, false, G3_LDS>,
-       (const void*)conv_gemm3_kernel<BM, BN, true, false, false, G3_F16>,
-       (const void*)conv_gemm3_kernel<BM, BN, true, false, false, G3_RES32>,
-       (const void*)conv_gemm3_kernel<BM, BN, true, false, false, G3_SPLIT>}};
+      {(const void*)conv_gemm3_kernel<BM, BN, false, PAIR, G3_LDS>,
+       (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_F16>,
+       (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_RES32>,
+       (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_SPLIT>},
+      {(const void*)conv_gemm3_kernel<BM, BN, true, PAIR, G3_LDS>,
+       (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_F16>,
+       (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_RES32>,
+       (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_SPLIT>}};
   const void* fn = fns[cp64][form];
   // the register forms need only the operand ring (no C staging)
   const int lds = form == G3_LDS ? CF::LDS : CF::RING;

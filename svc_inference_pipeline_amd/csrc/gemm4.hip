@@ -11,6 +11,7 @@
 //     epilogue runs beside the other's MFMAs (inter-workgroup overlap in place of intra-workgroup staggering);
 //   * the same operand images (128-B rows, 16-B chunk swizzle kv ^ (row & 6)), A loader (per-tap row shifts, zero
 //     rows outside the utterance) and LDS-staged vector epilogue (epilogue.h) as conv_gemm3.
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -45,10 +46,8 @@ __device__ __forceinline__ void g4_barrier() {
 // sit in the same lane. The gate is then applied in registers: no 64 KiB f32 round trip through LDS, the conditioner
 // projection and bias are prefetched into registers under the last K-tile's MFMAs, and each lane stores 4 channels
 // (8 B) per row.
-//
-// DIRECT without PAIR: the same register epilogue for the residual read-modify-write (the DiffSVC output projection):
-// v = (acc32 + (C + bias)) / acc_div -> out32, f16(v + add16) -> out16, with rows stored in place (orow = m). Each lane
-// owns 4 consecutive columns of a row: 16-B f32 loads / stores, the acc32 tile prefetched under the last K-tile.
+// (Round 2 also had a register read-modify-write epilogue for the DiffSVC output projection here; faster alone, slower
+// beside the sampler's other stream, it was removed in round 3.)
 // blockIdx -> a workgroup index whose consecutive values land on one XCD (tiles sharing A rows share that XCD's L2)
 __device__ __forceinline__ int g4_xcd_remap() {
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -57,9 +56,10 @@ __device__ __forceinline__ int g4_xcd_remap() {
 }
 
 // One 128 x 128 output tile (index wgid, N-tiles fastest) of the implicit GEMM, by the calling 256-thread workgroup.
-template <bool CP64, bool PAIR, bool DIRECT>
+template <bool CP64, bool PAIR, bool DIRECT, int OPT = 0>
 __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage,
                                                 float inv_cp, int wgid, unsigned char* sm4) {
+  static_assert(!DIRECT || PAIR, "the register epilogue is the gate's");
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -91,6 +91,22 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
     }
     b_p[v] = a.W + (int64_t)(n0 + row) * a.Kpad + kv * 8;
   }
+  // (experiment OPT & 1) interior tiles: all 128 rows in one utterance; a K-tile whose tap shift keeps every row's
+  // source inside it needs no per-lane validity select (wave-uniform test per K-tile)
+  const f16* a_base[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) a_base[v] = a_p[v] + (int64_t)a_t[v] * a.ldx;
+  int i_lo = 1, i_hi = 0;  // interior K-tiles need i_lo <= shift < i_hi
+  {
+    const int b0 = m0 / a.T_out, t0 = m0 - b0 * a.T_out;
+    if (m0 + G4_BM <= M && t0 + G4_BM <= a.T_out) {
+      const int tin = valid_in_rows(a, b0);
+      i_lo = -t0 * a.istride;
+      i_hi = tin - (t0 + G4_BM - 1) * a.istride;
+    }
+    i_lo = __builtin_amdgcn_readfirstlane(i_lo);
+    i_hi = __builtin_amdgcn_readfirstlane(i_hi);
+  }
   auto issue = [&](int kt) {
     unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
     unsigned char* Bm = A + G4_BM * 128;
@@ -101,12 +117,16 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
       const int c0 = kg - tap * a.Cp;
       const int shift = tap * a.tap_mul + a.tap_add;
       const int64_t off = (int64_t)shift * a.ldx + c0;
+      if ((OPT & 1) && live && shift >= i_lo && shift < i_hi) {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int st = a_t[v] + shift;
-        const bool ok = live && st >= 0 && st < a_tin[v];
-        g4_dma(ok ? (const void*)(a_p[v] + (int64_t)a_t[v] * a.ldx + off) : (const void*)zsrc,
-               A + (wave * 4 + v) * 1024);
+        for (int v = 0; v < 4; ++v) g4_dma(a_base[v] + off, A + (wave * 4 + v) * 1024);
+      } else {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int st = a_t[v] + shift;
+          const bool ok = live && st >= 0 && st < a_tin[v];
+          g4_dma(ok ? (const void*)(a_base[v] + off) : (const void*)zsrc, A + (wave * 4 + v) * 1024);
+        }
       }
     } else {
 #pragma unroll
@@ -146,26 +166,8 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
     for (int j = 0; j < 2; ++j) cpg[i][j].u = cpf[i][j].u = make_uint2(0u, 0u);  // diagnostics runs without cp
   bg[0] = bg[1] = bfl[0] = bfl[1] = make_float4(0.f, 0.f, 0.f, 0.f);
   // row group i of the epilogue operands; group 0 also loads the bias
-  float4 res[4][4];  // DIRECT && !PAIR: the acc32 (residual) tile
   auto prefetch = [&](auto ic) {
     constexpr int i = decltype(ic)::value;
-    if constexpr (!PAIR) {
-      if (!wave_cols) return;
-      const int m = min(m0 + wm * 64 + i * 16 + fr, M - 1);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = min(nw + j * 16 + fk * 4, a.N - 4);  // clamped columns are loaded but never stored
-        if (e.acc16_hi) {  // split residual: the raw hi / lo halves, combined in the epilogue
-          const uint2 h = *reinterpret_cast<const uint2*>(e.acc16_hi + (int64_t)m * e.ld_acc + n);
-          const uint2 l = *reinterpret_cast<const uint2*>(e.acc16_lo + (int64_t)m * e.ld_acc + n);
-          res[i][j] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x),
-                                  __uint_as_float(l.y));
-        } else {
-          res[i][j] = *reinterpret_cast<const float4*>(e.acc32 + (int64_t)m * e.ld_acc + n);
-        }
-      }
-      return;
-    }
     if (!wave_cols || e.cp == nullptr) return;
     if constexpr (i == 0) {
 #pragma unroll
@@ -189,6 +191,21 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
   for (int kt = 0; kt < nk; ++kt) {
     g4_vmwait<0>();  // this wave's DMAs of stage kt have landed (nothing younger is outstanding)
     g4_barrier();    // ... and everyone's; stage (kt + 1) & 1 is free
+    const unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
+    const unsigned char* Bm = A + G4_BM * 128;
+    half8 af0[4], bf0[4];
+    if constexpr ((OPT & 2) != 0) {  // (experiment) this K-tile's first fragments before the next DMA issue
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        af0[i] = *reinterpret_cast<const half8*>(A + row * 128 + (sw4(row, fk) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = wn * 64 + j * 16 + fr;
+        bf0[j] = *reinterpret_cast<const half8*>(Bm + row * 128 + (sw4(row, fk) << 4));
+      }
+    }
     if (kt + 1 < nk) issue(kt + 1);
     if constexpr (DIRECT) {
       if (kt + 1 == nk) {  // under the last K-tile's MFMAs (spreading these over earlier K-steps measured no better)
@@ -198,20 +215,23 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
         prefetch(std::integral_constant<int, 3>{});
       }
     }
-    const unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
-    const unsigned char* Bm = A + G4_BM * 128;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       half8 af[4], bf[4];
+      if ((OPT & 2) != 0 && s == 0) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + fr;
-        af[i] = *reinterpret_cast<const half8*>(A + row * 128 + (sw4(row, s * 4 + fk) << 4));
-      }
+        for (int i = 0; i < 4; ++i) af[i] = af0[i], bf[i] = bf0[i];
+      } else {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wn * 64 + j * 16 + fr;
-        bf[j] = *reinterpret_cast<const half8*>(Bm + row * 128 + (sw4(row, s * 4 + fk) << 4));
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * 64 + i * 16 + fr;
+          af[i] = *reinterpret_cast<const half8*>(A + row * 128 + (sw4(row, s * 4 + fk) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = wn * 64 + j * 16 + fr;
+          bf[j] = *reinterpret_cast<const half8*>(Bm + row * 128 + (sw4(row, s * 4 + fk) << 4));
+        }
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -225,48 +245,6 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
         }
       __builtin_amdgcn_s_setprio(0);
     }
-  }
-  if constexpr (DIRECT && !PAIR) {
-    if (!wave_cols) return;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = nw + j * 16 + fk * 4;
-      if (n >= a.N) continue;
-      const float4 bi = *reinterpret_cast<const float4*>(e.bias + n);
-      const float4 ad = *reinterpret_cast<const float4*>(e.add16 + n);
-      const bool split = e.acc16_hi != nullptr;
-      const float4 sb = split ? *reinterpret_cast<const float4*>(e.acc_sub + n) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wm * 64 + i * 16 + fr;
-        if (m >= M) continue;
-        float4 v = make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w);
-        float4 ac = res[i][j];
-        if (split) {  // (hi + lo) - the add16 it was stored with, as epilogue_pass
-          H4 hi, lo;
-          hi.u = make_uint2(__float_as_uint(ac.x), __float_as_uint(ac.y));
-          lo.u = make_uint2(__float_as_uint(ac.z), __float_as_uint(ac.w));
-          ac.x = ((float)hi.h[0] + (float)lo.h[0]) - sb.x; ac.y = ((float)hi.h[1] + (float)lo.h[1]) - sb.y;
-          ac.z = ((float)hi.h[2] + (float)lo.h[2]) - sb.z; ac.w = ((float)hi.h[3] + (float)lo.h[3]) - sb.w;
-        }
-        v.x = (ac.x + v.x) / e.acc_div;  // the order and IEEE division of epilogue_pass
-        v.y = (ac.y + v.y) / e.acc_div;
-        v.z = (ac.z + v.z) / e.acc_div;
-        v.w = (ac.w + v.w) / e.acc_div;
-        if (!split) *reinterpret_cast<float4*>(e.out32 + (int64_t)m * e.ld32 + n) = v;
-        const float4 w = make_float4(v.x + ad.x, v.y + ad.y, v.z + ad.z, v.w + ad.w);
-        H4 pk;
-        pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
-        *reinterpret_cast<uint2*>(e.out16 + (int64_t)m * e.ld16 + n) = pk.u;
-        if (split) {
-          H4 lo;
-          lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);
-          lo.h[2] = (f16)(w.z - (float)pk.h[2]); lo.h[3] = (f16)(w.w - (float)pk.h[3]);
-          *reinterpret_cast<uint2*>(e.lo16 + (int64_t)m * e.ld16 + n) = lo.u;
-        }
-      }
-    }
-    return;
   }
   if constexpr (DIRECT && PAIR) {
     if (!wave_cols) return;
@@ -319,24 +297,13 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
   epilogue_pass<G4_BM, G4_BN, G4_LDC, G4_NT, PAIR>(Cs, m0, n0, M, a, e, tid);
 }
 
-template <bool CP64, bool PAIR, bool DIRECT>
+template <bool CP64, bool PAIR, bool DIRECT, int OPT = 0>
 __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage, float inv_cp) {
   extern __shared__ __align__(16) unsigned char sm4[];
-  conv_gemm4_tile<CP64, PAIR, DIRECT>(a, e, zpage, inv_cp, g4_xcd_remap(), sm4);
+  conv_gemm4_tile<CP64, PAIR, DIRECT, OPT>(a, e, zpage, inv_cp, g4_xcd_remap(), sm4);
 }
 
-// the direct residual epilogue covers exactly the DiffSVC output projection's form
-bool conv_gemm4_rmw_form(const ConvGemmArgs& a, const EpiArgs& e) {
-  // f32 residual (acc32 -> out32) or the split-fp16 one (acc16_hi / acc16_lo - acc_sub -> out16 / lo16)
-  const bool f32 = e.acc32 && e.out32 && !e.acc16_hi && !e.lo16 && e.ld32 % 4 == 0;
-  const bool split = !e.acc32 && !e.out32 && e.acc16_hi && e.acc16_lo && e.acc_sub && e.lo16;
-  return e.kind == EPI_GENERIC && e.act == ACT_NONE && (f32 || split) && e.out16 && e.add16 && !e.add_t &&
-         !e.add_row && e.scale_cols == 0 && e.split16 == 0 && e.T_ostore == a.T_out && e.ostride == 1 &&
-         e.ophase == 0 && a.N % 4 == 0 && e.ld_acc % 4 == 0 && e.ld16 % 4 == 0;
-}
-
-// direct: the register epilogue (DIRECT: gate, or the residual read-modify-write) where the epilogue has that form,
-// otherwise the LDS-staged epilogue_pass
+// direct: the register gate epilogue (paired epilogues only), otherwise the LDS-staged epilogue_pass
 int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate) {
   ConvGemmArgs a = a0;
   SVC_REQUIRE(a.Cp % 8 == 0 && a.ldx % 8 == 0 && a.Kpad % 64 == 0 && a.N % 4 == 0, "conv_gemm4: layout");
@@ -345,25 +312,34 @@ int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipSt
   SVC_REQUIRE(!pair || a.N % 64 == 0, "conv_gemm4: paired epilogue needs N %% 64 == 0");
   const int M = a.B * a.T_out;
   a.ntiles_n = cdiv(a.N, G4_BN);
-  a.halo = 0;
   const int64_t grid = (int64_t)cdiv(M, G4_BM) * a.ntiles_n;
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm4: bad grid");
   const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
-  const bool direct = direct_gate && (pair || conv_gemm4_rmw_form(a, e));
+  const bool direct = direct_gate && pair;
   static bool attr[2][2][2] = {};
   const void* fns[2][2][2] = {
-      {{(const void*)conv_gemm4_kernel<false, false, false>, (const void*)conv_gemm4_kernel<false, false, true>},
+      {{(const void*)conv_gemm4_kernel<false, false, false>, nullptr},
        {(const void*)conv_gemm4_kernel<false, true, false>, (const void*)conv_gemm4_kernel<false, true, true>}},
-      {{(const void*)conv_gemm4_kernel<true, false, false>, (const void*)conv_gemm4_kernel<true, false, true>},
+      {{(const void*)conv_gemm4_kernel<true, false, false>, nullptr},
        {(const void*)conv_gemm4_kernel<true, true, false>, (const void*)conv_gemm4_kernel<true, true, true>}}};
   const void* fn = fns[cp64][pair][direct];
-  if (!attr[cp64][pair][direct]) {
+  static const int xopt = getenv("SVC_X_G4") ? atoi(getenv("SVC_X_G4")) : 0;  // experiment
+  if (cp64 && pair && direct && xopt) {
+    const void* xf[4] = {nullptr, (const void*)conv_gemm4_kernel<true, true, true, 1>,
+                         (const void*)conv_gemm4_kernel<true, true, true, 2>,
+                         (const void*)conv_gemm4_kernel<true, true, true, 3>};
+    fn = xf[xopt & 3];
+    static bool xa[4] = {};
+    if (!xa[xopt & 3]) {
+      SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G4_LDS));
+      xa[xopt & 3] = true;
+    }
+  } else if (!attr[cp64][pair][direct]) {
     SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G4_LDS));
     attr[cp64][pair][direct] = true;
   }
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
-  const char* tag = direct ? (pair ? "conv_gemm4<128,128,gate>" : "conv_gemm4<128,128,rmw>")
-                           : pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>";
+  const char* tag = direct ? "conv_gemm4<128,128,gate>" : pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>";
   const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);
   const dim3 g((unsigned)grid), b(G4_NT);
   const float inv = 1.0f / (float)a.Cp;

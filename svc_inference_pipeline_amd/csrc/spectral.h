@@ -20,7 +20,6 @@ struct DftArgs {
   // ragged batches (optional): utterance b has nb[b] samples (its n_valid and n_logical) and Tb[b] frames
   const int64_t* nb;
   const int* Tb;
-  int dbg;  // tuning dft_dbg (diagnostics)
 };
 
 // windowed frames -> f64 FFT -> |X| or |X|^2 -> filterbank -> ln / log10 (-> energy), one launch

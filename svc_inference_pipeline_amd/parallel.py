@@ -6,6 +6,7 @@ shard with no data-path collective; the only exchange is the final gather of eve
 waveforms to rank 0. Sampler noise is keyed by the global utterance id, so outputs are identical
 for any world size.
 """
+import datetime
 import os
 
 import torch
@@ -19,23 +20,35 @@ def shard(n_items, rank, world):
     return start, start + q + (1 if rank < r else 0)
 
 
+DEFAULT_TIMEOUT_S = 600.0  # rendezvous and every collective; SVC_DIST_TIMEOUT_S overrides
+
+
 class DistContext:
     def __init__(self, rank=0, world=1, local_rank=0, backend=None):
         self.rank, self.world, self.local_rank, self.backend = rank, world, local_rank, backend
 
     @classmethod
-    def from_env(cls, backend=None):
+    def from_env(cls, backend=None, timeout_s=None):
+        """One rank of a torch.distributed.run / bench.spawn_ranks launch (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_*).
+        Collectives time out after `timeout_s` (default SVC_DIST_TIMEOUT_S or 600 s): a rank whose peer hangs
+        raises instead of waiting forever, so the launcher sees it exit and can end the job."""
         world = int(os.environ.get("WORLD_SIZE", "1"))
         rank = int(os.environ.get("RANK", "0"))
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if world > 1 and not torchdist.is_initialized():
             backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if timeout_s is None:
+                timeout_s = float(os.environ.get("SVC_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+            timeout = datetime.timedelta(seconds=timeout_s)
             if backend == "nccl":
                 torch.cuda.set_device(local)
-                torchdist.init_process_group(backend, device_id=torch.device("cuda", local))
+                torchdist.init_process_group(backend, timeout=timeout, device_id=torch.device("cuda", local))
             else:
-                torchdist.init_process_group(backend)
+                torchdist.init_process_group(backend, timeout=timeout)
+        if torchdist.is_initialized():  # the process group's own view (what rank 0 reports)
+            world, rank = torchdist.get_world_size(), torchdist.get_rank()
+            backend = str(torchdist.get_backend())
         return cls(rank, world, local, backend)
 
     def barrier(self):
@@ -66,14 +79,19 @@ class DistContext:
         The (B_r, S_r) shapes are all-gathered first (one int64 pair per rank); each shard is zero-padded to the
         largest B and S, so ranks may hold different numbers of utterances and different clip lengths.
         `lengths` (int [B_r], default S_r for every row) are the per-utterance valid sample counts; with
-        `return_lengths` rank 0 also gets them for the whole gathered batch (int64 [sum B_r], None elsewhere)."""
+        `return_lengths` rank 0 also gets them for the whole gathered batch (int64 [sum B_r], None elsewhere).
+        A 1-D wav is one utterance ([1, S_r])."""
+        if wav.dim() == 1:
+            wav = wav.reshape(1, -1)
+        if wav.dim() != 2:
+            raise ValueError(f"gather_waveforms: wav must be [B, S] or [S], got {tuple(wav.shape)}")
         if lengths is None:
-            lengths = torch.full((wav.shape[0],), wav.shape[1] if wav.dim() > 1 else 0, dtype=torch.int64)
+            lengths = torch.full((wav.shape[0],), wav.shape[1], dtype=torch.int64)
         lengths = torch.as_tensor(lengths, dtype=torch.int64)
         if self.world == 1:
             return (wav, lengths) if return_lengths else wav
         dev = wav.device
-        shape = torch.tensor([wav.shape[0], wav.shape[1] if wav.dim() > 1 else 0], dtype=torch.int64, device=dev)
+        shape = torch.tensor([wav.shape[0], wav.shape[1]], dtype=torch.int64, device=dev)
         shapes = [torch.zeros_like(shape) for _ in range(self.world)]
         torchdist.all_gather(shapes, shape)
         shapes = [(int(s[0].item()), int(s[1].item())) for s in shapes]

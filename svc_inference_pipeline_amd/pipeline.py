@@ -101,6 +101,13 @@ class SVCPipeline:
 
     def convert(self, wav24, wav16, singer, fast_inference=True, speedup=10, seed=0, utt_ids=None, x_T=None,
                 noise=None, f0=None, wav16_float=None):
+        """infer.py's sequence for B equal-length clips -> ConvertResult. `f0` (optional, f64 [B, T]) replaces the
+        Praat extraction; it is pitch-shifted on a copy (the caller's tensor is not modified)."""
+        with self.engine.lock:
+            return self._convert(wav24, wav16, singer, fast_inference, speedup, seed, utt_ids, x_T, noise, f0,
+                                 wav16_float)
+
+    def _convert(self, wav24, wav16, singer, fast_inference, speedup, seed, utt_ids, x_T, noise, f0, wav16_float):
         e = self.engine
         T = mel_frames(wav24.shape[1], e.cfg.n_fft, e.cfg.hop_length)  # utils/mel.py:130-174 frame count
         # The 24 kHz features (mel / energy, and F0: Praat AC + pitch shift, latency-bound serial work on few CUs)
@@ -111,8 +118,8 @@ class SVCPipeline:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             mel, energy = e.mel_energy(wav24)
-            if f0 is None:
-                f0 = e.f0(wav24, T)
+            # a caller-supplied f0 is shifted on a copy (svc_pitch_shift works in place)
+            f0 = e.f0(wav24, T) if f0 is None else f0.to(torch.float64).contiguous().clone()
             e.pitch_shift(f0)
         assert mel.shape[1] == T
         content = self.content(wav16, T, wav16_float)
@@ -217,6 +224,10 @@ class SVCPipeline:
         """infer.py's sequence for B clips of different lengths as ONE padded batch: the C-ABI stages take the
         per-utterance lengths (include/svc_hip.h, "Ragged batches") and compute each clip exactly as alone.
         -> list of waveforms f32 [T_b * hop]."""
+        with self.engine.lock:
+            return self._convert_ragged(wavs24, wavs16, singers, wavs16_float, fast_inference, speedup, seed, utt_ids)
+
+    def _convert_ragged(self, wavs24, wavs16, singers, wavs16_float, fast_inference, speedup, seed, utt_ids):
         e = self.engine
         n = len(wavs24)
         ids = list(range(n)) if utt_ids is None else [int(u) for u in utt_ids]

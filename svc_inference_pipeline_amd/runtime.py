@@ -3,6 +3,7 @@ torch device tensors (PyTorch supplies device memory and the HIP stream; all com
 libsvc_hip.so). Layout of every tensor is time-major [B, T, C] (row = b*T + t).
 """
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -52,6 +53,38 @@ def check_supported(cfg):
                          "(modules/bigvgan.py:392-421)")
 
 
+def engine_config_keys(c):
+    """The reference config (utils/util.py JSON5 tree) flattened into the numeric keys svc_ctx_set_config takes."""
+    kv = {k: getattr(c, k) for k in ("fs", "n_fft", "hop_length", "win_length", "n_mels", "fmin", "fmax", "f0_min",
+                                     "f0_max")}
+    m = c.mapper
+    for k in ("residual_channels", "residual_layer_num", "n_mel", "diffusion_fc_size", "dilation_cycle_length",
+              "residual_kernel_size"):
+        kv["mapper." + k] = m[k]
+    kv["mapper.noise_schedule_factors.0"] = m.noise_schedule_factors[0]
+    kv["mapper.noise_schedule_factors.1"] = m.noise_schedule_factors[1]
+    v = c.vocoder
+    kv["vocoder.n_stages"] = len(v.upsample_rates)
+    kv["vocoder.n_kernels"] = len(v.resblock_kernel_sizes)
+    kv["vocoder.upsample_initial_channel"] = v.upsample_initial_channel
+    kv["vocoder.input_dim"] = v.input_dim
+    # modules/bigvgan.py:536 (AMPBlock1 if resblock == "1" else AMPBlock2), :392-421 snake / snakebeta
+    kv["vocoder.resblock"] = 2 if str(v.resblock) == "2" else 1
+    if v.activation not in ("snake", "snakebeta"):
+        raise ValueError(f"vocoder.activation {v.activation!r}: snake or snakebeta (modules/bigvgan.py:392-421)")
+    kv["vocoder.snake"] = 1 if v.activation == "snake" else 0
+    kv["vocoder.snake_logscale"] = 1 if v.snake_logscale else 0
+    for i, (u, k) in enumerate(zip(v.upsample_rates, v.upsample_kernel_sizes)):
+        kv[f"vocoder.upsample_rates.{i}"] = u
+        kv[f"vocoder.upsample_kernel_sizes.{i}"] = k
+    for j, (k, ds) in enumerate(zip(v.resblock_kernel_sizes, v.resblock_dilation_sizes)):
+        kv[f"vocoder.resblock_kernel_sizes.{j}"] = k
+        kv[f"vocoder.resblock_dilation_sizes.{j}.n"] = len(ds)
+        for l, d in enumerate(ds):
+            kv[f"vocoder.resblock_dilation_sizes.{j}.{l}"] = d
+    return kv
+
+
 class SVCEngine:
     """Stages of infer.py on one GPU. `whisper_state`, `mapper_state`, `vocoder_state`, `hubert_state` are dicts
     in the reference's state_dict naming (svc_inference_pipeline_amd.weights; fairseq's for HuBERT); any subset
@@ -62,13 +95,17 @@ class SVCEngine:
     2x, no extra activation bytes; the weight rounding is the larger share of their error) with the conv stem and
     HuBERT as in 1. `head_split` runs the DiffSVC head (skip_projection, output_projection) on split-fp16 operands,
     the largest denoiser-side term left. `config`: further numeric svc_ctx_set_config keys, set before finalize
-    (e.g. {"content.wsplit_linears": 12} to weight-split only the MLP linears)."""
+    (e.g. {"content.wsplit_mlp": 0xffffff} to weight-split the MLP linears of all 24 Whisper blocks; an unknown key
+    raises)."""
 
     def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None, hubert_state=None,
                  hubert_output_layer=9, content_split=2, head_split=True, config=None):
         check_supported(cfg)
         _lib.load()
         self.cfg = cfg
+        # a libsvc_hip context is not thread-safe (its workspace and length-table rings are shared by its entry
+        # points): SVCPipeline conversions and SVCServer's worker take this lock around a whole conversion
+        self.lock = threading.RLock()
         self.device = device
         self._ctx = ctypes.c_void_p()
         torch.cuda.set_device(device)
@@ -78,7 +115,7 @@ class SVCEngine:
         # content_split: False / 0 = fp16, True / 1 = split-fp16 operands, 2 = weight-split Whisper linears
         _lib.call("svc_ctx_set_config", self._ctx, b"content.split", float(int(content_split)))
         _lib.call("svc_ctx_set_config", self._ctx, b"mapper.head_split", 1.0 if head_split else 0.0)
-        for k, v in (config or {}).items():  # further svc_ctx_set_config keys (e.g. "content.wsplit_linears")
+        for k, v in (config or {}).items():  # further svc_ctx_set_config keys (e.g. "content.wsplit_mlp")
             _lib.call("svc_ctx_set_config", self._ctx, k.encode(), float(v))
         if whisper_state is not None:
             self._add_state("whisper.", whisper_state)
@@ -101,34 +138,7 @@ class SVCEngine:
 
     # ------------------------------------------------------------------ setup
     def _set_config(self):
-        c = self.cfg
-        kv = {k: getattr(c, k) for k in ("fs", "n_fft", "hop_length", "win_length", "n_mels", "fmin", "fmax", "f0_min", "f0_max")}
-        m = c.mapper
-        for k in ("residual_channels", "residual_layer_num", "n_mel", "diffusion_fc_size", "dilation_cycle_length",
-                  "residual_kernel_size"):
-            kv["mapper." + k] = m[k]
-        kv["mapper.noise_schedule_factors.0"] = m.noise_schedule_factors[0]
-        kv["mapper.noise_schedule_factors.1"] = m.noise_schedule_factors[1]
-        v = c.vocoder
-        kv["vocoder.n_stages"] = len(v.upsample_rates)
-        kv["vocoder.n_kernels"] = len(v.resblock_kernel_sizes)
-        kv["vocoder.upsample_initial_channel"] = v.upsample_initial_channel
-        kv["vocoder.input_dim"] = v.input_dim
-        # modules/bigvgan.py:536 (AMPBlock1 if resblock == "1" else AMPBlock2), :392-421 snake / snakebeta
-        kv["vocoder.resblock"] = 2 if str(v.resblock) == "2" else 1
-        if v.activation not in ("snake", "snakebeta"):
-            raise ValueError(f"vocoder.activation {v.activation!r}: snake or snakebeta (modules/bigvgan.py:392-421)")
-        kv["vocoder.snake"] = 1 if v.activation == "snake" else 0
-        kv["vocoder.snake_logscale"] = 1 if v.snake_logscale else 0
-        for i, (u, k) in enumerate(zip(v.upsample_rates, v.upsample_kernel_sizes)):
-            kv[f"vocoder.upsample_rates.{i}"] = u
-            kv[f"vocoder.upsample_kernel_sizes.{i}"] = k
-        for j, (k, ds) in enumerate(zip(v.resblock_kernel_sizes, v.resblock_dilation_sizes)):
-            kv[f"vocoder.resblock_kernel_sizes.{j}"] = k
-            kv[f"vocoder.resblock_dilation_sizes.{j}.n"] = len(ds)
-            for l, d in enumerate(ds):
-                kv[f"vocoder.resblock_dilation_sizes.{j}.{l}"] = d
-        for k, val in kv.items():
+        for k, val in engine_config_keys(self.cfg).items():
             _lib.call("svc_ctx_set_config", self._ctx, k.encode(), float(val))
 
     def _add(self, name, arr):
@@ -163,6 +173,10 @@ class SVCEngine:
         wb, wsb = ctypes.c_int64(), ctypes.c_int64()
         _lib.call("svc_ctx_memory", self._ctx, ctypes.byref(wb), ctypes.byref(wsb))
         return wb.value, wsb.value
+
+    def get_config(self, key):
+        """A configuration key's value on this context, or a kernel switch's ("tune.<name>")."""
+        return _lib.get_config(self._ctx, key)
 
     def tune(self, **switches):
         """Kernel switches of this context (csrc/common.h Tuning: A/B runs and parity tests), e.g.

@@ -13,6 +13,12 @@ it (so padding stays bounded: the kernels skip the padded tail, but its rows sti
 `max_batch`, waits at most `max_wait_s` for a batch to fill, and runs SVCPipeline.convert_ragged on it. Each request
 carries an utterance id (given, or a running counter) that keys its device noise, so its waveform is bit-identical to
 converting that clip alone with the same id, whatever it was batched with (tests/test_gpu_ragged.py).
+
+Streams: submit() records an event on the caller's current stream, and the worker's stream waits for it before it
+reads the request's tensors, so inputs produced by kernels still in flight on the caller's stream are safe to
+submit. A result is a view into the batch's output, recorded for use on the submitting stream (record_stream), and
+the future resolves once it is complete. The engine's lock (SVCEngine.lock) serialises the worker's conversions with
+any direct use of the same engine.
 """
 import collections
 import itertools
@@ -36,6 +42,8 @@ class _Request:
     wav16_float: torch.Tensor = None
     frames: int = 0
     t_submit: float = 0.0
+    ready: object = None    # torch.cuda.Event recorded on the submitting stream (None on the CPU)
+    stream: object = None   # the submitting stream
     future: Future = field(default_factory=Future)
 
 
@@ -70,6 +78,10 @@ class SVCServer:
                        utt_id=next(self._ids) if utt_id is None else int(utt_id),
                        wav16_float=None if wav16_float is None else wav16_float.reshape(-1),
                        frames=self._frames(n), t_submit=time.monotonic())
+        if wav24.is_cuda:
+            req.stream = torch.cuda.current_stream(wav24.device)
+            req.ready = torch.cuda.Event()
+            req.ready.record(req.stream)
         with self._cv:
             if self._closed:
                 raise RuntimeError("SVCServer.submit: the server is closed")
@@ -132,6 +144,14 @@ class SVCServer:
 
     def _convert(self, batch):
         try:
+            if torch.cuda.is_available():
+                work = torch.cuda.current_stream()
+                for r in batch:  # the inputs' producers on the submitting streams
+                    if r.ready is not None:
+                        work.wait_event(r.ready)
+                    for t in (r.wav24, r.wav16, r.wav16_float):
+                        if t is not None and t.is_cuda:
+                            t.record_stream(work)
             w16f = [r.wav16_float for r in batch] if batch[0].wav16_float is not None else None
             wavs = self.pipeline.convert_ragged([r.wav24 for r in batch], [r.wav16 for r in batch],
                                                 [r.singer for r in batch], wavs16_float=w16f,
@@ -140,6 +160,8 @@ class SVCServer:
                 torch.cuda.current_stream().synchronize()
             self.batches.append([r.utt_id for r in batch])
             for r, w in zip(batch, wavs):
+                if r.stream is not None and w.is_cuda:
+                    w.record_stream(r.stream)  # the batch buffer outlives the consumer's use on its own stream
                 r.future.set_result(w)
         except Exception as exc:  # noqa: BLE001 - every waiting caller gets the failure
             for r in batch:

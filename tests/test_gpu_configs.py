@@ -18,8 +18,8 @@ import torch
 pytestmark = pytest.mark.gpu
 
 from gpu_util import dev, rel_l2  # noqa: E402
+from mel_l1 import MEL_L1_TARGET, ddpm1000_mel_l1  # noqa: E402
 from oracle import features as OF  # noqa: E402
-from oracle import models as OM  # noqa: E402
 from oracle import noise as ON  # noqa: E402
 from oracle import pipeline as OP  # noqa: E402
 from oracle import praat_ac as PA  # noqa: E402
@@ -29,7 +29,6 @@ from svc_inference_pipeline_amd.pipeline import WINDOW_MEL_FRAMES, SVCPipeline  
 from svc_inference_pipeline_amd.runtime import SVCEngine  # noqa: E402
 
 MEDIUM = W.WHISPER_DIMS["medium"]
-MEL_L1_TARGET = 1e-3
 
 
 @pytest.fixture(scope="module")
@@ -81,45 +80,21 @@ def test_config4_180s_mel_f0_and_full_length_convert(long_setup):
     assert bool(torch.isfinite(r.wav).all()) and bool(torch.isfinite(r.x0).all())
 
 
-def test_config5_contentvec_ddpm1000_mel_l1():
-    """ContentVec (768 wide, 12 layers used up to output_layer 9, final_proj 256) + DDPM-1000 on a 1 s clip, shared
-    x_T and per-step noise, default precision mode: de-normalised ln-mel L1 <= 1e-3 against the fp32 oracle."""
+@pytest.mark.parametrize("seconds", [1.0, pytest.param(10.0, marks=pytest.mark.timeout(900))])
+def test_config5_contentvec_ddpm1000_mel_l1(seconds):
+    """ContentVec (768 wide, 12 layers used up to output_layer 9, final_proj 256) + DDPM-1000, shared x_T and per-step
+    noise, default precision mode: de-normalised ln-mel L1 <= 1e-3 against the fp32 oracle, at 1 s (T = 93) and at the
+    headline 10 s (T = 937)."""
     torch.set_num_threads(16)
     cfg = C.load_config()
     cfg.mapper.content_feature = ["contentvec"]
     cfg.mapper.input_content_dim["contentvec"] = W.HUBERT_DIMS["contentvec"]["final_dim"]
-    hs = W.make_hubert_state(W.HUBERT_DIMS["contentvec"], 0)
-    ms = W.make_mapper_state(cfg.mapper, 0)
-    vs = W.make_vocoder_state(cfg.vocoder, 0)
-    stats = C.load_stats(cfg)
-    w24 = ON.synth_clip(7, 1.0, 24000).astype(np.float32)
-    w16 = ON.synth_clip(7, 1.0, 16000).astype(np.float32)
-    T = OF.mel_frames(len(w24))
-    f0 = ON.synth_f0(4, T)
-    seed = 17
-    xT = ON.x_T(seed, 1, T)
-    noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
-    e = SVCEngine(cfg, 0, mapper_state=ms, vocoder_state=vs, hubert_state=hs)
+    states = dict(hubert=W.make_hubert_state(W.HUBERT_DIMS["contentvec"], 0), mapper=W.make_mapper_state(cfg.mapper, 0))
+    e = SVCEngine(cfg, 0, mapper_state=states["mapper"], vocoder_state=W.make_vocoder_state(cfg.vocoder, 0),
+                  hubert_state=states["hubert"])
     try:
-        res = SVCPipeline(e).convert(dev(w24[None]), dev(w16[None]), dev(np.array([2]), torch.int32),
-                                     fast_inference=False, x_T=dev(xT), noise=dev(noise),
-                                     f0=dev(f0[None], torch.float64), wav16_float=dev(w16[None]))
-        _, mel_gpu = e.bigvgan(res.x0, return_mel=True)
-        mel_gpu = mel_gpu[0].cpu().numpy().T
-        assert bool(torch.isfinite(res.wav).all())
+        l1 = ddpm1000_mel_l1(e, cfg, states, "contentvec", seconds)
     finally:
         e.close()
-    with torch.no_grad():
-        mel = OF.mel_spectrogram(torch.from_numpy(w24)[None], cfg)
-        en = OF.energy_from_mel(mel)
-        f0s = torch.from_numpy(OF.pitch_shift(f0, stats["target_f0_median"]))[None]
-        content = torch.from_numpy(np.asarray(OP.hubert_content(hs, w16, T), np.float32))[None]
-        cond = OM.conditioner(ms, {"contentvec": content}, f0s, en, torch.tensor([[2]]))
-        table = W.step_embedding_table(1000)
-        consts = OM.schedule_constants(C.noise_schedule(cfg.mapper))
-        den = lambda x, t: OM.diffsvc_forward(ms, cfg.mapper, x, cond, t, table)  # noqa: E731
-        x0 = OM.sample_ddpm(den, torch.from_numpy(xT), 1, T, 1000, consts,
-                            lambda i: torch.from_numpy(ON.step_noise(seed, i, 1, T)))
-    ref = OF.denormalize_mel_channel(x0[0].numpy().T, stats["mel_min"], stats["mel_max"])
-    l1 = float(np.mean(np.abs(mel_gpu - ref)))
+    print(f"mel-L1 contentvec DDPM-1000 {seconds:g} s: {l1:.4e}")
     assert l1 <= MEL_L1_TARGET, l1

@@ -16,17 +16,16 @@ import torch
 pytestmark = pytest.mark.gpu
 
 from gpu_util import dev, rel_l2  # noqa: E402
+from mel_l1 import MEL_L1_TARGET, ddpm1000_mel_l1  # noqa: E402
 from oracle import features as OF  # noqa: E402
 from oracle import models as OM  # noqa: E402
 from oracle import noise as ON  # noqa: E402
-from oracle import pipeline as OP  # noqa: E402
 from svc_inference_pipeline_amd import config as C  # noqa: E402
 from svc_inference_pipeline_amd import weights as W  # noqa: E402
 from svc_inference_pipeline_amd.pipeline import SVCPipeline  # noqa: E402
 from svc_inference_pipeline_amd.runtime import SVCEngine  # noqa: E402
 
 MEDIUM = W.WHISPER_DIMS["medium"]
-MEL_L1_TARGET = 1e-3   # BASELINE.json north_star: "<= 1e-3 mel-L1 vs the CPU reference"
 
 
 @pytest.fixture(scope="module")
@@ -78,38 +77,16 @@ def test_plms100_vs_golden(engine, golden):
     assert rel_l2(x[0].cpu().numpy().T, g["plms100"]) < 1e-3, rel_l2(x[0].cpu().numpy().T, g["plms100"])
 
 
-def _mel_l1(engine, cfg, states, seconds=1.0):
-    """Whisper-medium path, DDPM-1000, shared x_T and step noise: mean |delta| of the de-normalised ln-mel."""
-    stats = C.load_stats(cfg)
-    w24 = ON.synth_clip(7, seconds, 24000).astype(np.float32)
-    w16 = ON.synth_clip_16k_quantised(7, seconds)
-    T = OF.mel_frames(len(w24))
-    f0 = ON.synth_f0(4, T)
-    seed = 17
-    xT = ON.x_T(seed, 1, T)
-    noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
-    res = SVCPipeline(engine).convert(dev(w24[None]), dev(w16[None]), dev(np.array([2]), torch.int32),
-                                      fast_inference=False, x_T=dev(xT), noise=dev(noise),
-                                      f0=dev(f0[None], torch.float64))
-    _, mel_gpu = engine.bigvgan(res.x0, return_mel=True)
-    with torch.no_grad():
-        mel = OF.mel_spectrogram(torch.from_numpy(w24)[None], cfg)
-        en = OF.energy_from_mel(mel)
-        f0s = torch.from_numpy(OF.pitch_shift(f0, stats["target_f0_median"]))[None]
-        content = torch.from_numpy(np.asarray(OP.whisper_content(states["whisper"], w16, T), np.float32))[None]
-        cond = OM.conditioner(states["mapper"], {"whisper": content}, f0s, en, torch.tensor([[2]]))
-        table = W.step_embedding_table(1000)
-        consts = OM.schedule_constants(C.noise_schedule(cfg.mapper))
-        den = lambda x, t: OM.diffsvc_forward(states["mapper"], cfg.mapper, x, cond, t, table)  # noqa: E731
-        x0 = OM.sample_ddpm(den, torch.from_numpy(xT), 1, T, 1000, consts,
-                            lambda i: torch.from_numpy(ON.step_noise(seed, i, 1, T)))
-    ref = OF.denormalize_mel_channel(x0[0].numpy().T, stats["mel_min"], stats["mel_max"])
-    return float(np.mean(np.abs(mel_gpu[0].cpu().numpy().T - ref)))
-
-
-def test_mel_l1_north_star_whisper_medium(engine, cfg, states):
-    """The north-star tolerance on the headline content encoder, in the default precision mode."""
-    l1 = _mel_l1(engine, cfg, states)
+@pytest.mark.parametrize("seconds", [
+    1.0,
+    # the headline clip length (T = 937 frames): the oracle's DDPM-1000 takes ~1.5-3 min on 16 host threads
+    pytest.param(10.0, marks=pytest.mark.timeout(900)),
+])
+def test_mel_l1_north_star_whisper_medium(engine, cfg, states, seconds):
+    """The north-star tolerance on the headline content encoder, in the default precision mode, at 1 s (T = 93) and at
+    the headline 10 s (T = 937). Measured (round 2) 0.76-0.78e-3 at 1 s."""
+    l1 = ddpm1000_mel_l1(engine, cfg, states, "whisper", seconds)
+    print(f"mel-L1 whisper-medium DDPM-1000 {seconds:g} s: {l1:.4e}")
     assert l1 <= MEL_L1_TARGET, l1
 
 

@@ -37,10 +37,9 @@ def test_convert_many_matches_single_clips():
         e.close()
 
 
-def test_feature_side_stream_and_residual_modes(tune):
+def test_feature_side_stream():
     """The 24 kHz features on the context's sub-stream 2 (SVCPipeline.f0_side, default on) give bit-identical
-    conversions to running them on the caller's stream; the split-fp16 DiffSVC residual stream (default) stays within
-    2e-3 of the f32 one (tuning diff_res32 = 1) on the sampler output."""
+    conversions to running them on the caller's stream."""
     cfg = C.load_config()
     dims = W.WHISPER_DIMS["tiny-test"]
     cfg.mapper.input_content_dim["whisper"] = dims["n_audio_state"]
@@ -58,10 +57,6 @@ def test_feature_side_stream_and_residual_modes(tune):
             res[side] = (r.wav.clone(), r.f0.clone(), r.mel.clone(), r.x0.clone())
         for a, b in zip(res["1"], res["0"]):
             assert torch.equal(a, b)
-        tune(e, diff_res32=1)
-        x32 = pipe.convert(w24, w16, sing, speedup=250, seed=3).x0
-        rel = float(torch.linalg.norm(res["1"][3] - x32) / torch.linalg.norm(x32))
-        assert rel < 2e-3, rel
     finally:
         e.close()
 

@@ -148,20 +148,16 @@ def test_denoiser_vs_oracle(engine, states, cfg, B, T):
         assert rel_l2(eps, ref) < 5e-3, (t, rel_l2(eps, ref))
 
 
-@pytest.mark.parametrize("variant", ["20", "24", "rmw", "rmw32"])
+@pytest.mark.parametrize("variant", ["20", "24"])
 @pytest.mark.parametrize("B,T", [(3, 50), (2, 700), (5, 937)])
 def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, tune):
-    """The DiffSVC gate GEMM kernels (LDS-staged and in-register gate epilogues) and the register
-    residual epilogue of the output projection (rmw: split-fp16 residual, rmw32: f32 residual) on ragged row counts
-    (B*T not a multiple of the 128-row tile, utterance boundaries inside tiles) against the oracle's eps."""
+    """The DiffSVC gate GEMM kernels (conv_gemm4 with the LDS-staged and the in-register gate epilogue) on ragged row
+    counts (B*T not a multiple of the 128-row tile, utterance boundaries inside tiles) against the oracle's eps."""
     rng = np.random.default_rng(B * 7 + T)
     cond = rng.standard_normal((B, T, 384)).astype(np.float32)
     x = rng.standard_normal((B, T, 100)).astype(np.float32)
     table = W.step_embedding_table(1000)
-    if variant.startswith("rmw"):
-        tune(engine, gemm4_rmw=1, diff_res32=int(variant == "rmw32"))
-        variant = "15"
-    tune(engine, gemm_variant=variant, diff_fused=0)
+    tune(engine, gemm_variant=variant)
     eps = engine.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()
     with torch.no_grad():
         ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond),
@@ -170,35 +166,8 @@ def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, tune):
 
 
 @pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700), (5, 937)])
-def test_fused_layer_bit_identical(engine, states, cfg, B, T, tune):
-    """diff_layer.hip (dilated conv + gate + residual projection + split-fp16 residual update in ONE launch per layer,
-    opt-in) against the unfused kernels with the same K order, MFMA operand order and epilogue expressions
-    (conv_gemm4's register gate epilogue + its register residual epilogue): bit-identical eps on row counts that are not
-    multiples of the 128-row tile, utterance boundaries inside tiles and per-utterance frame counts (ragged dilated-conv
-    zero padding); the default unfused path (LDS-staged residual epilogue) within 1e-5, the oracle within 5e-3."""
-    rng = np.random.default_rng(B * 31 + T)
-    cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
-    x = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
-    frames = [max(1, T - 37 * b) for b in range(B)]
-    out = {}
-    for name, sw in (("fused", dict(diff_fused=1)), ("rmw", dict(diff_fused=0, gemm4_rmw=1)),
-                     ("lds", dict(diff_fused=0, gemm4_rmw=0))):
-        tune(engine, **sw)
-        out[name] = (engine.diffsvc_eps(cond, x, 250, frames=frames), engine.diffsvc_eps(cond, x, 7))
-    for k in range(2):
-        assert torch.equal(out["fused"][k], out["rmw"][k]), (k, rel_l2(out["fused"][k].cpu().numpy(),
-                                                                       out["rmw"][k].cpu().numpy()))
-        assert rel_l2(out["fused"][k].cpu().numpy(), out["lds"][k].cpu().numpy()) < 1e-5
-    table = W.step_embedding_table(1000)
-    with torch.no_grad():
-        ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, x.cpu(), cond.cpu(), torch.full((B,), 7, dtype=torch.long),
-                                 table).numpy()
-    assert rel_l2(out["fused"][1].cpu().numpy(), ref) < 5e-3
-
-
-@pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700), (5, 937)])
 def test_fused_head(engine, states, cfg, B, T, tune):
-    """diff_layer.hip diff_head (relu(skip_projection) + output_projection in one launch, u kept on chip) against the
+    """diff_head.hip (relu(skip_projection) + output_projection in one launch, u kept on chip) against the
     two unfused GEMMs: the same products, output_projection's K segments summed in another order (hi.W_hi, hi.W_lo,
     lo.W_hi), so within 1e-6 (f32 rounding order only); the oracle within 5e-3; ragged row counts."""
     rng = np.random.default_rng(B * 13 + T)
@@ -227,28 +196,6 @@ def test_fused_head_plms(engine, golden, tune):
     assert rel_l2(x4[0].cpu().numpy().T, g["plms4"]) < 1e-3
 
 
-@pytest.mark.parametrize("B,T,speedup", [(1, None, 250), (1, None, 10), (3, 211, 25)])
-def test_plms_fused_bit_identical(engine, golden, tune, B, T, speedup):
-    """The PLMS update applied in diff_head's epilogue (tuning plms_fused, opt-in), and with it the next denoise's
-    input projection (melpre_fused), against separate launches: the same expressions, K order and MFMA operand order,
-    so the sampled mel is bit-identical (first-step predictor pair, AB2-AB4, ragged sub-batches on several streams)."""
-    if T is None:
-        cond = dev(golden("conditioner_diffsvc")["cond"])
-        x_T = dev(golden("samplers")["x_T"])
-    else:
-        rng = np.random.default_rng(B * 5 + T)
-        cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
-        x_T = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
-    frames = None if T is None else [T - 41 * b for b in range(B)]
-    out = []
-    for sw in (dict(plms_fused=1, melpre_fused=1), dict(plms_fused=1, melpre_fused=0), dict(plms_fused=0)):
-        tune(engine, **sw)
-        out.append(engine.diffsvc_sample(cond, fast_inference=True, speedup=speedup, x_T=x_T, frames=frames))
-    assert torch.isfinite(out[0]).all()
-    for k in (0, 1):
-        assert torch.equal(out[k], out[2]), (k, rel_l2(out[k].cpu().numpy(), out[2].cpu().numpy()))
-
-
 @pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "24"])
 def test_eps_gemm_variants(engine, golden, variant, tune):
     """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path); 15lds:
@@ -256,7 +203,7 @@ def test_eps_gemm_variants(engine, golden, variant, tune):
     if variant in ("15lds", "15reg"):
         tune(engine, gemm3_direct=0 if variant == "15lds" else 15)
         variant = "15"
-    tune(engine, gemm_variant=variant, diff_fused=0)
+    tune(engine, gemm_variant=variant)
     g = golden("conditioner_diffsvc")
     eps = engine.diffsvc_eps(dev(g["cond"]), dev(g["x_in"]), 500)
     assert rel_l2(eps.cpu().numpy(), g["eps_t500"]) < 5e-3

@@ -145,3 +145,32 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--dry-run"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+@pytest.mark.parametrize("fault", ["raise", "hang"])
+def test_bench_spawn_rank_failure_ends_job(tmp_path, fault):
+    """A rank that raises mid-run, or hangs without exiting, ends the whole world-2 job with a non-zero status within
+    the collective timeout: the raising rank exits and spawn_ranks kills its peer; with a hanging rank, the peer's
+    gather times out (DistContext collective timeout), it exits non-zero, and spawn_ranks kills the hung rank."""
+    import subprocess
+    import sys
+    import time
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["CUDA_VISIBLE_DEVICES"] = ""
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run", "--batch", "2",
+                        "--seconds", "0.25", "--steps", "3", "--fault", fault, "--dist-timeout", "15"], env=env,
+                       capture_output=True, text=True, timeout=200)
+    assert r.returncode != 0
+    assert time.time() - t0 < 150
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]  # no result line from a failed job
+
+
+def test_gather_one_dimensional_world1():
+    """gather_waveforms takes a 1-D waveform as one utterance (world 1 returns it as [1, S] with its length)."""
+    d = DistContext()
+    out, lens = d.gather_waveforms(torch.arange(7, dtype=torch.float32), return_lengths=True)
+    assert out.shape == (1, 7) and lens.tolist() == [7]
+    with pytest.raises(ValueError):
+        d.gather_waveforms(torch.zeros(2, 3, 4))

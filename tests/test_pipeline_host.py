@@ -55,6 +55,8 @@ class _FakeEngine:
         self.cfg = C.load_config()
         self.cfg.mapper.content_feature = list(types)
         self.calls = []
+        import threading
+        self.lock = threading.RLock()
 
     def mel_energy(self, w24, n_samples=None):
         self.calls.append(("mel", tuple(w24.shape), list(n_samples)))

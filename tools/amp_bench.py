@@ -1,13 +1,11 @@
 """Fused BigVGAN activation + conv (amp_conv) microbenchmark (GPU): per-launch time of each (C, k, d) on the stage
-shapes (B = 32 clips x 10 s), full kernel and with one phase removed (kernel switch amp_dbg = 1: no activation, 2: no conv), so
-the activation / conv split of a launch can be read off. Usage: python tools/amp_bench.py"""
+shapes (B = 32 clips x 10 s). Usage: python tools/amp_bench.py"""
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from svc_inference_pipeline_amd import _lib  # noqa: E402
 from svc_inference_pipeline_amd._lib import call, profile_enable, profile_read  # noqa: E402
 
 SHAPES = [(48, 119936), (24, 239872)]
@@ -27,8 +25,7 @@ def main():
             w = torch.randn(C, C, k, device="cuda") * 0.05
             for d in ((1, 3, 5) if k > 1 else (1,)):
                 row = []
-                for mode in ("", "1", "2"):
-                    _lib.tune(None, amp_dbg=int(mode or 0))
+                for _rep in range(2):
                     args = (x.data_ptr(), B, L, C, al.data_ptr(), be.data_ptr(), f.data_ptr(), w.data_ptr(),
                             bias.data_ptr(), k, d, None, y.data_ptr(), s)
                     call("svc_op_amp_conv", *args)
@@ -40,9 +37,8 @@ def main():
                     p = {n: v for n, v in profile_read().items() if n.startswith("amp_conv")}
                     profile_enable(False)
                     us = 1000 * sum(v["ms"] for v in p.values()) / sum(v["launches"] for v in p.values())
-                    row.append(f"{['full', 'no-act', 'no-conv'][int(mode or 0)]} {us:7.1f} us")
+                    row.append(f"{us:7.1f} us")
                 print(f"C={C} L={L} k={k:2d} d={d}:", " | ".join(row), flush=True)
-        _lib.tune(None, amp_dbg=0)
         del x, y
 
 

@@ -1,6 +1,6 @@
 """Probe (GPU): PLMS-100 sampler (B = 32 x 937 frames) wall time and per kernel@site times (live HIP-event
 profiler) under kernel-switch settings given as JSON dicts on the command line, e.g.
-python tools/sampler_probe.py '{}' '{"sampler_streams": 1, "gemm4_rmw": 1}'"""
+python tools/sampler_probe.py '{}' '{"sampler_streams": 1}'"""
 import json
 import os
 import sys
