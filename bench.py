@@ -239,6 +239,9 @@ def main():
                          "(blocks 0-3), split-fp16 conv stem / HuBERT / DiffSVC head, the mode that meets the 1e-3 "
                          "mel-L1 target (tests/test_gpu_headline.py); split: every content GEMM on split-fp16 "
                          "operands; fp16: plain fp16 operands (faster, fails the target)")
+    ap.add_argument("--operands", choices=["fp16", "bf16"], default="fp16",
+                    help="16-bit MFMA operand format of the content encoder, conditioner and DiffSVC GEMMs (BigVGAN "
+                         "stays fp16); bf16 = BASELINE configs[4]'s variant, which does not meet the mel-L1 target")
     ap.add_argument("--wsplit-mlp", type=int, default=None,
                     help="wsplit: bit mask of the Whisper blocks whose MLP linears are weight-split (default 0xf; "
                          "16777215 = all 24, the round-2 default before the precision sweep)")
@@ -268,7 +271,8 @@ def main():
     eng = SVCEngine(cfg, dist.local_rank, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs,
                     content_split={"split": 1, "wsplit": 2, "fp16": 0}[args.precision],
                     head_split=args.precision != "fp16",
-                    config=None if args.wsplit_mlp is None else {"content.wsplit_mlp": args.wsplit_mlp})
+                    config=None if args.wsplit_mlp is None else {"content.wsplit_mlp": args.wsplit_mlp},
+                    operands=args.operands)
     fast = args.sampler == "plms"
     pipe = SVCPipeline(eng)
     B = args.batch
@@ -443,11 +447,11 @@ def main():
             "dist_world": dist.world, "backend": dist.backend or "none",
             "per_rank_ms_per_step": [round(1000.0 * t / args.steps, 2) for t in per_rank],
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp16", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.operands, "data": "synthetic",
             "config": {"workload": f"batch={B}/GPU x {args.seconds:g} s synthetic clips, "
                                    + ("Whisper-medium" if hs is None else "HuBERT/ContentVec (layer 9)")
                                    + (f" + PLMS-100 DiffSVC (speedup {args.speedup})" if fast else " + DDPM-1000 DiffSVC")
-                                   + " + BigVGAN, fp16 MFMA operands / fp32 accumulate"
+                                   + f" + BigVGAN, {args.operands} MFMA operands (BigVGAN fp16) / fp32 accumulate"
                                    + {"split": ", split-fp16 content encoder + DiffSVC head (mel-L1 <= 1e-3 mode)",
                                       "wsplit": ", weight-split Whisper attention linears (all blocks) + MLP linears "
                                                 "(blocks 0-3) + split-fp16 stem / DiffSVC head",

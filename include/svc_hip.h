@@ -58,7 +58,9 @@ svc_status svc_ctx_create(int device, svc_ctx** out);
 svc_status svc_ctx_destroy(svc_ctx* ctx);
 /* numeric configuration (config.json keys, flattened: "fs", "mapper.residual_layer_num", "vocoder.upsample_rates.0",
    ...; and the precision keys "content.split", "content.wsplit_attn" / _mlp / _qk / _v / _out, "mapper.head_split",
-   "hubert.output_layer"). An unknown key is SVC_ERR_INVALID (a misspelt key must not leave a default in place).
+   "operands.bf16" (1: the content encoders, conditioner and DiffSVC GEMMs take bfloat16 operands on
+   v_mfma_f32_16x16x32_bf16, and content features cross svc_map_content* / svc_condition as bfloat16; BigVGAN stays
+   fp16), "hubert.output_layer"). An unknown key is SVC_ERR_INVALID (a misspelt key must not leave a default in place).
    "tune.<name>" keys set a kernel switch of this context at any time (gemm_variant, gemm3_direct, whisper_streams,
    sampler_streams, vocoder_streams, diff_head, amp_maxc; "tune.reset" restores the creation-time values). Defaults
    are the measured production kernels; at creation an SVC_<NAME> environment variable overrides each. ctx may be

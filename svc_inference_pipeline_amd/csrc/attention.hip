@@ -1,6 +1,7 @@
 // Whisper encoder self-attention (non-causal, head dim 64) as a flash-style MFMA kernel for gfx950.
 // Restates MultiHeadAttention.qkv_attention (utils/whisper_extractor/model.py:88-101): q and k are
-// pre-scaled by dh^-1/4 in the QKV GEMM epilogue, softmax in f32, P rounded to f16 for P.V.
+// pre-scaled by dh^-1/4 in the QKV GEMM epilogue, q also by log2(e) (ATT_LOG2E), so the scores leave the MFMAs in
+// exp2 units; softmax in f32, P rounded to f16 for P.V.
 //
 // Layout: qkv f16 [B*L][3*D] (q | k | v, head h at columns h*64..h*64+63 of each third),
 // out f16 [B*L][D]. One workgroup = 4 waves = 128 queries of one (utterance, head); each wave owns
@@ -10,9 +11,11 @@
 // O^T = V^T P^T (k-order permuted). V stays row-major in LDS (one ds_write_b128 per 8 values, as K) and the V^T
 // A operand is read with gfx950's transposing ds_read_b64_tr_b16 (a 16-lane group reads 4 keys x 16 head columns and
 // each lane receives its column), from an image whose 16-B chunks are XOR-swizzled so those reads are conflict-free.
-// Softmax VALU work: the key mask only on the last tile, exp2 arguments as one FMA, the row max as a v_max3_f32 tree,
-// and the O rescale skipped when no lane of the wave raised its running max (alpha is then exactly 1 by
-// construction, so the result is unchanged). The kernel is VALU-issue bound (PMC: ~9.6 VALU instructions per MFMA, 0.30 MFMA busy).
+// Softmax VALU work per score: the score MFMAs accumulate onto -m (the running max as their C operand), so S - m
+// comes out of the matrix core and goes straight into v_exp_f32; the lane's max of S - m is a v_max3_f32 tree, and
+// only when some lane of the wave sees S - m > ATT_DEFER (rare after the first tile) is the running max moved: the
+// cross-lane column max, O / l rescaled, S - m shifted. The first tile sets m exactly; the key mask runs on the last
+// tile only. The kernel is VALU-issue bound (round 2 PMC: ~9.6 VALU instructions per MFMA, 0.30 MFMA busy).
 #include <type_traits>
 
 #include "common.h"
@@ -21,6 +24,7 @@ namespace svc {
 
 constexpr int ATT_QT = 128;   // queries per workgroup
 constexpr int ATT_KT = 64;    // keys per tile
+constexpr float ATT_DEFER = 8.0f * ATT_LOG2E;  // deferred-rescale threshold of the running max (exp2 units: e^8)
 
 __device__ __forceinline__ int kswz(int row, int kv) { return row * 64 + ((kv ^ ((row >> 1) & 7)) << 3); }
 // V image: [key][64 f16] rows, 16-B chunk c of row r stored at chunk c ^ (((r >> 1) & 3) << 1). A transposing read of
@@ -52,6 +56,7 @@ __device__ __forceinline__ float sum_xor32(float x) {
 __device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
 typedef short short4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef float float2v __attribute__((ext_vector_type(2)));
 typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 typedef _Float16 half4v __attribute__((ext_vector_type(4)));
@@ -59,8 +64,13 @@ __device__ __forceinline__ half4v lds_tr16(const f16* p) {
   return __builtin_bit_cast(half4v, __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) short4v*)p));
 }
 
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+// BF: q / k / v and the output are bfloat16 (the bf16 operand variant, Op16<true>), P is rounded to bf16
+template <bool BF>
 __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict__ qkv, f16* __restrict__ out, int L,
                                                            int D) {
+  using O = Op16<BF>;
   // double-buffered K / V^T tiles: tile kt + 1 is loaded into registers while tile kt is multiplied, then written to
   // the other buffer (one barrier per tile)
   __shared__ __align__(16) f16 Ksb[2][ATT_KT * 64];
@@ -94,31 +104,36 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
   for (int df = 0; df < 4; ++df)
 #pragma unroll
     for (int f = 0; f < 2; ++f) o[df][f] = (floatx4){0.f, 0.f, 0.f, 0.f};
-  float mrun[2] = {-INFINITY, -INFINITY}, lrun[2] = {0.f, 0.f};
-  const float LOG2E = 1.4426950408889634f;
+  // running max m (exp2 units; set exactly by the first tile), its negation as the score MFMAs' C operand, and the
+  // lane's share of the row sum
+  float mrun[2] = {0.f, 0.f}, lrun[2] = {0.f, 0.f};
+  floatx4 negm[2] = {(floatx4){0.f, 0.f, 0.f, 0.f}, (floatx4){0.f, 0.f, 0.f, 0.f}};
 
   const int ntiles = (L + ATT_KT - 1) / ATT_KT;
-  uint4 kreg[2], vreg[2];
+  u32x4 kreg[2], vreg[2];  // (a native vector type: the uint4 struct copies were kept in scratch)
+  // K / V rows of tile kt: a wave-uniform base (this utterance and head) plus a 32-bit per-lane byte offset, so the
+  // loads take the SGPR-base form. Keys past L (last tile only) load the last key's row: their scores are masked to
+  // -inf, so P = 0 multiplies a finite V row (no zero fill, no exec-masked branch around the loads).
+  const char* kbase = reinterpret_cast<const char*>(base + D + h * 64);
+  const char* vbase = reinterpret_cast<const char*>(base + 2 * D + h * 64);
+  const int krow = tid >> 3, kvv = tid & 7;  // vectors tid + 256 i: key row krow + 32 i, 16-B column chunk kvv
   auto gload = [&](int kt) {
+    const int k0 = kt * ATT_KT;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int v = tid + 256 * i;  // 512 vectors of 8 f16
-      const int row = v >> 3, kvv = v & 7;
-      const int key = kt * ATT_KT + row;
-      kreg[i] = vreg[i] = make_uint4(0, 0, 0, 0);
-      if (key < L) {
-        kreg[i] = *reinterpret_cast<const uint4*>(base + (int64_t)key * ld + D + h * 64 + kvv * 8);
-        vreg[i] = *reinterpret_cast<const uint4*>(base + (int64_t)key * ld + 2 * D + h * 64 + kvv * 8);
-      }
+      int key = k0 + krow + 32 * i;
+      if (k0 + ATT_KT > L) key = min(key, L - 1);
+      const uint32_t off = (uint32_t)(key * ld + kvv * 8) * 2u;
+      kreg[i] = *reinterpret_cast<const u32x4*>(kbase + off);
+      vreg[i] = *reinterpret_cast<const u32x4*>(vbase + off);
     }
   };
   auto lstore = [&](int buf) {  // K and V row-major (swizzled)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int v = tid + 256 * i;
-      const int row = v >> 3, kvv = v & 7;
-      *reinterpret_cast<uint4*>(Ksb[buf] + kswz(row, kvv)) = kreg[i];
-      *reinterpret_cast<uint4*>(Vsb[buf] + vswz(row, kvv)) = vreg[i];
+      const int row = krow + 32 * i;
+      *reinterpret_cast<u32x4*>(Ksb[buf] + kswz(row, kvv)) = kreg[i];
+      *reinterpret_cast<u32x4*>(Vsb[buf] + vswz(row, kvv)) = vreg[i];
     }
   };
   // transposing-read lane roles: lane 4q + p of its 16-lane group supplies key row q, head columns 4p .. 4p + 3
@@ -126,27 +141,24 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
   gload(0);
   lstore(0);
   __syncthreads();
-  // one 64-key tile; TAIL (the last tile only, peeled out of the loop) masks the keys past L, so the key compares are
-  // not computed (and hoisted) on every tile
-  auto key_tile = [&](int kt, auto tail_c) {
+  // one 64-key tile; FIRST (tile 0) sets the running max, TAIL (the last tile) masks the keys past L: both peeled out
+  // of the loop, so neither the exact max nor the key compares run on the other tiles
+  auto key_tile = [&](int kt, auto first_c, auto tail_c) {
+    constexpr bool FIRST = decltype(first_c)::value;
     constexpr bool TAIL = decltype(tail_c)::value;
     const int k0 = kt * ATT_KT;
     const f16* Ks = Ksb[kt & 1];
     const f16* Vs = Vsb[kt & 1];
     if (kt + 1 < ntiles) gload(kt + 1);  // lands while this tile is multiplied
 
-    // ---- S^T = K Q^T : s[kf][f][r] = S[q = f*16 + c16][key = kf*16 + 4g + r]
+    // ---- S^T - m = K Q^T - m : s[kf][f][r] = S[q = f*16 + c16][key = kf*16 + 4g + r] - m[q]
     floatx4 s[4][2];
 #pragma unroll
     for (int kf = 0; kf < 4; ++kf) {
+      const half8 k0f = *reinterpret_cast<const half8*>(Ks + kswz(kf * 16 + c16, g));
+      const half8 k1f = *reinterpret_cast<const half8*>(Ks + kswz(kf * 16 + c16, 4 + g));
 #pragma unroll
-      for (int f = 0; f < 2; ++f) s[kf][f] = (floatx4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        half8 kfrag = *reinterpret_cast<const half8*>(Ks + kswz(kf * 16 + c16, ks * 4 + g));
-#pragma unroll
-        for (int f = 0; f < 2; ++f) s[kf][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfrag, qf[f][ks], s[kf][f], 0, 0, 0);
-      }
+      for (int f = 0; f < 2; ++f) s[kf][f] = O::mfma(k1f, qf[f][1], O::mfma(k0f, qf[f][0], negm[f]));
     }
     // ---- online softmax per query column
     const bool tail = TAIL && k0 + ATT_KT > L;  // keys past L only in the last tile (wave-uniform)
@@ -160,39 +172,45 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
           for (int r = 0; r < 4; ++r)
             if (k0 + kf * 16 + 4 * g + r >= L) s[kf][f][r] = -INFINITY;
       }
-      // the lane's 16 scores of this query column: a v_max3_f32 tree (8 instructions instead of 16 v_max_f32)
-      float m4[4];
+      // the lane's max of its 16 scores: a v_max3_f32 tree (8 instructions)
+      const float x0 = max3f(s[0][f][0], s[0][f][1], s[0][f][2]), x1 = max3f(s[0][f][3], s[1][f][0], s[1][f][1]);
+      const float x2 = max3f(s[1][f][2], s[1][f][3], s[2][f][0]), x3 = max3f(s[2][f][1], s[2][f][2], s[2][f][3]);
+      const float x4 = max3f(s[3][f][0], s[3][f][1], s[3][f][2]);
+      const float mx = fmaxf(max3f(x0, x1, x2), max3f(x3, x4, s[3][f][3]));
+      // deferred rescale (cdna_hip_programming.md T13): after the first tile the running max moves only when some
+      // lane's S - m exceeds ATT_DEFER, so P = 2^(S - m) stays <= e^8 (2981, exact to f16's relative precision) and the
+      // cross-lane max, the O / l rescale and its v_exp run on a few tiles instead of every one
+      if (FIRST || __ballot(!(mx <= ATT_DEFER))) {
+        const float cm = max_xor32(max_xor16(mx));  // the column's max of S - m over the tile
+        const float d = FIRST ? cm : fmaxf(cm, 0.f);  // how far m moves (0: this column keeps its max)
+        if constexpr (!FIRST) {
+          const float alpha = __builtin_amdgcn_exp2f(-d);  // exactly 1 where d = 0
+          lrun[f] *= alpha;
 #pragma unroll
-      for (int kf = 0; kf < 4; ++kf) m4[kf] = fmaxf(max3f(s[kf][f][0], s[kf][f][1], s[kf][f][2]), s[kf][f][3]);
-      float mx = fmaxf(max3f(m4[0], m4[1], m4[2]), m4[3]);
-      mx = max_xor32(max_xor16(mx));
-      const float mnew = fmaxf(mrun[f], mx);
-      const float msc = mnew * LOG2E;
-      const bool grew = mnew != mrun[f];
-      // v_exp_f32 (arguments <= 0); exactly 1 where the max did not grow (exp2 of msc's rounding error otherwise is
-      // not), so the skipped O rescale below and the row sum's factor agree
-      const float alpha = grew ? __builtin_amdgcn_exp2f(fmaf(mrun[f], LOG2E, -msc)) : 1.0f;
-      mrun[f] = mnew;
-      // exponent arguments, row sum and f16 conversion on packed f32 pairs (v_pk_fma_f32, v_pk_add_f32,
-      // v_cvt_pk_f16_f32): half the VALU issue slots of the scalar forms; only v_exp_f32 stays per element
-      const float2v l2e = {LOG2E, LOG2E}, nm = {-msc, -msc};
-      float2v psum2 = {0.f, 0.f};
+          for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
+        }
+        mrun[f] += d;
+        negm[f] = (floatx4){-mrun[f], -mrun[f], -mrun[f], -mrun[f]};
+#pragma unroll
+        for (int kf = 0; kf < 4; ++kf) s[kf][f] -= d;
+      }
+      // P = 2^(S - m) straight from the accumulators; row sum and f16 conversion on packed f32 pairs
+      float2v psum2;
       half2v ph[4][2];
 #pragma unroll
       for (int kf = 0; kf < 4; ++kf)
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
-          float2v a = (float2v){s[kf][f][2 * hh], s[kf][f][2 * hh + 1]} * l2e + nm;
-          a.x = __builtin_amdgcn_exp2f(a.x);
-          a.y = __builtin_amdgcn_exp2f(a.y);
-          psum2 += a;
-          ph[kf][hh] = __builtin_convertvector(a, half2v);
+          float2v a;
+          a.x = __builtin_amdgcn_exp2f(s[kf][f][2 * hh]);
+          a.y = __builtin_amdgcn_exp2f(s[kf][f][2 * hh + 1]);
+          psum2 = kf == 0 && hh == 0 ? a : psum2 + a;
+          if constexpr (BF)
+            ph[kf][hh] = __builtin_bit_cast(half2v, __builtin_convertvector(a, bf16x2));
+          else
+            ph[kf][hh] = __builtin_convertvector(a, half2v);
         }
-      lrun[f] = lrun[f] * alpha + (psum2.x + psum2.y);
-      if (__ballot(grew)) {  // alpha == 1 exactly in every lane that did not raise its max
-#pragma unroll
-        for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
-      }
+      lrun[f] += psum2.x + psum2.y;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
         pb[f][ks] = (half8){ph[2 * ks][0].x, ph[2 * ks][0].y, ph[2 * ks][1].x, ph[2 * ks][1].y,
@@ -209,14 +227,19 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
         const half4v hi = lds_tr16(Vs + vswz(r0 + 16, c) + e);
         const half8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-        for (int f = 0; f < 2; ++f) o[df][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va, pb[f][ks], o[df][f], 0, 0, 0);
+        for (int f = 0; f < 2; ++f) o[df][f] = O::mfma(va, pb[f][ks], o[df][f]);
       }
     }
     if (kt + 1 < ntiles) lstore((kt + 1) & 1);  // that buffer was last read in iteration kt - 1, before its barrier
     __syncthreads();
   };
-  for (int kt = 0; kt + 1 < ntiles; ++kt) key_tile(kt, std::false_type{});
-  key_tile(ntiles - 1, std::true_type{});
+  if (ntiles == 1) {
+    key_tile(0, std::true_type{}, std::true_type{});
+  } else {
+    key_tile(0, std::true_type{}, std::false_type{});
+    for (int kt = 1; kt + 1 < ntiles; ++kt) key_tile(kt, std::false_type{}, std::false_type{});
+    key_tile(ntiles - 1, std::false_type{}, std::true_type{});
+  }
 
   // ---- normalise and store: lane holds O[q = f*16 + c16][d = df*16 + 4g + r]
 #pragma unroll
@@ -231,19 +254,22 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
     for (int df = 0; df < 4; ++df) {
       union { uint2 u; f16 e[4]; } pk;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pk.e[r] = (f16)(o[df][f][r] * inv);
+      for (int r = 0; r < 4; ++r) pk.e[r] = O::enc_lo(o[df][f][r] * inv);
       *reinterpret_cast<uint2*>(orow + df * 16 + 4 * g) = pk.u;
     }
   }
 }
 
-int attention(const f16* qkv, f16* out, int B, int L, int D, hipStream_t s) {
+int attention(const f16* qkv, f16* out, int B, int L, int D, hipStream_t s, bool bf16) {
   SVC_REQUIRE(D % 64 == 0 && L > 0 && B > 0, "attention: bad shape B=%d L=%d D=%d", B, L, D);
   const int64_t nwg = (int64_t)((L + ATT_QT - 1) / ATT_QT) * (D / 64) * B;
   SVC_REQUIRE(nwg < (1ll << 31), "attention: grid");
   dim3 grid((unsigned)nwg);
   const int tok = prof_begin("attention", 4.0 * B * (double)L * L * D, 0.0, s);
-  hipLaunchKernelGGL(attention_kernel, grid, dim3(256), 0, s, qkv, out, L, D);
+  if (bf16)
+    hipLaunchKernelGGL(attention_kernel<true>, grid, dim3(256), 0, s, qkv, out, L, D);
+  else
+    hipLaunchKernelGGL(attention_kernel<false>, grid, dim3(256), 0, s, qkv, out, L, D);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;

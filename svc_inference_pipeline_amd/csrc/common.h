@@ -95,6 +95,41 @@ __device__ __forceinline__ float gate_act(float a, float b) {
   return copysignf(r, b);
 }
 
+// ------------------------------------------------------------------ 16-bit MFMA operand formats
+// GEMM operands (activations and packed weights) are 16-bit values in f16-typed buffers: IEEE binary16 by default, or
+// bfloat16 bit patterns when a context runs its DiffSVC / content-encoder GEMMs in the bf16 operand variant (config
+// "operands.bf16", BASELINE configs[4]'s fp16-vs-bf16 sweep). Op16<BF> encodes / decodes them and picks the MFMA.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+template <bool BF>
+struct Op16;
+template <>
+struct Op16<false> {
+  static __device__ __forceinline__ float dec(f16 h) { return (float)h; }
+  static __device__ __forceinline__ f16 enc(float v) { return f16_sat(v); }  // saturating, NaN stays NaN
+  static __device__ __forceinline__ f16 enc_lo(float v) { return (f16)v; }  // low half of a split value
+  static __device__ __forceinline__ floatx4 mfma(half8 a, half8 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+template <>
+struct Op16<true> {
+  static __device__ __forceinline__ float dec(f16 h) {
+    return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, h) << 16);
+  }
+  static __device__ __forceinline__ f16 enc(float v) { return __builtin_bit_cast(f16, (__bf16)v); }  // RNE
+  static __device__ __forceinline__ f16 enc_lo(float v) { return __builtin_bit_cast(f16, (__bf16)v); }
+  static __device__ __forceinline__ floatx4 mfma(half8 a, half8 b, floatx4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
+};
+// runtime-format forms for the element-wise producers (a wave-uniform flag)
+__device__ __forceinline__ f16 enc16(float v, bool bf) { return bf ? Op16<true>::enc(v) : Op16<false>::enc(v); }
+__device__ __forceinline__ f16 enc16_lo(float v, bool bf) {
+  return bf ? Op16<true>::enc_lo(v) : Op16<false>::enc_lo(v);
+}
+__device__ __forceinline__ float dec16(f16 h, bool bf) { return bf ? Op16<true>::dec(h) : Op16<false>::dec(h); }
+
 // ------------------------------------------------------------------ implicit-GEMM descriptors
 // Y[m, n] = epilogue( sum_{tap, c} X[in_row(m, tap), c] * Wp[n, tap*Cp + c] )
 //   m = b*T_out + t  (b < B, t < T_out);   in_row = b*T_in + t*istride + tap*tap_mul + tap_add
@@ -116,6 +151,7 @@ struct ConvGemmArgs {
   // as zero, exactly the Conv1d zero padding of a clip of that length (its own rows keep the batch stride T_in)
   const int* tv;
   int tv_mul;
+  int bf16;      // operands (X, W) are bfloat16 (Op16<true>); the epilogue's 16-bit inputs / outputs too
 };
 
 __device__ __forceinline__ int valid_in_rows(const ConvGemmArgs& a, int b) {
@@ -131,6 +167,10 @@ enum EpiKind : int {
 
 enum ActKind : int { ACT_NONE = 0, ACT_GELU = 1, ACT_RELU = 2 };
 
+// The attention kernel takes q pre-multiplied by log2(e) (with its dh^-1/4 share of the score scale, in the QKV GEMM
+// epilogue), so its scores come out of the MFMAs in exp2 units
+constexpr float ATT_LOG2E = 1.4426950408889634f;
+
 struct EpiArgs {
   int kind;
   const float* bias;  // [Npad] packed order
@@ -142,7 +182,8 @@ struct EpiArgs {
   f16* out16; int ld16; const float* add16; // out16 = f16(v + add16[n])  (next-layer input)
   const float* add_t; int ld_add_t;         // added after act, indexed by t (positional embedding)
   const float* add_row; int ld_add_row;     // added after act, indexed by orow (residual input)
-  int scale_cols; float col_scale;          // columns < scale_cols multiplied by col_scale (q/k scaling)
+  int scale_cols; float col_scale;          // columns < scale_cols multiplied by col_scale (q/k scaling) ...
+  int scale_cols2; float col_scale2;        // ... except columns < scale_cols2 (<= scale_cols): by col_scale2 (q)
   // DiffSVC gate
   const f16* cp; int ld_cp;                 // conditioner projection (packed order, bias folded)
   f16* y16; int ldy16;                      // gate output sigmoid(gate) * tanh(filter), f16
@@ -225,6 +266,7 @@ struct PlmsArgs {
   const float* xin;  // x the update is applied to
   float* xout; f16* x16; int ld16;
   float* e_avg_out;  // optional: store e' (used for the first PLMS step's x_pred path)
+  int bf16;          // x16 holds bfloat16 operands (the bf16 variant)
 };
 // Kernel-selection switches: the measured production choices by default, other values select the earlier or
 // alternative kernel forms that the parity tests cover and the A/B benches compare (DESIGN.md records each result).

@@ -65,7 +65,9 @@ struct DiffHeadArgs {
   int ld_eps, n_out, M;
 };
 
+template <bool BF>
 __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, const f16* zpage) {
+  using O = Op16<BF>;  // operand format (binary16 or bfloat16)
   extern __shared__ __align__(16) unsigned char sm[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 6; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < 6; ++j) acc[i][j] = O::mfma(bf[j], af[i], acc[i][j]);
     __builtin_amdgcn_s_setprio(0);
   }
   // u = relu(acc + b_sp); hi = f16(u) goes to the LDS image, lo = f16(u - hi) stays in registers (packed, half the
@@ -157,8 +159,8 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
       DlH4 hi, lo;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        hi.h[r] = f16_sat(u[r]);
-        lo.h[r] = (f16)(u[r] - (float)hi.h[r]);
+        hi.h[r] = O::enc(u[r]);
+        lo.h[r] = O::enc_lo(u[r] - O::dec(hi.h[r]));
       }
       ulo[i][j] = lo.u;
       *reinterpret_cast<uint2*>(sm + DH_IMG + (n >> 7) * DL_GCHUNK + row * 256 + (dl_swg(row, (n & 127) >> 3) << 4) +
@@ -211,7 +213,7 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc2[i][j], 0, 0, 0);
+        acc2[i][j] = O::mfma(bf[j], af[i], acc2[i][j]);
     __builtin_amdgcn_s_setprio(0);
   }
   // ---- eps = acc + b_out, columns < n_out
@@ -231,7 +233,8 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
 }
 
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
-              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s) {
+              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
+              bool bf16) {
   SVC_REQUIRE(Nsp == DL_C && Ksp == 3 * DL_C && Kout == 3 * DL_C && Nout >= 1 && Nout <= 128 && Nout % 4 == 0 &&
                   Npad_out >= 128 && ld_eps % 4 == 0,
               "diff_head: shape (Nsp %d Ksp %d Nout %d Kout %d)", Nsp, Ksp, Nout, Kout);
@@ -240,16 +243,16 @@ int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp
   const int64_t grid = cdiv64(M, DL_BM);
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "diff_head: bad grid");
   DiffHeadArgs p{s16, Wsp, bsp, Wout, bout, eps, ld_eps, Nout, M};
-  static bool attr = false;
-  if (!attr) {
-    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)diff_head_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      DH_LDS));
-    attr = true;
+  const void* fn = bf16 ? (const void*)diff_head_kernel<true> : (const void*)diff_head_kernel<false>;
+  static bool attr[2] = {};
+  if (!attr[bf16]) {
+    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, DH_LDS));
+    attr[bf16] = true;
   }
   const double flops = 2.0 * M * (double)DL_C * 3 * DL_C + 2.0 * M * (double)Nout * 3 * DL_C;
   const int tok = prof_begin("diff_head<128>", flops, 0.0, s);
   void* args[] = {&p, const_cast<const f16**>(&zpage)};
-  SVC_HIP_CHECK(hipLaunchKernel((const void*)diff_head_kernel, dim3((unsigned)grid), dim3(DL_NT), args, DH_LDS, s));
+  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(DL_NT), args, DH_LDS, s));
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;

@@ -11,10 +11,11 @@ namespace svc {
 
 // ============================================================================ LayerNorm
 // utils/whisper_extractor/model.py:29-31 (LayerNorm in fp32), eps 1e-5, biased variance.
+// 16-bit outputs are GEMM operands: binary16, or bfloat16 bits when bf (the bf16 operand variant, common.h Op16)
 template <typename OutT, bool SPLIT = false>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, const float* __restrict__ gam,
                                                         const float* __restrict__ bet, OutT* __restrict__ y, int rows,
-                                                        int D, int ldy) {
+                                                        int D, int ldy, bool bf) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -47,10 +48,14 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     if (i < per) {
       int c = i * 64 + lane;
       const float o = (v[i] - mean) * rstd * gam[c] + bet[c];
-      yr[c] = (OutT)o;
-      if constexpr (SPLIT) {  // split-fp16 operand [hi | lo | hi] (ldy >= 3 D)
-        yr[D + c] = (OutT)(o - (float)yr[c]);
-        yr[2 * D + c] = yr[c];
+      if constexpr (std::is_same<OutT, float>::value) {
+        yr[c] = o;
+      } else {
+        yr[c] = enc16_lo(o, bf);
+        if constexpr (SPLIT) {  // split-fp16 operand [hi | lo | hi] (ldy >= 3 D)
+          yr[D + c] = enc16_lo(o - dec16(yr[c], bf), bf);
+          yr[2 * D + c] = yr[c];
+        }
       }
     }
 }
@@ -60,7 +65,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 template <typename OutT, bool SPLIT>
 __global__ __launch_bounds__(256) void layernorm_v4_kernel(const float* __restrict__ x, const float* __restrict__ gam,
                                                            const float* __restrict__ bet, OutT* __restrict__ y,
-                                                           int rows, int D, int ldy) {
+                                                           int rows, int D, int ldy, bool bf) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -102,35 +107,36 @@ __global__ __launch_bounds__(256) void layernorm_v4_kernel(const float* __restri
       }
       union { uint2 u; f16 h[4]; } hi, lo;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) hi.h[k] = (f16)o[k];
+      for (int k = 0; k < 4; ++k) hi.h[k] = enc16_lo(o[k], bf);
       *reinterpret_cast<uint2*>(yr + c) = hi.u;
       if constexpr (SPLIT) {  // split-fp16 operand [hi | lo | hi] (ldy >= 3 D)
 #pragma unroll
-        for (int k = 0; k < 4; ++k) lo.h[k] = (f16)(o[k] - (float)hi.h[k]);
+        for (int k = 0; k < 4; ++k) lo.h[k] = enc16_lo(o[k] - dec16(hi.h[k], bf), bf);
         *reinterpret_cast<uint2*>(yr + D + c) = lo.u;
         *reinterpret_cast<uint2*>(yr + 2 * D + c) = hi.u;
       }
     }
 }
 
-int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int rows, int D, int ldy, hipStream_t s) {
+int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int rows, int D, int ldy, hipStream_t s,
+                  bool bf) {
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm: D=%d", D);
   if (D % 256 == 0 && ldy % 4 == 0)
     hipLaunchKernelGGL((layernorm_v4_kernel<f16, false>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D,
-                       ldy);
+                       ldy, bf);
   else
-    hipLaunchKernelGGL(layernorm_kernel<f16>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy);
+    hipLaunchKernelGGL(layernorm_kernel<f16>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy, bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
-int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s) {
+int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s, bool bf) {
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm: D=%d", D);
   if (D % 256 == 0)
     hipLaunchKernelGGL((layernorm_v4_kernel<f16, true>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D,
-                       3 * D);
+                       3 * D, bf);
   else
     hipLaunchKernelGGL((layernorm_kernel<f16, true>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D,
-                       3 * D);
+                       3 * D, bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -138,9 +144,9 @@ int layernorm_f32(const float* x, const float* g, const float* b, float* y, int 
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm: D=%d", D);
   if (D % 256 == 0 && ldy % 4 == 0)
     hipLaunchKernelGGL((layernorm_v4_kernel<float, false>), dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D,
-                       ldy);
+                       ldy, false);
   else
-    hipLaunchKernelGGL(layernorm_kernel<float>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy);
+    hipLaunchKernelGGL(layernorm_kernel<float>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y, rows, D, ldy, false);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -149,17 +155,17 @@ int layernorm_f32(const float* x, const float* g, const float* b, float* y, int 
 
 // ============================================================================ conversions
 __global__ void f32_to_f16_kernel(const float* __restrict__ x, int ldx, f16* __restrict__ y, int ldy, int rows, int C,
-                                  int Cpad) {
+                                  int Cpad, bool bf) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t n = (int64_t)rows * Cpad;
   if (i >= n) return;
   int r = (int)(i / Cpad), c = (int)(i - (int64_t)r * Cpad);
-  y[(int64_t)r * ldy + c] = c < C ? f16_sat(x[(int64_t)r * ldx + c]) : (f16)0.0f;
+  y[(int64_t)r * ldy + c] = c < C ? enc16(x[(int64_t)r * ldx + c], bf) : (f16)0.0f;  // +0 in both formats
 }
 
-int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s) {
+int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s, bool bf) {
   int64_t n = (int64_t)rows * Cpad;
-  hipLaunchKernelGGL(f32_to_f16_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, x, ldx, y, ldy, rows, C, Cpad);
+  hipLaunchKernelGGL(f32_to_f16_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, x, ldx, y, ldy, rows, C, Cpad, bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -167,13 +173,14 @@ int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cp
 // Split-fp16 operand ("fp16x3"): x f32 [rows][ldx] -> y f16 [rows][3C] = [hi | lo | hi], hi = f16(x),
 // lo = f16(x - hi). A GEMM over these 3C columns against weights packed [W_hi; W_hi; W_lo] (pack_gemm_split3)
 // computes x_hi W_hi + x_lo W_hi + x_hi W_lo: ~19 significand bits instead of fp16's 11, at 3x the MFMA work.
-__global__ void f32_to_f16x3_kernel(const float* __restrict__ x, int ldx, f16* __restrict__ y, int rows, int C) {
+__global__ void f32_to_f16x3_kernel(const float* __restrict__ x, int ldx, f16* __restrict__ y, int rows, int C,
+                                    bool bf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)rows * C) return;
   const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
   const float v = x[(int64_t)r * ldx + c];
-  const f16 hi = f16_sat(v);
-  const f16 lo = (f16)(v - (float)hi);
+  const f16 hi = enc16(v, bf);
+  const f16 lo = enc16_lo(v - dec16(hi, bf), bf);
   f16* yr = y + (int64_t)r * 3 * C;
   yr[c] = hi;
   yr[C + c] = lo;
@@ -181,30 +188,32 @@ __global__ void f32_to_f16x3_kernel(const float* __restrict__ x, int ldx, f16* _
 }
 
 // grouped layout for grouped convolutions: group g's split operand is contiguous, [g][hi | lo | hi] of Cg columns
-__global__ void f32_to_f16x3_grouped_kernel(const float* __restrict__ x, f16* __restrict__ y, int rows, int C, int Cg) {
+__global__ void f32_to_f16x3_grouped_kernel(const float* __restrict__ x, f16* __restrict__ y, int rows, int C, int Cg,
+                                            bool bf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)rows * C) return;
   const int r = (int)(i / C), c = (int)(i - (int64_t)r * C);
   const int g = c / Cg, j = c - g * Cg;
   const float v = x[i];
-  const f16 hi = f16_sat(v);
+  const f16 hi = enc16(v, bf);
   f16* yg = y + (int64_t)r * 3 * C + (int64_t)g * 3 * Cg;
   yg[j] = hi;
-  yg[Cg + j] = (f16)(v - (float)hi);
+  yg[Cg + j] = enc16_lo(v - dec16(hi, bf), bf);
   yg[2 * Cg + j] = hi;
 }
 
-int f32_to_f16x3_grouped(const float* x, f16* y, int rows, int C, int Cg, hipStream_t s) {
+int f32_to_f16x3_grouped(const float* x, f16* y, int rows, int C, int Cg, hipStream_t s, bool bf) {
   SVC_REQUIRE(C % Cg == 0, "f16x3 grouped: C=%d Cg=%d", C, Cg);
   const int64_t n = (int64_t)rows * C;
-  hipLaunchKernelGGL(f32_to_f16x3_grouped_kernel, dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, y, rows, C, Cg);
+  hipLaunchKernelGGL(f32_to_f16x3_grouped_kernel, dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, y, rows, C, Cg,
+                     bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
 
-int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s) {
+int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s, bool bf) {
   const int64_t n = (int64_t)rows * C;
-  hipLaunchKernelGGL(f32_to_f16x3_kernel, dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, ldx, y, rows, C);
+  hipLaunchKernelGGL(f32_to_f16x3_kernel, dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, ldx, y, rows, C, bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -220,13 +229,14 @@ int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s) {
   return SVC_OK;
 }
 
-// q,k,v f32 [rows][D] -> f16 [rows][3D] with q,k scaled (the QKV GEMM epilogue's layout; op-level tests)
+// q,k,v f32 [rows][D] -> f16 [rows][3D] with q,k scaled and q also by log2(e) (the QKV GEMM epilogue's layout;
+// op-level tests)
 __global__ void pack_qkv_kernel(const float* q, const float* k, const float* v, f16* o, int64_t rows, int D, float sc) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= rows * D) return;
   int64_t r = i / D;
   int c = (int)(i - r * D);
-  o[r * 3 * D + c] = (f16)(q[i] * sc);
+  o[r * 3 * D + c] = (f16)(q[i] * (sc * ATT_LOG2E));
   o[r * 3 * D + D + c] = (f16)(k[i] * sc);
   o[r * 3 * D + 2 * D + c] = (f16)v[i];
 }
@@ -264,7 +274,7 @@ int denorm_mel(const float* x, f16* y, float* y32, int ldy, int rows, int C, con
 // utils/whisper.py:31-81: 15:8 repeat/average. Row j of the output averages the 8 repeated rows
 // 8j..8j+7 of np.repeat(raw, 15): source rows (8j+i)//15, summed sequentially in f32 then /8.
 __global__ void content_map_kernel(const float* __restrict__ src, int src_rows_per_utt, int ld_src,
-                                   f16* __restrict__ dst, int ld_dst, int T, int D, int n_down) {
+                                   f16* __restrict__ dst, int ld_dst, int T, int D, int n_down, bool bf) {
   const int jo = blockIdx.x;  // output frame
   const int j = min(jo, n_down - 1);  // HuBERT: frames past the mapped length repeat the last one
   const int b = blockIdx.y;
@@ -273,14 +283,15 @@ __global__ void content_map_kernel(const float* __restrict__ src, int src_rows_p
     float acc = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc += sb[(int64_t)((8 * j + i) / 15) * ld_src + c];
-    dst[((int64_t)b * T + jo) * ld_dst + c] = (f16)(acc / 8.0f);
+    dst[((int64_t)b * T + jo) * ld_dst + c] = enc16_lo(acc / 8.0f, bf);
   }
 }
 
-int content_map(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst, hipStream_t s) {
+int content_map(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst, hipStream_t s,
+                bool bf) {
   // the reference caps the target at 2812 frames (utils/whisper.py:56); longer clips are chunked by the host
   SVC_REQUIRE(T >= 1 && T <= 2812 && (T * 8 / 15 + 1) <= src_rows, "content_map: T=%d src_rows=%d", T, src_rows);
-  hipLaunchKernelGGL(content_map_kernel, dim3(T, B), dim3(256), 0, s, src, src_rows, ld_src, dst, ld_dst, T, D, T);
+  hipLaunchKernelGGL(content_map_kernel, dim3(T, B), dim3(256), 0, s, src, src_rows, ld_src, dst, ld_dst, T, D, T, bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -289,12 +300,13 @@ int content_map(const float* src, int B, int src_rows, int ld_src, int T, int D,
 // n_down = src_rows*15//8 mapped frames, at most 3 missing frames repeat the last one, and a larger
 // mismatch is an error (the reference calls exit()).
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
-                       hipStream_t s) {
+                       hipStream_t s, bool bf) {
   const int n_down = (int)((int64_t)src_rows * 15 / 8);
   SVC_REQUIRE(T >= 1 && src_rows >= 1 && n_down >= 1 && std::abs(T - n_down) <= 3,
               "content_map_hubert: %d content frames map to %d rows but T=%d (|diff| > 3; utils/hubert.py:114-120)",
               src_rows, n_down, T);
-  hipLaunchKernelGGL(content_map_kernel, dim3(T, B), dim3(256), 0, s, src, src_rows, ld_src, dst, ld_dst, T, D, n_down);
+  hipLaunchKernelGGL(content_map_kernel, dim3(T, B), dim3(256), 0, s, src, src_rows, ld_src, dst, ld_dst, T, D, n_down,
+                     bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -355,7 +367,7 @@ __global__ void plms_kernel(PlmsArgs p, int rows, int C) {
   if (p.x16) {
     int64_t r = i / C;
     int c = (int)(i - r * C);
-    p.x16[r * p.ld16 + c] = f16_sat(xn);
+    p.x16[r * p.ld16 + c] = enc16(xn, p.bf16);
   }
 }
 
@@ -390,7 +402,8 @@ __global__ void plms4_kernel(PlmsArgs p, int rows, int C) {
     const int64_t r = i4 / C4;
     const int c = (int)(i4 - r * C4) * 4;
     union { uint2 u; f16 h[4]; } pk;
-    pk.h[0] = f16_sat(xn.x); pk.h[1] = f16_sat(xn.y); pk.h[2] = f16_sat(xn.z); pk.h[3] = f16_sat(xn.w);
+    const bool bf = p.bf16;
+    pk.h[0] = enc16(xn.x, bf); pk.h[1] = enc16(xn.y, bf); pk.h[2] = enc16(xn.z, bf); pk.h[3] = enc16(xn.w, bf);
     *reinterpret_cast<uint2*>(p.x16 + r * p.ld16 + c) = pk.u;
   }
 }
@@ -436,7 +449,7 @@ __device__ __forceinline__ float philox_normal(uint64_t seed, uint32_t utt, uint
 
 // x_T ~ N(0, (1/1.2)^2) generated on device (modules/diffsvcrepo_inference.py:208-214)
 __global__ void init_noise_kernel(float* x, f16* x16, int ld16, int T, int C, uint64_t seed, const int* utt_ids,
-                                  int rows, float std) {
+                                  int rows, float std, bool bf) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (int64_t)rows * C) return;
   int64_t r = i / C;
@@ -444,15 +457,15 @@ __global__ void init_noise_kernel(float* x, f16* x16, int ld16, int T, int C, ui
   int b = (int)(r / T), t = (int)(r - (int64_t)b * T);
   float v = std * philox_normal(seed, (uint32_t)utt_ids[b], 0xFFFFFFFFu, (uint32_t)(t * C + c));
   x[i] = v;
-  x16[r * ld16 + c] = f16_sat(v);
+  x16[r * ld16 + c] = enc16(v, bf);
 }
 
 int init_noise(float* x, f16* x16, int ld16, int B, int T, int C, uint64_t seed, const int* utt_ids, float std,
-               hipStream_t s) {
+               hipStream_t s, bool bf) {
   int rows = B * T;
   int64_t n = (int64_t)rows * C;
   hipLaunchKernelGGL(init_noise_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, x, x16, ld16, T, C, seed, utt_ids, rows,
-                     std);
+                     std, bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -462,6 +475,7 @@ int init_noise(float* x, f16* x16, int ld16, int B, int T, int C, uint64_t seed,
 struct DdpmArgs {
   float sra, srm1, c1, c2, sigma;  // sigma = exp(0.5*logvar) * (t > 0)
   const float* z; uint64_t seed; const int* utt_ids; int step;
+  int bf16;  // x16 holds bfloat16 operands
 };
 
 __global__ void ddpm_kernel(float* x, const float* eps, f16* x16, int ld16, int T, int C, int rows, DdpmArgs a) {
@@ -483,7 +497,7 @@ __global__ void ddpm_kernel(float* x, const float* eps, f16* x16, int ld16, int 
   }
   float xn = mean + a.sigma * z;
   x[i] = xn;
-  x16[r * ld16 + c] = f16_sat(xn);
+  x16[r * ld16 + c] = enc16(xn, a.bf16);
 }
 
 int ddpm_update(float* x, const float* eps, f16* x16, int ld16, int B, int T, int C, const DdpmArgs& a, hipStream_t s) {

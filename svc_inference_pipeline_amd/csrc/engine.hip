@@ -73,46 +73,50 @@ void prof_end(int tok, hipStream_t s) {
 }
 
 // kernels in other translation units
-int attention(const f16* qkv, f16* out, int B, int L, int D, hipStream_t s);
-int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int rows, int D, int ldy, hipStream_t s);
+int attention(const f16* qkv, f16* out, int B, int L, int D, hipStream_t s, bool bf16);
+int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int rows, int D, int ldy, hipStream_t s,
+                  bool bf);
 int layernorm_f32(const float* x, const float* g, const float* b, float* y, int rows, int D, int ldy, hipStream_t s);
 int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const float* alpha_log, const float* beta_log,
                  const float* filt, hipStream_t s, const int* tv = nullptr, int tv_mul = 1);
-int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s);
+int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s, bool bf);
 int denorm_mel(const float* x, f16* y, float* y32, int ldy, int rows, int C, const float* mn, const float* mx,
                hipStream_t s);
-int content_map(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst, hipStream_t s);
+int content_map(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst, hipStream_t s,
+                bool bf);
 int bucketize(const double* f0, const float* en, const float* mbins, const float* ebins, int nb, int* im, int* ie,
               int n, hipStream_t s);
 int plms_update(const PlmsArgs& p, int rows, int C, hipStream_t s);
 struct DdpmArgs {
   float sra, srm1, c1, c2, sigma;
   const float* z; uint64_t seed; const int* utt_ids; int step;
+  int bf16;  // x16 holds bfloat16 operands
 };
 int ddpm_update(float* x, const float* eps, f16* x16, int ld16, int B, int T, int C, const DdpmArgs& a, hipStream_t s);
 int init_noise(float* x, f16* x16, int ld16, int B, int T, int C, uint64_t seed, const int* utt_ids, float std,
-               hipStream_t s);
+               hipStream_t s, bool bf);
 int conv_post(const f16* a, int lda, int B, int L, int C, const float* w, float bias, const float* fade, int nfade,
               float* out, hipStream_t s, const int* tv = nullptr, int tv_mul = 1);
 int zero_tail_rows(float* x, int B, int T, int C, const int* Tb, hipStream_t s);
 int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s,
-                      int split_c);
-int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s);
-int f32_to_f16x3_grouped(const float* x, f16* y, int rows, int C, int Cg, hipStream_t s);
+                      int split_c, bool bf);
+int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s, bool bf);
+int f32_to_f16x3_grouped(const float* x, f16* y, int rows, int C, int Cg, hipStream_t s, bool bf);
 int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
-int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s);
+int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s, bool bf);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
-              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s);
+              int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
+              bool bf16);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
-                       hipStream_t s);
-int hubert_frames5(const float* wav, int B, int64_t n, f16* out, bool split, hipStream_t s);
+                       hipStream_t s, bool bf);
+int hubert_frames5(const float* wav, int B, int64_t n, f16* out, bool split, hipStream_t s, bool bf);
 int groupnorm_gelu(const float* x, int B, int T, int C, const float* gamma, const float* beta, double* part,
-                   int max_chunks, float2* ss, f16* y, bool split, hipStream_t s);
+                   int max_chunks, float2* ss, f16* y, bool split, hipStream_t s, bool bf);
 int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f16* y16, int rows, int D, bool split,
-                   hipStream_t s);
+                   hipStream_t s, bool bf);
 int pack_qkv(const float* q, const float* k, const float* v, f16* qkv, int64_t rows, int D, float scale, hipStream_t s);
 int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double time_step, double floor_hz,
                 double ceiling_hz, double voicing, int T, double* f0_out, void* workspace, size_t ws_bytes,
@@ -229,7 +233,31 @@ struct PackedGemm {
   float* bias = nullptr;
   int N = 0, Npad = 0, K = 0, Kpad = 0, Cp = 0, Cin = 0, taps = 0;
   int tap_mul = 1, tap_add = 0, istride = 1;
+  bool bf16 = false;  // W (and so the GEMM's operands) in bfloat16 (the bf16 operand variant, common.h Op16)
 };
+
+// host-side rounding of a weight to the 16-bit operand format: binary16 (default) or bfloat16 (round to nearest even)
+static inline uint16_t bf16_bits(float v) {
+  uint32_t u;
+  memcpy(&u, &v, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static inline f16 enc16_host(float v, bool bf) {
+  if (!bf) return (f16)v;
+  const uint16_t b = bf16_bits(v);
+  f16 h;
+  memcpy(&h, &b, 2);
+  return h;
+}
+static inline float round16_host(float v, bool bf) {
+  if (!bf) return (float)(f16)v;
+  const uint32_t u = (uint32_t)bf16_bits(v) << 16;
+  float r;
+  memcpy(&r, &u, 4);
+  return r;
+}
 
 struct Param {
   const float* host = nullptr;
@@ -343,6 +371,11 @@ struct svc_ctx {
   bool content_split = false;  // content_mode == 1
   int content_mode = 0;         // "content.split": 0 fp16, 1 split-fp16 operands (x3), 2 weight-split (x2, Whisper)
   bool head_split = true;  // DiffSVC skip_projection / output_projection on split-fp16 operands ("mapper.head_split")
+  // bf16 operand variant ("operands.bf16" at finalize, BASELINE configs[4]'s fp16-vs-bf16 sweep): the DiffSVC,
+  // conditioner and content-encoder GEMMs (and Whisper / HuBERT attention) take bfloat16 operands on
+  // v_mfma_f32_16x16x32_bf16; BigVGAN stays binary16. pack_bf16: the weights being packed are for such a GEMM.
+  bool bf16 = false;
+  bool pack_bf16 = false;
   // whisper
   bool has_whisper = false;
   int wD = 0, wH = 0, wL = 0, wctx = 0, wmels = 80;
@@ -449,11 +482,13 @@ int pack_gemm(svc_ctx* c, PackedGemm& g, int N, int Cin, int Cp, int taps, WG wg
   g.K = taps * Cp;
   g.Kpad = (int)round_up(g.K, 64);
   g.Npad = (int)std::max(round_up(N, 256), round_up(N, 384));  // every conv_gemm2/3 tile width fits
-  std::vector<f16> w((size_t)g.Npad * g.Kpad, (f16)0.0f);
+  g.bf16 = c->pack_bf16;
+  std::vector<f16> w((size_t)g.Npad * g.Kpad, (f16)0.0f);  // +0 in both formats
   std::vector<float> b((size_t)g.Npad, 0.0f);
   for (int n = 0; n < N; ++n) {
     for (int t = 0; t < taps; ++t)
-      for (int ci = 0; ci < Cin; ++ci) w[(size_t)n * g.Kpad + (size_t)t * Cp + ci] = (f16)wget(n, ci, t);
+      for (int ci = 0; ci < Cin; ++ci)
+        w[(size_t)n * g.Kpad + (size_t)t * Cp + ci] = enc16_host(wget(n, ci, t), g.bf16);
     b[n] = bget(n);
   }
   int st = upload_vec(c, w, &g.W);
@@ -470,7 +505,7 @@ int pack_gemm_split3(svc_ctx* c, PackedGemm& g, int N, int Cin, WG wget, BG bget
       [&](int n, int ci, int t) {
         const int seg = ci / Cin;
         const float w = wget(n, ci - seg * Cin, t);
-        const float hi = (float)(f16)w;
+        const float hi = round16_host(w, c->pack_bf16);
         return seg < 2 ? hi : w - hi;
       },
       bget);
@@ -486,7 +521,7 @@ int pack_gemm_wsplit2(svc_ctx* c, PackedGemm& g, int N, int Cin, WG wget, BG bge
       c, g, N, Cin, Cin, 2,
       [&](int n, int ci, int t) {
         const float w = wget(n, ci, 0);
-        const float hi = (float)(f16)w;
+        const float hi = round16_host(w, c->pack_bf16);
         return t == 0 ? hi : w - hi;
       },
       bget);
@@ -621,6 +656,7 @@ static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cv
   a.B = B;
   a.T_out = T_out;
   a.N = g.N;
+  a.bf16 = g.bf16 ? 1 : 0;
   if (e.T_ostore == 0) {
     e.T_ostore = T_out;
     e.ostride = 1;
@@ -797,7 +833,7 @@ int build_hubert(svc_ctx* c) {
           if (ci >= 15) return 0.0f;
           const int seg = ci / 5;
           const float w = c0->host[(int64_t)n * 10 + t * 5 + (ci - seg * 5)];
-          const float hi = (float)(f16)w;
+          const float hi = round16_host(w, c->pack_bf16);
           return seg < 2 ? hi : w - hi;
         },
         [&](int) { return 0.0f; });
@@ -1321,7 +1357,7 @@ static bool known_config_key(const char* key) {
       "mapper.noise_schedule_factors.1", "mapper.head_split", "content.split", "content.wsplit_attn",
       "content.wsplit_mlp", "content.wsplit_qk", "content.wsplit_v", "content.wsplit_out", "hubert.output_layer",
       "vocoder.n_stages", "vocoder.n_kernels", "vocoder.upsample_initial_channel", "vocoder.input_dim",
-      "vocoder.resblock", "vocoder.snake", "vocoder.snake_logscale"};
+      "vocoder.resblock", "vocoder.snake", "vocoder.snake_logscale", "operands.bf16"};
   for (const char* k : exact)
     if (strcmp(key, k) == 0) return true;
   // indexed lists: <prefix><i> or, for the dilations, <prefix><j>.n / <prefix><j>.<l>
@@ -1413,9 +1449,12 @@ svc_status svc_ctx_finalize(svc_ctx* c) {
   SVC_REQUIRE(c->content_mode >= 0 && c->content_mode <= 2, "content.split %d: 0 fp16, 1 split-fp16, 2 weight-split",
               c->content_mode);
   c->content_split = c->content_mode == 1;
+  c->bf16 = cfgv(c, "operands.bf16", 0) != 0;
+  c->pack_bf16 = c->bf16;  // the content encoders, the conditioner and DiffSVC
   if (any_w && (st = build_whisper(c))) return st;
   if (any_h && (st = build_hubert(c))) return st;
   if (any_m && (st = build_mapper(c))) return st;
+  c->pack_bf16 = false;  // BigVGAN stays binary16
   if (any_v && (st = build_vocoder(c))) return st;
   c->params.clear();  // host arrays are no longer referenced
   c->finalized = true;
@@ -1650,7 +1689,7 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   a.n_mels = c->wmels;
   a.out = ls;
   if ((st = dft_mel(a, B, s))) return st;
-  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s, XS == 3 ? c->wmels : 0))) return st;
+  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s, XS == 3 ? c->wmels : 0, c->bf16))) return st;
   // conv stem
   WS_GET(f16, h1, rows1 * D * XS);
   EpiArgs e = epi();
@@ -1694,8 +1733,8 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
       f16* o16h = o16 + r * D;
       f16* h16h = h16 + r * 4 * D * X3;
       auto ln16 = [&](const float* g, const float* bb) {
-        return X3 == 3 ? layernorm_f16x3(xh, g, bb, n16h, (int)rows_h, D, hs)
-                       : layernorm_f16(xh, g, bb, n16h, (int)rows_h, D, D, hs);
+        return X3 == 3 ? layernorm_f16x3(xh, g, bb, n16h, (int)rows_h, D, hs, c->bf16)
+                       : layernorm_f16(xh, g, bb, n16h, (int)rows_h, D, D, hs, c->bf16);
       };
       if ((st = ln16(b.ln1_g, b.ln1_b))) return st;
       e = epi();
@@ -1703,6 +1742,8 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
       e.ld16 = 3 * D;
       e.scale_cols = 2 * D;
       e.col_scale = qk_scale;
+      e.scale_cols2 = D;  // q also carries log2(e): the attention kernel's scores are in exp2 units
+      e.col_scale2 = qk_scale * ATT_LOG2E;
       if ((st = run_gemm(b.qkv, n16h, D * X3, D * X3, Bh, L, L, e, hs, "whisper.qkv"))) return st;
       if (b.split_v) {
         e = epi();
@@ -1710,7 +1751,7 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
         e.ld16 = 3 * D;
         if ((st = run_gemm(b.v, n16h, D * X3, D * X3, Bh, L, L, e, hs, "whisper.v"))) return st;
       }
-      if ((st = attention(qkvh, o16h, Bh, L, D, hs))) return st;
+      if ((st = attention(qkvh, o16h, Bh, L, D, hs, c->bf16))) return st;
       e = epi();
       e.add_row = xh;
       e.ld_add_row = D;
@@ -1744,7 +1785,7 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
 svc_status svc_map_content(svc_ctx* c, const float* feats, int B, int src_rows, int T, int D, void* out, void* stream) {
   SVC_REQUIRE(c && feats && out, "map_content: null");
   SVC_HIP_CHECK(hipSetDevice(c->device));
-  return content_map(feats, B, src_rows, D, T, D, (f16*)out, D, (hipStream_t)stream);
+  return content_map(feats, B, src_rows, D, T, D, (f16*)out, D, (hipStream_t)stream, c->bf16);
 }
 
 svc_status svc_map_content_ex(svc_ctx* c, const float* feats, int B, int src_rows, int T, int D, int mode, void* out,
@@ -1752,8 +1793,8 @@ svc_status svc_map_content_ex(svc_ctx* c, const float* feats, int B, int src_row
   SVC_REQUIRE(c && feats && out && B > 0 && D > 0 && ld_out >= D, "map_content_ex: bad args");
   SVC_REQUIRE(mode == 0 || mode == 1, "map_content_ex: mode %d", mode);
   SVC_HIP_CHECK(hipSetDevice(c->device));
-  if (mode == 0) return content_map(feats, B, src_rows, D, T, D, (f16*)out, ld_out, (hipStream_t)stream);
-  return content_map_hubert(feats, B, src_rows, D, T, D, (f16*)out, ld_out, (hipStream_t)stream);
+  if (mode == 0) return content_map(feats, B, src_rows, D, T, D, (f16*)out, ld_out, (hipStream_t)stream, c->bf16);
+  return content_map_hubert(feats, B, src_rows, D, T, D, (f16*)out, ld_out, (hipStream_t)stream, c->bf16);
 }
 
 // ---------------------------------------------------------------------------- hubert / contentvec (A8)
@@ -1796,12 +1837,13 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
   WS_GET(f16, pb, (size_t)B * t[3] * Cc * X3);
   WS_GET(float, c6, rowsF * Cc);
   WS_GET(f16, ln16, rowsF * Cc * X3);
-  if ((st = hubert_frames5(wav16, B, n, f5, sp, s))) return st;
+  if ((st = hubert_frames5(wav16, B, n, f5, sp, s, c->bf16))) return st;
   EpiArgs e = epi();
   e.out32 = c0;
   e.ld32 = Cc;
   if ((st = run_gemm(c->hconv[0], f5, w5, w5, B, (int)R5, (int)t[1], e, s, "hubert.conv0"))) return st;
-  if ((st = groupnorm_gelu(c0, B, (int)t[1], Cc, c->hgn_g, c->hgn_b, part, kChunks, gss, g16, sp, s))) return st;
+  if ((st = groupnorm_gelu(c0, B, (int)t[1], Cc, c->hgn_g, c->hgn_b, part, kChunks, gss, g16, sp, s, c->bf16)))
+    return st;
   const f16* in = g16;
   for (int i = 1; i < 7; ++i) {
     e = epi();
@@ -1818,8 +1860,8 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
     in = e.out16;
   }
   // ---- HubertModel.forward_features tail: LayerNorm(C) -> post_extract_proj
-  if ((st = sp ? layernorm_f16x3(c6, c->hln_g, c->hln_b, ln16, (int)rowsF, Cc, s)
-               : layernorm_f16(c6, c->hln_g, c->hln_b, ln16, (int)rowsF, Cc, Cc, s)))
+  if ((st = sp ? layernorm_f16x3(c6, c->hln_g, c->hln_b, ln16, (int)rowsF, Cc, s, c->bf16)
+               : layernorm_f16(c6, c->hln_g, c->hln_b, ln16, (int)rowsF, Cc, Cc, s, c->bf16)))
     return st;
   WS_GET(float, x, rowsF * D);
   WS_GET(f16, x16, rowsF * D * X3);
@@ -1833,7 +1875,7 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
   if ((st = run_gemm(c->hproj, ln16, Cc * X3, Cc * X3, B, F, F, e, s, "hubert.proj"))) return st;
   // ---- TransformerEncoder: x += GELU(pos_conv(x)) per group, then LayerNorm (layer_norm_first = False)
   const int Cg = D / c->hPosG;
-  if (sp && (st = f32_to_f16x3_grouped(x, x16, (int)rowsF, D, Cg, s))) return st;  // group g: [hi | lo | hi] x Cg
+  if (sp && (st = f32_to_f16x3_grouped(x, x16, (int)rowsF, D, Cg, s, c->bf16))) return st;  // group g: [hi | lo | hi] x Cg
   for (int gi = 0; gi < c->hPosG; ++gi) {
     e = epi();
     e.act = ACT_GELU;
@@ -1844,7 +1886,7 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
     if ((st = run_gemm(c->hpos[gi], x16 + (size_t)gi * Cg * X3, D * X3, Cg * X3, B, F, F, e, s, "hubert.pos_conv")))
       return st;
   }
-  if ((st = layernorm_dual(x, c->henc_ln_g, c->henc_ln_b, x, x16, (int)rowsF, D, sp, s))) return st;
+  if ((st = layernorm_dual(x, c->henc_ln_g, c->henc_ln_b, x, x16, (int)rowsF, D, sp, s, c->bf16))) return st;
   WS_GET(f16, qkv, rowsF * 3 * D);
   WS_GET(f16, o16, rowsF * D);
   WS_GET(f16, h16, rowsF * Fd * X3);
@@ -1856,15 +1898,17 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
     e.ld16 = 3 * D;
     e.scale_cols = 2 * D;
     e.col_scale = qk_scale;
+    e.scale_cols2 = D;
+    e.col_scale2 = qk_scale * ATT_LOG2E;
     if ((st = run_gemm(b.qkv, x16, D * X3, D * X3, B, F, F, e, s, "hubert.qkv"))) return st;
-    if ((st = attention(qkv, o16, B, F, D, s))) return st;
+    if ((st = attention(qkv, o16, B, F, D, s, c->bf16))) return st;
     e = epi();
     e.add_row = x;
     e.ld_add_row = D;
     e.out32 = x;
     e.ld32 = D;
     if ((st = run_gemm(b.out, o16, D, D, B, F, F, e, s, "hubert.out"))) return st;
-    if ((st = layernorm_dual(x, b.ln1_g, b.ln1_b, x, x16, (int)rowsF, D, sp, s))) return st;
+    if ((st = layernorm_dual(x, b.ln1_g, b.ln1_b, x, x16, (int)rowsF, D, sp, s, c->bf16))) return st;
     e = epi();
     e.act = ACT_GELU;
     e.out16 = h16;
@@ -1877,7 +1921,7 @@ svc_status svc_hubert_encode(svc_ctx* c, const float* wav16, int B, int64_t n, f
     e.out32 = x;
     e.ld32 = D;
     if ((st = run_gemm(b.fc2, h16, Fd * X3, Fd * X3, B, F, F, e, s, "hubert.fc2"))) return st;
-    if ((st = layernorm_dual(x, b.ln2_g, b.ln2_b, x, x16, (int)rowsF, D, sp, s))) return st;
+    if ((st = layernorm_dual(x, b.ln2_g, b.ln2_b, x, x16, (int)rowsF, D, sp, s, c->bf16))) return st;
   }
   e = epi();
   e.out32 = feats;
@@ -2017,7 +2061,8 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
       c->skipproj.K == 3 * C && c->skipproj.Kpad == 3 * C && c->outproj.K == 3 * C && c->outproj.Kpad == 3 * C &&
       c->outproj.Npad >= 128 && c->outproj.N <= 128 && c->n_mel % 4 == 0) {
     if ((st = diff_head(bb.s16, c->skipproj.W, c->skipproj.bias, C, 3 * C, c->outproj.W, c->outproj.bias,
-                        c->outproj.N, 3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s)))
+                        c->outproj.N, 3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s,
+                        c->skipproj.bf16)))
       return st;
     return plms ? plms_update(*plms, rows, c->n_mel, s) : SVC_OK;
   }
@@ -2055,7 +2100,7 @@ static int project_cond(svc_ctx* c, const float* cond, int B, int T, const Denoi
   const int rows = B * T, C = c->C;
   WS_GET(f16, cond16, (size_t)rows * 3 * C);
   int st;
-  if ((st = f32_to_f16x3(cond, C, cond16, rows, C, s))) return st;  // [hi | lo | hi] split-fp16 operand
+  if ((st = f32_to_f16x3(cond, C, cond16, rows, C, s, c->bf16))) return st;  // [hi | lo | hi] split-fp16 operand
   // one GEMM per layer over that layer's rows of the packed weights, writing its layer-major cp block
   for (int l = 0; l < c->n_layers; ++l) {
     PackedGemm g = c->cp_all;
@@ -2101,7 +2146,7 @@ svc_status svc_diffsvc_eps(svc_ctx* c, const float* cond, const float* x, int B,
   if ((st = alloc_denoise(c, B, T, bb))) return st;
   if ((st = project_cond(c, cond, B, T, bb, s))) return st;
   WS_GET(f16, x16, (size_t)rows * ld16);
-  if ((st = f32_to_f16(x, c->n_mel, x16, ld16, rows, c->n_mel, ld16, s))) return st;
+  if ((st = f32_to_f16(x, c->n_mel, x16, ld16, rows, c->n_mel, ld16, s, c->bf16))) return st;
   if ((st = denoise(c, bb, x16, B, T, t, eps, s, tv))) return st;
   return tv ? zero_tail_rows(eps, B, T, c->n_mel, tv, s) : SVC_OK;
 }
@@ -2146,9 +2191,9 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
   SVC_HIP_CHECK(hipMemsetAsync(x16, 0, (size_t)rows * ld16 * sizeof(f16), s));  // zero pad channels
   if (x_T) {
     SVC_HIP_CHECK(hipMemcpyAsync(x, x_T, (size_t)rows * nm * 4, hipMemcpyDeviceToDevice, s));
-    if ((st = f32_to_f16(x, nm, x16, ld16, rows, nm, ld16, s))) return st;
+    if ((st = f32_to_f16(x, nm, x16, ld16, rows, nm, ld16, s, c->bf16))) return st;
   } else {
-    if ((st = init_noise(x, x16, ld16, B, T, nm, seed, utt_ids, 1.0f / 1.2f, s))) return st;
+    if ((st = init_noise(x, x16, ld16, B, T, nm, seed, utt_ids, 1.0f / 1.2f, s, c->bf16))) return st;
   }
   WS_GET(float, eps, (size_t)rows * nm);
   float* hist[5];
@@ -2212,6 +2257,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
         a.seed = seed;
         a.utt_ids = utt_ids ? utt_ids + u.b0 : nullptr;
         a.step = i;
+        a.bf16 = c->bf16;
         if ((st = ddpm_update(x + r * nm, eps + r * nm, x16 + r * ld16, ld16, u.B, T, nm, a, u.s))) return st;
       }
     }
@@ -2235,6 +2281,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
       const DenoiseBufs ub = sub_bufs(u);
       float* ecur = hist[head] + r * nm;
       PlmsArgs p{};
+      p.bf16 = c->bf16;
       p.d = d;
       p.A = A;
       p.Bc = Bc;
@@ -2548,7 +2595,7 @@ svc_status svc_op_conv1d(const float* x, int B, int T_in, int Cin, const float* 
   if ((st = c->ws.reserve(std::max((size_t)B * T_in * Cp * 2 + 4096, c->ws.cap)))) return st;
   c->ws.reset();
   WS_GET(f16, x16, (size_t)B * T_in * Cp);
-  if ((st = f32_to_f16(x, Cin, x16, Cp, B * T_in, Cin, Cp, s))) return st;
+  if ((st = f32_to_f16(x, Cin, x16, Cp, B * T_in, Cin, Cp, s, false))) return st;
   EpiArgs e = epi();
   e.act = act;
   e.out32 = y;
@@ -2602,7 +2649,7 @@ svc_status svc_op_conv_transpose1d(const float* x, int B, int T_in, int Cin, con
   if ((st = c->ws.reserve(std::max((size_t)B * T_in * Cin * 2 + 4096, c->ws.cap)))) return st;
   c->ws.reset();
   WS_GET(f16, x16, (size_t)B * T_in * Cin);
-  if ((st = f32_to_f16(x, Cin, x16, Cin, B * T_in, Cin, Cin, s))) return st;
+  if ((st = f32_to_f16(x, Cin, x16, Cin, B * T_in, Cin, Cin, s, false))) return st;
   for (int r = 0; r < stride && !st; ++r) {
     EpiArgs e = epi();
     e.T_ostore = T_out;
@@ -2645,7 +2692,7 @@ svc_status svc_op_attention(const float* q, const float* k, const float* v, int 
   WS_GET(f16, qkv, rows * 3 * D);
   WS_GET(f16, o16, rows * D);
   if ((st = pack_qkv(q, k, v, qkv, (int64_t)rows, D, powf(64.0f, -0.25f), s))) return st;
-  if ((st = attention(qkv, o16, B, L, D, s))) return st;
+  if ((st = attention(qkv, o16, B, L, D, s, false))) return st;
   return f16_to_f32(o16, out, (int64_t)rows * D, s);
 }
 

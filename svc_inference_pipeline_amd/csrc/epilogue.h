@@ -1,4 +1,4 @@
-// Shared GEMM epilogue (conv_gemm2 / conv_gemm3): applied to a BM x BNP pass of the f32 C tile staged
+// Shared GEMM epilogue (conv_gemm3 / conv_gemm4 LDS-staged forms): applied to a BM x BNP pass of the f32 C tile staged
 // in LDS (row stride LDC floats), on 4-column chunks with 16-byte vector loads/stores (coalesced rows).
 //   generic : v = act(acc + bias) (*col_scale) (+add_t) (+add_row) ((acc32 + v) / acc_div) -> out32 / out16
 //   COND    : acc + bias + emb_m[idx_m] + emb_l[idx_l] + emb_s[singer] (modules/encoder.py conditioner sum)
@@ -10,9 +10,10 @@
 
 namespace svc {
 
-template <int BM, int BNP, int LDC, int NT, bool PAIR>
+template <int BM, int BNP, int LDC, int NT, bool PAIR, bool BF = false>
 __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase, int M, const ConvGemmArgs& a,
                                               const EpiArgs& e, int tid) {
+  using O = Op16<BF>;
   if constexpr (!PAIR) {
     constexpr int CPR = BNP / 4;
     for (int idx = tid; idx < BM * CPR; idx += NT) {
@@ -39,7 +40,8 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
         if (n < e.scale_cols) {
-          v.x *= e.col_scale; v.y *= e.col_scale; v.z *= e.col_scale; v.w *= e.col_scale;
+          const float cs = n < e.scale_cols2 ? e.col_scale2 : e.col_scale;
+          v.x *= cs; v.y *= cs; v.z *= cs; v.w *= cs;
         }
         if (e.add_t) {
           const float4 at = *reinterpret_cast<const float4*>(e.add_t + (int64_t)t * e.ld_add_t + n);
@@ -58,8 +60,8 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
             hi.u = *reinterpret_cast<const uint2*>(e.acc16_hi + orow * e.ld_acc + n);
             lo.u = *reinterpret_cast<const uint2*>(e.acc16_lo + orow * e.ld_acc + n);
             const float4 sb = *reinterpret_cast<const float4*>(e.acc_sub + n);
-            ac.x = ((float)hi.h[0] + (float)lo.h[0]) - sb.x; ac.y = ((float)hi.h[1] + (float)lo.h[1]) - sb.y;
-            ac.z = ((float)hi.h[2] + (float)lo.h[2]) - sb.z; ac.w = ((float)hi.h[3] + (float)lo.h[3]) - sb.w;
+            ac.x = (O::dec(hi.h[0]) + O::dec(lo.h[0])) - sb.x; ac.y = (O::dec(hi.h[1]) + O::dec(lo.h[1])) - sb.y;
+            ac.z = (O::dec(hi.h[2]) + O::dec(lo.h[2])) - sb.z; ac.w = (O::dec(hi.h[3]) + O::dec(lo.h[3])) - sb.w;
           }
           v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
           if (e.acc_div != 1.0f) {
@@ -75,18 +77,18 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
           w.x += ad.x; w.y += ad.y; w.z += ad.z; w.w += ad.w;
         }
         union { uint2 u; f16 h[4]; } pk;
-        pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
+        pk.h[0] = O::enc(w.x); pk.h[1] = O::enc(w.y); pk.h[2] = O::enc(w.z); pk.h[3] = O::enc(w.w);
         *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
         if (e.lo16) {
           union { uint2 u; f16 h[4]; } lo;
-          lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);
-          lo.h[2] = (f16)(w.z - (float)pk.h[2]); lo.h[3] = (f16)(w.w - (float)pk.h[3]);
+          lo.h[0] = O::enc_lo(w.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(w.y - O::dec(pk.h[1]));
+          lo.h[2] = O::enc_lo(w.z - O::dec(pk.h[2])); lo.h[3] = O::enc_lo(w.w - O::dec(pk.h[3]));
           *reinterpret_cast<uint2*>(e.lo16 + orow * e.ld16 + n) = lo.u;
         }
         if (e.split16) {
           union { uint2 u; f16 h[4]; } lo;
-          lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);
-          lo.h[2] = (f16)(w.z - (float)pk.h[2]); lo.h[3] = (f16)(w.w - (float)pk.h[3]);
+          lo.h[0] = O::enc_lo(w.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(w.y - O::dec(pk.h[1]));
+          lo.h[2] = O::enc_lo(w.z - O::dec(pk.h[2])); lo.h[3] = O::enc_lo(w.w - O::dec(pk.h[3]));
           *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + e.split16 + n) = lo.u;
           *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + 2 * e.split16 + n) = pk.u;
         }
@@ -111,10 +113,10 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
       union { uint2 u; f16 h[4]; } pk, c1, c2;  // EPI_GATE
       c1.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n);
       c2.u = *reinterpret_cast<const uint2*>(e.cp + (int64_t)m * e.ld_cp + n + 32);
-      pk.h[0] = (f16)gate_act(v1.x + (float)c1.h[0], v2.x + (float)c2.h[0]);
-      pk.h[1] = (f16)gate_act(v1.y + (float)c1.h[1], v2.y + (float)c2.h[1]);
-      pk.h[2] = (f16)gate_act(v1.z + (float)c1.h[2], v2.z + (float)c2.h[2]);
-      pk.h[3] = (f16)gate_act(v1.w + (float)c1.h[3], v2.w + (float)c2.h[3]);
+      pk.h[0] = O::enc_lo(gate_act(v1.x + O::dec(c1.h[0]), v2.x + O::dec(c2.h[0])));
+      pk.h[1] = O::enc_lo(gate_act(v1.y + O::dec(c1.h[1]), v2.y + O::dec(c2.h[1])));
+      pk.h[2] = O::enc_lo(gate_act(v1.z + O::dec(c1.h[2]), v2.z + O::dec(c2.h[2])));
+      pk.h[3] = O::enc_lo(gate_act(v1.w + O::dec(c1.h[3]), v2.w + O::dec(c2.h[3])));
       *reinterpret_cast<uint2*>(e.y16 + (int64_t)m * e.ldy16 + ch) = pk.u;
     }
   }

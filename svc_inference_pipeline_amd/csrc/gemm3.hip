@@ -1,4 +1,5 @@
-// Third-generation implicit-GEMM Conv1d / Linear for gfx950: 8-wave ping-pong, v_mfma_f32_16x16x32_f16.
+// Third-generation implicit-GEMM Conv1d / Linear for gfx950: 8-wave ping-pong, v_mfma_f32_16x16x32_f16 (or _bf16 for
+// bfloat16 operands, ConvGemmArgs::bf16).
 //
 // Same operands and epilogues as conv_gemm2 (A = time-major f16 activations read through per-tap row
 // shifts, B = weights packed [Npad][Kpad], LDS images of 128-B rows with the 16-B chunk XOR swizzle
@@ -77,11 +78,12 @@ __device__ __forceinline__ int half_row(int i, int h, int Q, int W) { return (i 
 //   G3_SPLIT: acc + bias, ((acc16_hi + acc16_lo) - acc_sub + v) / acc_div -> out16 = hi(v + add16), lo16 = lo
 enum { G3_LDS = 0, G3_F16 = 1, G3_RES32 = 2, G3_SPLIT = 3 };
 
-template <int BM, int BN, bool CP64, bool PAIR, int FORM = G3_LDS>
+template <int BM, int BN, bool CP64, bool PAIR, int FORM = G3_LDS, bool BF = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage,
                                                            float inv_cp) {
   static_assert(FORM == G3_LDS || !PAIR, "register epilogues: generic epilogues only");
   using CF = G3<BM, BN>;
+  using O = Op16<BF>;  // operand format (binary16 or bfloat16)
   extern __shared__ __align__(16) unsigned char sm3[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -236,9 +238,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
 #pragma unroll
         for (int j = 0; j < CF::FQN; ++j)
           if constexpr (FORM != G3_LDS)  // C^T fragment: acc[..][i][j][r] = C[row fr of block i][col fk*4 + r of j]
-            acc[QMI][QNI][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j][s], af[i][s], acc[QMI][QNI][i][j], 0, 0, 0);
+            acc[QMI][QNI][i][j] = O::mfma(bf[j][s], af[i][s], acc[QMI][QNI][i][j]);
           else
-            acc[QMI][QNI][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][s], bf[j][s], acc[QMI][QNI][i][j], 0, 0, 0);
+            acc[QMI][QNI][i][j] = O::mfma(af[i][s], bf[j][s], acc[QMI][QNI][i][j]);
     __builtin_amdgcn_s_setprio(0);
     g3_barrier();
   };
@@ -321,16 +323,17 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
                 v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
               }
               if (n < e.scale_cols) {
-                v.x *= e.col_scale; v.y *= e.col_scale; v.z *= e.col_scale; v.w *= e.col_scale;
+                const float cs = n < e.scale_cols2 ? e.col_scale2 : e.col_scale;
+                v.x *= cs; v.y *= cs; v.z *= cs; v.w *= cs;
               }
               H4 pk;
-              pk.h[0] = f16_sat(v.x); pk.h[1] = f16_sat(v.y); pk.h[2] = f16_sat(v.z); pk.h[3] = f16_sat(v.w);
+              pk.h[0] = O::enc(v.x); pk.h[1] = O::enc(v.y); pk.h[2] = O::enc(v.z); pk.h[3] = O::enc(v.w);
               f16* o = e.out16 + orow * e.ld16 + n;
               *reinterpret_cast<uint2*>(o) = pk.u;
               if (e.split16) {
                 H4 lo;
-                lo.h[0] = (f16)(v.x - (float)pk.h[0]); lo.h[1] = (f16)(v.y - (float)pk.h[1]);
-                lo.h[2] = (f16)(v.z - (float)pk.h[2]); lo.h[3] = (f16)(v.w - (float)pk.h[3]);
+                lo.h[0] = O::enc_lo(v.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(v.y - O::dec(pk.h[1]));
+                lo.h[2] = O::enc_lo(v.z - O::dec(pk.h[2])); lo.h[3] = O::enc_lo(v.w - O::dec(pk.h[3]));
                 *reinterpret_cast<uint2*>(o + e.split16) = lo.u;
                 *reinterpret_cast<uint2*>(o + 2 * e.split16) = pk.u;
               }
@@ -347,10 +350,10 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
                 H4 hi, lo;
                 hi.u = make_uint2(__float_as_uint(pq[y][j].x), __float_as_uint(pq[y][j].y));
                 lo.u = make_uint2(__float_as_uint(pq[y][j].z), __float_as_uint(pq[y][j].w));
-                ac.x = ((float)hi.h[0] + (float)lo.h[0]) - cs[y][j].x;
-                ac.y = ((float)hi.h[1] + (float)lo.h[1]) - cs[y][j].y;
-                ac.z = ((float)hi.h[2] + (float)lo.h[2]) - cs[y][j].z;
-                ac.w = ((float)hi.h[3] + (float)lo.h[3]) - cs[y][j].w;
+                ac.x = (O::dec(hi.h[0]) + O::dec(lo.h[0])) - cs[y][j].x;
+                ac.y = (O::dec(hi.h[1]) + O::dec(lo.h[1])) - cs[y][j].y;
+                ac.z = (O::dec(hi.h[2]) + O::dec(lo.h[2])) - cs[y][j].z;
+                ac.w = (O::dec(hi.h[3]) + O::dec(lo.h[3])) - cs[y][j].w;
               } else {
                 has_acc = e.acc32 != nullptr;
                 if (has_acc) ac = pq[y][j];
@@ -370,12 +373,12 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
                   w.x += ca[y][j].x; w.y += ca[y][j].y; w.z += ca[y][j].z; w.w += ca[y][j].w;
                 }
                 H4 pk;
-                pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
+                pk.h[0] = O::enc(w.x); pk.h[1] = O::enc(w.y); pk.h[2] = O::enc(w.z); pk.h[3] = O::enc(w.w);
                 *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
                 if constexpr (FORM == G3_SPLIT) {
                   H4 lo;
-                  lo.h[0] = (f16)(w.x - (float)pk.h[0]); lo.h[1] = (f16)(w.y - (float)pk.h[1]);
-                  lo.h[2] = (f16)(w.z - (float)pk.h[2]); lo.h[3] = (f16)(w.w - (float)pk.h[3]);
+                  lo.h[0] = O::enc_lo(w.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(w.y - O::dec(pk.h[1]));
+                  lo.h[2] = O::enc_lo(w.z - O::dec(pk.h[2])); lo.h[3] = O::enc_lo(w.w - O::dec(pk.h[3]));
                   *reinterpret_cast<uint2*>(e.lo16 + orow * e.ld16 + n) = lo.u;
                 }
               }
@@ -407,7 +410,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
                    j * 16 + fr] = acc[x][y][i][j][r];
     }
     __syncthreads();
-    epilogue_pass<BM, BNP, LDC, CF::NT, PAIR>(Cs, m0, n0 + pass * BNP, M, a, e, tid);
+    epilogue_pass<BM, BNP, LDC, CF::NT, PAIR, BF>(Cs, m0, n0 + pass * BNP, M, a, e, tid);
     __syncthreads();
   }
 }
@@ -440,22 +443,25 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
   SVC_REQUIRE((int64_t)a.ntiles_n * BN <= std::max(round_up(a.N, 256), round_up(a.N, 384)),
               "conv_gemm3: weights not padded for BN=%d", BN);
   const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
-  const void* fns[2][4] = {
-      {(const void*)conv_gemm3_kernel<BM, BN, false, PAIR, G3_LDS>,
-       (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_F16>,
-       (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_RES32>,
-       (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_SPLIT>},
-      {(const void*)conv_gemm3_kernel<BM, BN, true, PAIR, G3_LDS>,
-       (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_F16>,
-       (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_RES32>,
-       (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_SPLIT>}};
-  const void* fn = fns[cp64][form];
+  const int bf = a.bf16 ? 1 : 0;
+#define G3_FORMS(BFV)                                                                                    \
+  {{(const void*)conv_gemm3_kernel<BM, BN, false, PAIR, G3_LDS, BFV>,                                    \
+    (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_F16, BFV>,                                   \
+    (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_RES32, BFV>,                                 \
+    (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_SPLIT, BFV>},                                \
+   {(const void*)conv_gemm3_kernel<BM, BN, true, PAIR, G3_LDS, BFV>,                                     \
+    (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_F16, BFV>,                                    \
+    (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_RES32, BFV>,                                  \
+    (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_SPLIT, BFV>}}
+  const void* fns[2][2][4] = {G3_FORMS(false), G3_FORMS(true)};
+#undef G3_FORMS
+  const void* fn = fns[bf][cp64][form];
   // the register forms need only the operand ring (no C staging)
   const int lds = form == G3_LDS ? CF::LDS : CF::RING;
-  static bool attr[2][4] = {};
-  if (!attr[cp64][form]) {
+  static bool attr[2][2][4] = {};
+  if (!attr[bf][cp64][form]) {
     SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    attr[cp64][form] = true;
+    attr[bf][cp64][form] = true;
   }
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
   const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);

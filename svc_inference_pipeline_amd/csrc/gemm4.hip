@@ -11,7 +11,6 @@
 //     epilogue runs beside the other's MFMAs (inter-workgroup overlap in place of intra-workgroup staggering);
 //   * the same operand images (128-B rows, 16-B chunk swizzle kv ^ (row & 6)), A loader (per-tap row shifts, zero
 //     rows outside the utterance) and LDS-staged vector epilogue (epilogue.h) as conv_gemm3.
-#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -28,6 +27,16 @@ __device__ __forceinline__ int sw4(int row, int kv) { return kv ^ (row & 6); }
 
 __device__ __forceinline__ void g4_dma(const void* src, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+// CP64 form: LDS-DMA through buffer descriptors. A lane's 32-bit voffset is fixed per conv tap (per K-tile for W) and
+// the K-tile's channel offset is the scalar soffset, so the K-loop issues its DMAs with no per-lane address arithmetic;
+// a padding row (outside its utterance) gets a voffset past the descriptor's range, which the hardware bounds check
+// turns into zeros.
+constexpr uint32_t G4_OOR = 0x7ffffff0u;
+__device__ __forceinline__ void g4_bdma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, unsigned char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, (int)soff,
+                                           0, 0);
 }
 
 template <int N>
@@ -56,10 +65,11 @@ __device__ __forceinline__ int g4_xcd_remap() {
 }
 
 // One 128 x 128 output tile (index wgid, N-tiles fastest) of the implicit GEMM, by the calling 256-thread workgroup.
-template <bool CP64, bool PAIR, bool DIRECT, int OPT = 0>
+template <bool CP64, bool PAIR, bool DIRECT, bool BF>
 __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage,
                                                 float inv_cp, int wgid, unsigned char* sm4) {
   static_assert(!DIRECT || PAIR, "the register epilogue is the gate's");
+  using O = Op16<BF>;  // operand format (binary16 or bfloat16)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -73,6 +83,7 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
   int a_t[4], a_kv[4], a_tin[4];
   const f16* a_p[4];
   const f16* b_p[4];
+  uint32_t a_row[4], a_voff[4], b_voff[4];  // CP64: byte offsets of the lane's A row (tap shift 0) / W row
 #pragma unroll
   for (int v = 0; v < 4; ++v) {
     const int row = (wave * 4 + v) * 8 + (lane >> 3);
@@ -84,51 +95,44 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
       a_t[v] = t * a.istride;
       a_tin[v] = valid_in_rows(a, b);
       a_p[v] = a.X + (int64_t)b * a.T_in * a.ldx + kv * 8;
+      a_row[v] = (uint32_t)(((b * a.T_in + a_t[v]) * a.ldx + kv * 8) * 2);
     } else {
       a_t[v] = -(1 << 29);
       a_tin[v] = 0;
       a_p[v] = a.X;
+      a_row[v] = 0u;
     }
+    a_voff[v] = G4_OOR;
     b_p[v] = a.W + (int64_t)(n0 + row) * a.Kpad + kv * 8;
+    b_voff[v] = (uint32_t)(((n0 + row) * a.Kpad + kv * 8) * 2);
   }
-  // (experiment OPT & 1) interior tiles: all 128 rows in one utterance; a K-tile whose tap shift keeps every row's
-  // source inside it needs no per-lane validity select (wave-uniform test per K-tile)
-  const f16* a_base[4];
-#pragma unroll
-  for (int v = 0; v < 4; ++v) a_base[v] = a_p[v] + (int64_t)a_t[v] * a.ldx;
-  int i_lo = 1, i_hi = 0;  // interior K-tiles need i_lo <= shift < i_hi
-  {
-    const int b0 = m0 / a.T_out, t0 = m0 - b0 * a.T_out;
-    if (m0 + G4_BM <= M && t0 + G4_BM <= a.T_out) {
-      const int tin = valid_in_rows(a, b0);
-      i_lo = -t0 * a.istride;
-      i_hi = tin - (t0 + G4_BM - 1) * a.istride;
-    }
-    i_lo = __builtin_amdgcn_readfirstlane(i_lo);
-    i_hi = __builtin_amdgcn_readfirstlane(i_hi);
-  }
+  // CP64 descriptors (unused otherwise); extents checked on the host (< 1 GiB: no voffset + soffset wraps)
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.X), (short)0, a.B * a.T_in * a.ldx * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.W), (short)0, a.ntiles_n * G4_BN * a.Kpad * 2, 0x00020000);
   auto issue = [&](int kt) {
     unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
     unsigned char* Bm = A + G4_BM * 128;
-    const bool live = kt < nk;
     if constexpr (CP64) {
       const int kg = kt * 64;
       const int tap = kg / a.Cp;
       const int c0 = kg - tap * a.Cp;
-      const int shift = tap * a.tap_mul + a.tap_add;
-      const int64_t off = (int64_t)shift * a.ldx + c0;
-      if ((OPT & 1) && live && shift >= i_lo && shift < i_hi) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) g4_dma(a_base[v] + off, A + (wave * 4 + v) * 1024);
-      } else {
+      if (c0 == 0) {  // a new tap (wave-uniform): the rows it reads, and which of them are padding
+        const int shift = tap * a.tap_mul + a.tap_add;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           const int st = a_t[v] + shift;
-          const bool ok = live && st >= 0 && st < a_tin[v];
-          g4_dma(ok ? (const void*)(a_base[v] + off) : (const void*)zsrc, A + (wave * 4 + v) * 1024);
+          a_voff[v] = st >= 0 && st < a_tin[v] ? a_row[v] + (uint32_t)(shift * a.ldx * 2) : G4_OOR;
         }
       }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) g4_bdma(rx, a_voff[v], (uint32_t)(c0 * 2), A + (wave * 4 + v) * 1024);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) g4_bdma(rw, b_voff[v], (uint32_t)(kt * 128), Bm + (wave * 4 + v) * 1024);
+      return;
     } else {
+      const bool live = kt < nk;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int kg = kt * 64 + a_kv[v] * 8;
@@ -141,10 +145,10 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
         g4_dma(ok ? (const void*)(a_p[v] + (int64_t)st * a.ldx + (c - a_kv[v] * 8)) : (const void*)zsrc,
                A + (wave * 4 + v) * 1024);
       }
-    }
 #pragma unroll
-    for (int v = 0; v < 4; ++v)
-      g4_dma(live ? (const void*)(b_p[v] + kt * 64) : (const void*)zsrc, Bm + (wave * 4 + v) * 1024);
+      for (int v = 0; v < 4; ++v)
+        g4_dma(live ? (const void*)(b_p[v] + kt * 64) : (const void*)zsrc, Bm + (wave * 4 + v) * 1024);
+    }
   };
 
   floatx4 acc[4][4];
@@ -191,21 +195,6 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
   for (int kt = 0; kt < nk; ++kt) {
     g4_vmwait<0>();  // this wave's DMAs of stage kt have landed (nothing younger is outstanding)
     g4_barrier();    // ... and everyone's; stage (kt + 1) & 1 is free
-    const unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
-    const unsigned char* Bm = A + G4_BM * 128;
-    half8 af0[4], bf0[4];
-    if constexpr ((OPT & 2) != 0) {  // (experiment) this K-tile's first fragments before the next DMA issue
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = wm * 64 + i * 16 + fr;
-        af0[i] = *reinterpret_cast<const half8*>(A + row * 128 + (sw4(row, fk) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int row = wn * 64 + j * 16 + fr;
-        bf0[j] = *reinterpret_cast<const half8*>(Bm + row * 128 + (sw4(row, fk) << 4));
-      }
-    }
     if (kt + 1 < nk) issue(kt + 1);
     if constexpr (DIRECT) {
       if (kt + 1 == nk) {  // under the last K-tile's MFMAs (spreading these over earlier K-steps measured no better)
@@ -215,23 +204,20 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
         prefetch(std::integral_constant<int, 3>{});
       }
     }
+    const unsigned char* A = sm4 + (kt & 1) * G4_STAGE;
+    const unsigned char* Bm = A + G4_BM * 128;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       half8 af[4], bf[4];
-      if ((OPT & 2) != 0 && s == 0) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) af[i] = af0[i], bf[i] = bf0[i];
-      } else {
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        af[i] = *reinterpret_cast<const half8*>(A + row * 128 + (sw4(row, s * 4 + fk) << 4));
+      }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = wm * 64 + i * 16 + fr;
-          af[i] = *reinterpret_cast<const half8*>(A + row * 128 + (sw4(row, s * 4 + fk) << 4));
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int row = wn * 64 + j * 16 + fr;
-          bf[j] = *reinterpret_cast<const half8*>(Bm + row * 128 + (sw4(row, s * 4 + fk) << 4));
-        }
+      for (int j = 0; j < 4; ++j) {
+        const int row = wn * 64 + j * 16 + fr;
+        bf[j] = *reinterpret_cast<const half8*>(Bm + row * 128 + (sw4(row, s * 4 + fk) << 4));
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -239,9 +225,9 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if constexpr (DIRECT)  // C^T fragment: acc[i][j][r] = C[row fr of block i][col fk*4 + r of block j]
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+            acc[i][j] = O::mfma(bf[j], af[i], acc[i][j]);
           else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = O::mfma(af[i], bf[j], acc[i][j]);
         }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -273,10 +259,10 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
         const float4 f = make_float4(acc[i][j + 2][0] + bfl[j].x, acc[i][j + 2][1] + bfl[j].y,
                                      acc[i][j + 2][2] + bfl[j].z, acc[i][j + 2][3] + bfl[j].w);
         H4 pk;
-        pk.h[0] = (f16)gate_act(g.x + (float)cpg[i][j].h[0], f.x + (float)cpf[i][j].h[0]);
-        pk.h[1] = (f16)gate_act(g.y + (float)cpg[i][j].h[1], f.y + (float)cpf[i][j].h[1]);
-        pk.h[2] = (f16)gate_act(g.z + (float)cpg[i][j].h[2], f.z + (float)cpf[i][j].h[2]);
-        pk.h[3] = (f16)gate_act(g.w + (float)cpg[i][j].h[3], f.w + (float)cpf[i][j].h[3]);
+        pk.h[0] = O::enc_lo(gate_act(g.x + O::dec(cpg[i][j].h[0]), f.x + O::dec(cpf[i][j].h[0])));
+        pk.h[1] = O::enc_lo(gate_act(g.y + O::dec(cpg[i][j].h[1]), f.y + O::dec(cpf[i][j].h[1])));
+        pk.h[2] = O::enc_lo(gate_act(g.z + O::dec(cpg[i][j].h[2]), f.z + O::dec(cpf[i][j].h[2])));
+        pk.h[3] = O::enc_lo(gate_act(g.w + O::dec(cpg[i][j].h[3]), f.w + O::dec(cpf[i][j].h[3])));
         // 4 channels (8 B) per lane and row; a 16-B form (quad exchange between lanes fk, fk ^ 1) measured 2-3 % slower
         *reinterpret_cast<uint2*>(e.y16 + (int64_t)m * e.ldy16 + chb + j * 16) = pk.u;
       }
@@ -294,13 +280,13 @@ __device__ __forceinline__ void conv_gemm4_tile(const ConvGemmArgs& a, const Epi
 #pragma unroll
       for (int r = 0; r < 4; ++r) Cs[(wm * 64 + i * 16 + fk * 4 + r) * G4_LDC + wn * 64 + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
-  epilogue_pass<G4_BM, G4_BN, G4_LDC, G4_NT, PAIR>(Cs, m0, n0, M, a, e, tid);
+  epilogue_pass<G4_BM, G4_BN, G4_LDC, G4_NT, PAIR, BF>(Cs, m0, n0, M, a, e, tid);
 }
 
-template <bool CP64, bool PAIR, bool DIRECT, int OPT = 0>
+template <bool CP64, bool PAIR, bool DIRECT, bool BF>
 __global__ __launch_bounds__(256, 2) void conv_gemm4_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage, float inv_cp) {
   extern __shared__ __align__(16) unsigned char sm4[];
-  conv_gemm4_tile<CP64, PAIR, DIRECT, OPT>(a, e, zpage, inv_cp, g4_xcd_remap(), sm4);
+  conv_gemm4_tile<CP64, PAIR, DIRECT, BF>(a, e, zpage, inv_cp, g4_xcd_remap(), sm4);
 }
 
 // direct: the register gate epilogue (paired epilogues only), otherwise the LDS-staged epilogue_pass
@@ -314,29 +300,23 @@ int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipSt
   a.ntiles_n = cdiv(a.N, G4_BN);
   const int64_t grid = (int64_t)cdiv(M, G4_BM) * a.ntiles_n;
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm4: bad grid");
-  const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
+  // the buffer-descriptor (CP64) form: one tap per K-tile, and X / W extents addressable by 32-bit offsets
+  const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad && (int64_t)a.B * a.T_in * a.ldx * 2 < (1ll << 30) &&
+                    (int64_t)a.ntiles_n * G4_BN * a.Kpad * 2 < (1ll << 30);
   const bool direct = direct_gate && pair;
-  static bool attr[2][2][2] = {};
-  const void* fns[2][2][2] = {
-      {{(const void*)conv_gemm4_kernel<false, false, false>, nullptr},
-       {(const void*)conv_gemm4_kernel<false, true, false>, (const void*)conv_gemm4_kernel<false, true, true>}},
-      {{(const void*)conv_gemm4_kernel<true, false, false>, nullptr},
-       {(const void*)conv_gemm4_kernel<true, true, false>, (const void*)conv_gemm4_kernel<true, true, true>}}};
-  const void* fn = fns[cp64][pair][direct];
-  static const int xopt = getenv("SVC_X_G4") ? atoi(getenv("SVC_X_G4")) : 0;  // experiment
-  if (cp64 && pair && direct && xopt) {
-    const void* xf[4] = {nullptr, (const void*)conv_gemm4_kernel<true, true, true, 1>,
-                         (const void*)conv_gemm4_kernel<true, true, true, 2>,
-                         (const void*)conv_gemm4_kernel<true, true, true, 3>};
-    fn = xf[xopt & 3];
-    static bool xa[4] = {};
-    if (!xa[xopt & 3]) {
-      SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G4_LDS));
-      xa[xopt & 3] = true;
-    }
-  } else if (!attr[cp64][pair][direct]) {
+  const int bf = a.bf16 ? 1 : 0;
+#define G4_FORMS(BFV)                                                                                              \
+  {{{(const void*)conv_gemm4_kernel<false, false, false, BFV>, nullptr},                                           \
+    {(const void*)conv_gemm4_kernel<false, true, false, BFV>, (const void*)conv_gemm4_kernel<false, true, true, BFV>}}, \
+   {{(const void*)conv_gemm4_kernel<true, false, false, BFV>, nullptr},                                            \
+    {(const void*)conv_gemm4_kernel<true, true, false, BFV>, (const void*)conv_gemm4_kernel<true, true, true, BFV>}}}
+  const void* fns[2][2][2][2] = {G4_FORMS(false), G4_FORMS(true)};
+#undef G4_FORMS
+  const void* fn = fns[bf][cp64][pair][direct];
+  static bool attr[2][2][2][2] = {};
+  if (!attr[bf][cp64][pair][direct]) {
     SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G4_LDS));
-    attr[cp64][pair][direct] = true;
+    attr[bf][cp64][pair][direct] = true;
   }
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
   const char* tag = direct ? "conv_gemm4<128,128,gate>" : pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>";

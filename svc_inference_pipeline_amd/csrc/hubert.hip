@@ -15,7 +15,7 @@ namespace svc {
 
 // SPLIT: 16 halves per row = [hi(5) | lo(5) | hi(5) | 0] (split-fp16 operand of the split-packed conv_layers[0])
 template <bool SPLIT>
-__global__ void frames5_kernel(const float* __restrict__ wav, int64_t n, int64_t rows, f16* __restrict__ out) {
+__global__ void frames5_kernel(const float* __restrict__ wav, int64_t n, int64_t rows, f16* __restrict__ out, bool bf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one output row (8 or 16 halves)
   const int b = blockIdx.y;
   if (i >= rows) return;
@@ -28,10 +28,10 @@ __global__ void frames5_kernel(const float* __restrict__ wav, int64_t n, int64_t
   for (int j = 0; j < 5; ++j) {
     const int64_t k = 5 * i + j;
     const float v = k < n ? w[k] : 0.0f;
-    const f16 hi = (f16)v;
+    const f16 hi = enc16_lo(v, bf);
     pk.h[j] = hi;
     if constexpr (SPLIT) {
-      pk.h[5 + j] = (f16)(v - (float)hi);
+      pk.h[5 + j] = enc16_lo(v - dec16(hi, bf), bf);
       pk.h[10 + j] = hi;
     }
   }
@@ -39,12 +39,12 @@ __global__ void frames5_kernel(const float* __restrict__ wav, int64_t n, int64_t
   for (int q = 0; q < W / 8; ++q) *reinterpret_cast<uint4*>(out + ((int64_t)b * rows + i) * W + q * 8) = pk.u[q];
 }
 
-int hubert_frames5(const float* wav, int B, int64_t n, f16* out, bool split, hipStream_t s) {
+int hubert_frames5(const float* wav, int B, int64_t n, f16* out, bool split, hipStream_t s, bool bf) {
   const int64_t rows = cdiv64(n, 5);
   if (split)
-    hipLaunchKernelGGL(frames5_kernel<true>, dim3(cdiv(rows, 256), B), dim3(256), 0, s, wav, n, rows, out);
+    hipLaunchKernelGGL(frames5_kernel<true>, dim3(cdiv(rows, 256), B), dim3(256), 0, s, wav, n, rows, out, bf);
   else
-    hipLaunchKernelGGL(frames5_kernel<false>, dim3(cdiv(rows, 256), B), dim3(256), 0, s, wav, n, rows, out);
+    hipLaunchKernelGGL(frames5_kernel<false>, dim3(cdiv(rows, 256), B), dim3(256), 0, s, wav, n, rows, out, bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
@@ -97,7 +97,7 @@ __global__ void gn_finalize_kernel(const double* __restrict__ part, int nck, int
 
 template <bool SPLIT>
 __global__ void gn_gelu_apply_kernel(const float* __restrict__ x, const float2* __restrict__ ss, f16* __restrict__ y,
-                                     int64_t rows_per_utt, int C, int64_t nvec) {
+                                     int64_t rows_per_utt, int C, int64_t nvec, bool bf) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // one vector of 8 channels
   if (i >= nvec) return;
   const int cpr = C / 8;
@@ -112,8 +112,8 @@ __global__ void gn_gelu_apply_kernel(const float* __restrict__ x, const float2* 
   for (int j = 0; j < 8; ++j) {
     const float2 t = ss[(int64_t)b * C + c0 + j];
     const float o = gelu_erf(v[j] * t.x + t.y);
-    pk.h[j] = f16_sat(o);
-    lo.h[j] = (f16)(o - (float)pk.h[j]);
+    pk.h[j] = enc16(o, bf);
+    lo.h[j] = enc16_lo(o - dec16(pk.h[j], bf), bf);
   }
   if constexpr (SPLIT) {  // [hi | lo | hi] rows of 3 C
     f16* yr = y + row * 3 * C;
@@ -128,7 +128,7 @@ __global__ void gn_gelu_apply_kernel(const float* __restrict__ x, const float2* 
 // Fp32GroupNorm(C, C) + GELU over x f32 [B][T][C] -> y f16 [B][T][C]. part: >= B * chunks * C * 2 doubles,
 // ss: B * C float2.
 int groupnorm_gelu(const float* x, int B, int T, int C, const float* gamma, const float* beta, double* part,
-                   int max_chunks, float2* ss, f16* y, bool split, hipStream_t s) {
+                   int max_chunks, float2* ss, f16* y, bool split, hipStream_t s, bool bf) {
   SVC_REQUIRE(C % 8 == 0 && T > 0 && B > 0, "groupnorm: B=%d T=%d C=%d", B, T, C);
   const int chunks = std::max(1, std::min(max_chunks, cdiv(T, 256)));
   const int chunk = cdiv(T, chunks);
@@ -140,10 +140,10 @@ int groupnorm_gelu(const float* x, int B, int T, int C, const float* gamma, cons
   const int64_t nvec = (int64_t)B * T * C / 8;
   if (split)
     hipLaunchKernelGGL(gn_gelu_apply_kernel<true>, dim3((unsigned)cdiv64(nvec, 256)), dim3(256), 0, s, x, ss, y,
-                       (int64_t)T, C, nvec);
+                       (int64_t)T, C, nvec, bf);
   else
     hipLaunchKernelGGL(gn_gelu_apply_kernel<false>, dim3((unsigned)cdiv64(nvec, 256)), dim3(256), 0, s, x, ss, y,
-                       (int64_t)T, C, nvec);
+                       (int64_t)T, C, nvec, bf);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
@@ -154,7 +154,7 @@ int groupnorm_gelu(const float* x, int B, int T, int C, const float* gamma, cons
 template <bool SPLIT>
 __global__ __launch_bounds__(256) void layernorm_dual_kernel(const float* x, const float* __restrict__ gam,
                                                              const float* __restrict__ bet, float* y32,
-                                                             f16* __restrict__ y16, int rows, int D) {
+                                                             f16* __restrict__ y16, int rows, int D, bool bf) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -187,11 +187,11 @@ __global__ __launch_bounds__(256) void layernorm_dual_kernel(const float* x, con
       const int c = i * 64 + lane;
       const float o = (v[i] - mean) * rstd * gam[c] + bet[c];
       y32[(int64_t)row * D + c] = o;
-      const f16 hi = f16_sat(o);
+      const f16 hi = enc16(o, bf);
       if constexpr (SPLIT) {
         f16* yr = y16 + (int64_t)row * 3 * D;
         yr[c] = hi;
-        yr[D + c] = (f16)(o - (float)hi);
+        yr[D + c] = enc16_lo(o - dec16(hi, bf), bf);
         yr[2 * D + c] = hi;
       } else {
         y16[(int64_t)row * D + c] = hi;
@@ -200,12 +200,14 @@ __global__ __launch_bounds__(256) void layernorm_dual_kernel(const float* x, con
 }
 
 int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f16* y16, int rows, int D, bool split,
-                   hipStream_t s) {
+                   hipStream_t s, bool bf) {
   SVC_REQUIRE(D % 64 == 0 && D <= 1024, "layernorm_dual: D=%d", D);
   if (split)
-    hipLaunchKernelGGL(layernorm_dual_kernel<true>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y32, y16, rows, D);
+    hipLaunchKernelGGL(layernorm_dual_kernel<true>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y32, y16, rows, D,
+                       bf);
   else
-    hipLaunchKernelGGL(layernorm_dual_kernel<false>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y32, y16, rows, D);
+    hipLaunchKernelGGL(layernorm_dual_kernel<false>, dim3(cdiv(rows, 4)), dim3(256), 0, s, x, g, b, y32, y16, rows, D,
+                       bf);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

@@ -49,8 +49,8 @@ class SVCPipeline:
         self.f0_side = f0_side
 
     def content(self, wav16, T, wav16_float=None):
-        """Content features of every type in cfg.mapper.content_feature mapped to T mel frames -> f16
-        [B, T, sum of widths], the types' columns concatenated in ascending name order (the order in which the
+        """Content features of every type in cfg.mapper.content_feature mapped to T mel frames -> [B, T, sum of
+        widths] in the engine's content_dtype (f16, or bf16 with operands="bf16"), the types' columns concatenated in ascending name order (the order in which the
         native conditioner packs their ContentEncoder Linears). "whisper" runs Whisper on the int16-quantised
         16 kHz audio (utils/whisper.py:96-103); "contentvec" runs HuBERT/ContentVec on float 16 kHz audio
         (utils/hubert.py:137-143; `wav16_float`, defaulting to wav16)."""
@@ -61,7 +61,7 @@ class SVCPipeline:
             return self.whisper_content(wav16, T)
         widths = [int(m.input_content_dim[t]) for t in types]
         B = wav16.shape[0]
-        out = torch.empty(B, T, sum(widths), device=wav16.device, dtype=torch.float16)
+        out = torch.empty(B, T, sum(widths), device=wav16.device, dtype=e.content_dtype)
         col = 0
         for t, w in zip(types, widths):
             view = out[:, :, col:col + w]
@@ -89,7 +89,7 @@ class SVCPipeline:
         wins = w[:, :need].reshape(B * n_win, WHISPER_WINDOW).contiguous()
         feats = e.whisper_encode(wins)                      # [B*n_win, 1500, D]
         D = feats.shape[-1]
-        out = torch.empty(B, n_win * WINDOW_MEL_FRAMES, D, device=wav16.device, dtype=torch.float16)
+        out = torch.empty(B, n_win * WINDOW_MEL_FRAMES, D, device=wav16.device, dtype=e.content_dtype)
         full = e.map_content(feats, WINDOW_MEL_FRAMES)     # every window mapped to 2805 frames
         out.copy_(full.view(B, n_win * WINDOW_MEL_FRAMES, D))
         return out[:, :T].contiguous()
@@ -192,7 +192,7 @@ class SVCPipeline:
         widths = [int(m.input_content_dim[t]) for t in types]
         B = len(wavs16)
         dev = wavs16[0].device
-        out = torch.zeros(B, T, sum(widths), device=dev, dtype=torch.float16)
+        out = torch.zeros(B, T, sum(widths), device=dev, dtype=e.content_dtype)
         col = 0
         for t, w in zip(types, widths):
             if t == "whisper":

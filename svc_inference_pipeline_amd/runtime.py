@@ -94,12 +94,15 @@ class SVCEngine:
     bits, 3x the MFMA work); 2 (default) splits only the weights of Whisper's block linears ([x | x] x [W_hi; W_lo],
     2x, no extra activation bytes; the weight rounding is the larger share of their error) with the conv stem and
     HuBERT as in 1. `head_split` runs the DiffSVC head (skip_projection, output_projection) on split-fp16 operands,
-    the largest denoiser-side term left. `config`: further numeric svc_ctx_set_config keys, set before finalize
+    the largest denoiser-side term left. `operands`: "fp16" (default) or "bf16", the 16-bit format of the content
+    encoder, conditioner and DiffSVC GEMM operands (v_mfma_f32_16x16x32_f16 or _bf16; the split modes apply to either;
+    BigVGAN stays fp16) — BASELINE configs[4]'s fp16-vs-bf16 sweep (tools/precision_sweep.py --bf16).
+    `config`: further numeric svc_ctx_set_config keys, set before finalize
     (e.g. {"content.wsplit_mlp": 0xffffff} to weight-split the MLP linears of all 24 Whisper blocks; an unknown key
     raises)."""
 
     def __init__(self, cfg, device=0, whisper_state=None, mapper_state=None, vocoder_state=None, hubert_state=None,
-                 hubert_output_layer=9, content_split=2, head_split=True, config=None):
+                 hubert_output_layer=9, content_split=2, head_split=True, config=None, operands="fp16"):
         check_supported(cfg)
         _lib.load()
         self.cfg = cfg
@@ -115,6 +118,12 @@ class SVCEngine:
         # content_split: False / 0 = fp16, True / 1 = split-fp16 operands, 2 = weight-split Whisper linears
         _lib.call("svc_ctx_set_config", self._ctx, b"content.split", float(int(content_split)))
         _lib.call("svc_ctx_set_config", self._ctx, b"mapper.head_split", 1.0 if head_split else 0.0)
+        if operands not in ("fp16", "bf16"):
+            raise ValueError(f"operands {operands!r}: fp16 or bf16")
+        self.operands = operands
+        # the 16-bit format of content features (map_content's output, the conditioner's input)
+        self.content_dtype = torch.bfloat16 if operands == "bf16" else torch.float16
+        _lib.call("svc_ctx_set_config", self._ctx, b"operands.bf16", 1.0 if operands == "bf16" else 0.0)
         for k, v in (config or {}).items():  # further svc_ctx_set_config keys (e.g. "content.wsplit_mlp")
             _lib.call("svc_ctx_set_config", self._ctx, k.encode(), float(v))
         if whisper_state is not None:
@@ -223,13 +232,15 @@ class SVCEngine:
         return feats
 
     def map_content(self, feats, T, rule="whisper", out=None):
-        """15:8 repeat/average to mel frames -> f16 [B, T, D]. rule "whisper": utils/whisper.py:31-81 (T <= 2812);
-        rule "hubert": utils/hubert.py:83-134 (no cap, <= 3 missing frames repeat the last one, more is an
-        error). `out` may be a column slice [B, T, D] of a wider f16 buffer (concatenated content types)."""
+        """15:8 repeat/average to mel frames -> [B, T, D] in content_dtype (f16; bf16 with operands="bf16").
+        rule "whisper": utils/whisper.py:31-81 (T <= 2812); rule "hubert": utils/hubert.py:83-134 (no cap, <= 3
+        missing frames repeat the last one, more is an error). `out` may be a column slice [B, T, D] of a wider
+        buffer (concatenated content types)."""
         B, S, D = feats.shape
         if out is None:
-            out = torch.empty(B, T, D, device=feats.device, dtype=torch.float16)
+            out = torch.empty(B, T, D, device=feats.device, dtype=self.content_dtype)
         assert out.shape == (B, T, D) and out.stride(2) == 1 and out.stride(0) == T * out.stride(1)
+        assert out.dtype == self.content_dtype, f"map_content: out must be {self.content_dtype}"
         mode = {"whisper": 0, "hubert": 1}[rule]
         _lib.call("svc_map_content_ex", self._ctx, _ptr(feats.contiguous()), B, S, T, D, mode,
                   ctypes.c_void_p(out.data_ptr()), out.stride(1), _stream())
@@ -247,8 +258,11 @@ class SVCEngine:
         return feats
 
     def condition(self, content16, f0, energy, singer):
-        """EncoderFramework.forward (modules/encoder.py:165-201) -> cond f32 [B, T, C]."""
+        """EncoderFramework.forward (modules/encoder.py:165-201) -> cond f32 [B, T, C]. content16 in
+        content_dtype."""
         B, T, _ = content16.shape
+        if content16.dtype != self.content_dtype:
+            raise ValueError(f"condition: content must be {self.content_dtype}, got {content16.dtype}")
         cond = torch.empty(B, T, self.cfg.mapper.residual_channels, device=content16.device, dtype=torch.float32)
         singer = singer.to(torch.int32).contiguous()
         _lib.call("svc_condition", self._ctx, _ptr(content16), _ptr(f0.contiguous()), _ptr(energy.contiguous()),

@@ -408,3 +408,52 @@ def test_bigvgan_tamed_weights_tight(cfg, states, golden):
         assert d_hip < 2e-3 and d_hip < 1.2 * d_emu + 2e-4, (d_hip, d_emu)
     finally:
         e.close()
+
+
+@pytest.fixture(scope="module")
+def engine_bf16(cfg, states):
+    """The bf16 operand variant (content encoder, conditioner and DiffSVC GEMMs on v_mfma_f32_16x16x32_bf16), plain
+    operands (no split modes), so it compares with the oracle's all-bf16 operand rounding."""
+    e = SVCEngine(cfg, 0, whisper_state=states["whisper"], mapper_state=states["mapper"],
+                  vocoder_state=states["vocoder"], content_split=0, head_split=False, operands="bf16")
+    yield e
+    e.close()
+
+
+@pytest.mark.parametrize("B,T", [(1, 93), (3, 211)])
+def test_bf16_eps_vs_emulated_oracle(engine_bf16, engine, states, cfg, B, T):
+    """One denoiser call (gate GEMM, residual / skip / head GEMMs, hoisted conditioner projection) with bfloat16
+    operands: its distance from the fp32 oracle is that of the oracle with every operand rounded to bf16 (within 1.5x
+    + 1e-3; bf16 keeps 8 significand bits, so ~8x fp16's distance), and it is not the fp16 engine's result."""
+    rng = np.random.default_rng(B * 3 + T)
+    cond = rng.standard_normal((B, T, 384)).astype(np.float32)
+    x = rng.standard_normal((B, T, 100)).astype(np.float32)
+    table = W.step_embedding_table(1000)
+    t = torch.full((B,), 250, dtype=torch.long)
+    with torch.no_grad():
+        ref = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond), t,
+                                 table).numpy()
+        with OM.OperandRounding(torch.bfloat16, linear=True):
+            emu = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond), t,
+                                     table).numpy()
+    eps_bf = engine_bf16.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()
+    eps_h = engine.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()
+    d_bf, d_emu, d_h = rel_l2(eps_bf, ref), rel_l2(emu, ref), rel_l2(eps_h, ref)
+    assert np.isfinite(eps_bf).all()
+    assert d_bf <= 1.5 * d_emu + 1e-3, (d_bf, d_emu)
+    assert d_bf > 2 * d_h, (d_bf, d_h)  # really bf16 (fp16 is ~8x closer)
+
+
+def test_bf16_whisper_encoder_vs_emulated_oracle(engine_bf16, states, golden):
+    """The Whisper encoder (conv stem, LayerNorm operands, qkv / out / MLP GEMMs, attention with bf16 P) in the bf16
+    operand variant against the oracle with bf16 operand rounding: the same distance class from fp32."""
+    wav16 = golden("whisper_logmel")["wav16"]
+    feats = engine_bf16.whisper_encode(dev(wav16[None]))[0].cpu().numpy()
+    with torch.no_grad():
+        lm = OF.whisper_log_mel(torch.from_numpy(OF.pad_or_trim(wav16))[None])
+        ref = OM.whisper_encoder(states["whisper"], lm, TINY["n_audio_head"])[0].numpy()
+        with OM.OperandRounding(torch.bfloat16, linear=True):
+            emu = OM.whisper_encoder(states["whisper"], lm, TINY["n_audio_head"])[0].numpy()
+    d_bf, d_emu = rel_l2(feats, ref), rel_l2(emu, ref)
+    assert np.isfinite(feats).all()
+    assert d_bf <= 1.5 * d_emu + 1e-3, (d_bf, d_emu)

@@ -57,6 +57,7 @@ class _FakeEngine:
         self.calls = []
         import threading
         self.lock = threading.RLock()
+        self.content_dtype = torch.float16
 
     def mel_energy(self, w24, n_samples=None):
         self.calls.append(("mel", tuple(w24.shape), list(n_samples)))

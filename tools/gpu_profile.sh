@@ -25,13 +25,10 @@ import json, re, sys
 tag = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])["roofline"]["kernel"]
 m = re.match(r"conv_gemm3<(\d+),(\d+)(,pair)?>", tag)
 m4 = re.match(r"conv_gemm4<128,128(,pair|,gate)?>", tag)
-m5 = re.match(r"conv_gemm5<(\d)(,pair)?>", tag)
 if m:
     print(f"conv_gemm3_kernelILi{m[1]}ELi{m[2]}ELb.ELb{1 if m[3] else 0}E")
 elif m4:
     print(f"conv_gemm4_kernelILb.ELb{1 if m4[1] else 0}ELb{1 if m4[1] == ',gate' else 0}E")
-elif m5:
-    print(f"conv_gemm5_kernelILi{m5[1]}ELb.ELb{1 if m5[2] else 0}E")
 else:
     print(tag.split("<")[0])
 PY

@@ -19,10 +19,6 @@ import shutil
 import sys
 
 NAME_MAP = {
-    "conv_gemm_kernel<128, 128, true>": "conv_gemm<128,128,pair>",
-    "conv_gemm_kernel<128, 128, false>": "conv_gemm<128,128>",
-    "conv_gemm_kernel<256, 64, false>": "conv_gemm<256,64>",
-    "conv_gemm_kernel<256, 32, false>": "conv_gemm<256,32>",
     "attention_kernel": "attention",
     "activation1d_kernel": "activation1d",
 }
@@ -30,27 +26,18 @@ NAME_MAP = {
 
 def short(name):
     """Demangled kernel name -> the tag bench.py's live profile uses (libsvc_hip prof_begin names)."""
-    m = re.search(r"conv_gemm3_kernel<(\d+), (\d+), (true|false), (true|false)>", name)
+    m = re.search(r"conv_gemm3_kernel<(\d+), (\d+), (true|false), (true|false)", name)
     if m:
         return f"conv_gemm3<{m.group(1)},{m.group(2)}{',pair' if m.group(4) == 'true' else ''}>"
-    m = re.search(r"conv_gemm3_kernelILi(\d+)ELi(\d+)ELb([01])ELb([01])ELb0E", name)  # rocprof keeps these mangled
+    m = re.search(r"conv_gemm3_kernelILi(\d+)ELi(\d+)ELb([01])ELb([01])E", name)  # rocprof keeps these mangled
     if m:
         return f"conv_gemm3<{m.group(1)},{m.group(2)}{',pair' if m.group(4) == '1' else ''}>"
-    m = re.search(r"conv_gemm4_kernel<(true|false), (true|false), (true|false)>", name)
+    m = re.search(r"conv_gemm4_kernel<(true|false), (true|false), (true|false)", name)
     if m:
         return f"conv_gemm4<128,128{',gate' if m.group(3) == 'true' else ',pair' if m.group(2) == 'true' else ''}>"
     m = re.search(r"conv_gemm4_kernelILb([01])ELb([01])ELb([01])E", name)
     if m:
         return f"conv_gemm4<128,128{',gate' if m.group(3) == '1' else ',pair' if m.group(2) == '1' else ''}>"
-    m = re.search(r"conv_gemm5_kernel<(\d+), (true|false), (true|false)>", name)
-    if m:
-        return f"conv_gemm5<{m.group(1)}{',pair' if m.group(3) == 'true' else ''}>"
-    m = re.search(r"conv_gemm5_kernelILi(\d+)ELb([01])ELb([01])E", name)
-    if m:
-        return f"conv_gemm5<{m.group(1)}{',pair' if m.group(3) == '1' else ''}>"
-    m = re.search(r"conv_gemm2_kernel<(\d+), (\d+), \d+, \d+, (\d+), (true|false)>", name)
-    if m:
-        return f"conv_gemm2<{m.group(1)},{m.group(2)}{',pair' if m.group(4) == 'true' else ''}>"
     m = re.search(r"activation1d_rs_kernel", name)
     if m:
         return "activation1d"

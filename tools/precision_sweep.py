@@ -10,6 +10,8 @@ per-step noise:
                         that type (oracle.models.OperandRounding), fp32 accumulation — the operand precision a
                         bf16 build of the same kernels would have.
   gpu-fp16            : the actual HIP path (--gpu; needs an MI355X), through the C-ABI.
+  gpu-bf16            : the same kernels with bfloat16 operands on v_mfma_f32_16x16x32_bf16 (--gpu --bf16;
+                        SVCEngine(operands="bf16")), plain and in the default split modes.
 
 Metrics, per SURVEY.md §7.3: mel-L1 = mean |delta| of the de-normalised natural-log mel fed to the vocoder (the
 north-star target is <= 1e-3), plus the same in normalised units, the content features' and the waveform's
@@ -83,6 +85,8 @@ def main():
                          "(content.wsplit_attn / content.wsplit_mlp, bit i = block i; e.g. 16777215:0 = attention "
                          "linears of all 24 blocks, no MLP linear)")
     ap.add_argument("--seed", type=int, default=7, help="synthetic clip seed")
+    ap.add_argument("--bf16", action="store_true", help="with --gpu: the fp16-vs-bf16 operand sweep (BASELINE "
+                    "configs[4]): plain and default-mode fp16 against plain and default-mode bf16")
     args = ap.parse_args()
     torch.set_num_threads(args.threads)
     cfg = C.load_config()
@@ -125,6 +129,11 @@ def main():
                     ("gpu, split-fp16 DiffSVC head", False, True, None),
                     ("gpu, split-fp16 content encoder + DiffSVC head", True, True, None),
                     ("gpu, weight-split content linears + split-fp16 DiffSVC head (default)", 2, True, None)]
+        if args.bf16:
+            variants = [("gpu-fp16 (plain fp16 operands)", 0, False, None),
+                        ("gpu-fp16, default precision mode", 2, True, None),
+                        ("gpu-bf16 (plain bf16 operands)", 0, False, {"operands": "bf16"}),
+                        ("gpu-bf16, default precision mode (split bf16 operands)", 2, True, {"operands": "bf16"})]
         if args.wsplit_variants:
             variants = []
             for v in args.wsplit_variants.split(","):
@@ -136,8 +145,10 @@ def main():
                     name += f" (qk {f[2]:#x} v {f[3]:#x} out {f[4]:#x})"
                 variants.append((name + " + split-fp16 DiffSVC head", 2, True, extra))
         for name, split, head, extra in variants:
+            extra = dict(extra or {})
+            operands = extra.pop("operands", "fp16")
             e = SVCEngine(cfg, 0, whisper_state=ws, mapper_state=ms, vocoder_state=vs, hubert_state=hs,
-                          content_split=split, head_split=head, config=extra)
+                          content_split=split, head_split=head, config=extra or None, operands=operands)
             d = lambda a, t=torch.float32: torch.as_tensor(np.ascontiguousarray(a)).to(t).cuda()  # noqa: E731
             noise = np.stack([ON.step_noise(seed, i, 1, T) for i in reversed(range(1000))])
             pipe = SVCPipeline(e)
