@@ -18,8 +18,10 @@
 //     (write-after-read across the staggered groups) and retired (vmcnt + barrier) >= 1 phase before
 //     its first read; vmcnt(N) keeps the 3 youngest half-tiles in flight. Tiles past the end are
 //     dummy DMAs from the zero page so the counts stay uniform.
-//   * When Cp % 64 == 0 a K-tile lies inside one conv tap: the tap shift is wave-uniform and the
-//     A-operand address is a per-lane base plus a scalar offset (one compare + select per DMA).
+//   * When Cp % 64 == 0 (and X / W fit 32-bit offsets) a K-tile lies inside one conv tap: the DMAs go through buffer
+//     descriptors, each lane's 32-bit voffset fixed per tap (A; padding rows out of the descriptor's range, which the
+//     hardware bounds check turns into zeros) or per launch (B), the K-tile's channel offset the scalar soffset: no
+//     per-lane address arithmetic in the K-loop.
 //   (A tap-reuse form that staged a 64-channel chunk's A rows once for every tap moved ~40 % fewer operand bytes on
 //    the multi-tap convs yet ran 5-10 % slower; it was removed in round 3, DESIGN.md.)
 #include <cstdio>
@@ -66,6 +68,12 @@ __device__ __forceinline__ void g3_dma(const void* src, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
 }
 
+constexpr uint32_t G3_OOR = 0x7ffffff0u;  // a voffset past every descriptor's range: the DMA lands zeros
+__device__ __forceinline__ void g3_bdma(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, unsigned char* lds) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, (int)voff, (int)soff,
+                                           0, 0);
+}
+
 // row (within the A or B image) of element i of half-tile h, for a half made of blocks of Q rows
 // every W rows: rows w*W + h*Q + [0, Q)
 __device__ __forceinline__ int half_row(int i, int h, int Q, int W) { return (i / Q) * W + h * Q + (i % Q); }
@@ -102,6 +110,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   // LDS chunk lane & 7 holding logical k-chunk kv = sw3(row, lane & 7).
   int a_rb[2][CF::AH], a_kv[2][CF::AH], a_t[2][CF::AH], a_tin[2][CF::AH];
   const f16* a_p[2][CF::AH];
+  uint32_t a_row[2][CF::AH], a_voff[2][CF::AH];  // CP64: byte offset of the lane's A row at tap shift 0 / this tap
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -118,14 +127,18 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
         a_t[h][v] = t * a.istride;
         a_tin[h][v] = valid_in_rows(a, b);
         a_p[h][v] = a.X + (int64_t)b * a.T_in * a.ldx + kv * 8;
+        a_row[h][v] = (uint32_t)(((b * a.T_in + a_t[h][v]) * a.ldx + kv * 8) * 2);
       } else {
         a_t[h][v] = -(1 << 29);
         a_tin[h][v] = 0;
         a_p[h][v] = a.X;
+        a_row[h][v] = 0u;
       }
+      a_voff[h][v] = G3_OOR;
     }
   int b_rb[2][CF::BH];
   const f16* b_p[2][CF::BH];
+  uint32_t b_voff[2][CF::BH];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -135,25 +148,38 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
       const int row = rb + (lane >> 3);
       b_rb[h][v] = rb;
       b_p[h][v] = a.W + (int64_t)(n0 + row) * a.Kpad + sw3(row, lane & 7) * 8;
+      b_voff[h][v] = (uint32_t)(((n0 + row) * a.Kpad + sw3(row, lane & 7) * 8) * 2);
     }
+  // CP64 descriptors (unused otherwise); extents checked on the host (< 1 GiB: no voffset + soffset wraps)
+  const __amdgpu_buffer_rsrc_t rx =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.X), (short)0, a.B * a.T_in * a.ldx * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.W), (short)0, a.ntiles_n * BN * a.Kpad * 2, 0x00020000);
 
   auto a_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE; };
   auto b_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE + BM * 128; };
   auto issue_a = [&](int h, int kt) {
     unsigned char* dst = a_img(kt);
     if constexpr (CP64) {
-      // the whole K-tile lies in tap `tap`; columns c0 .. c0+63 of it
+      // the whole K-tile lies in tap `tap`; columns c0 .. c0+63 of it. Each half sees kt = 0, 1, 2, ... in order, so
+      // its voffsets are recomputed at the first K-tile of every tap; past the end (kt >= nk) the DMAs land zeros
       const int kg = kt * 64;
       const int tap = kg / a.Cp;  // wave-uniform
       const int c0 = kg - tap * a.Cp;
-      const int shift = tap * a.tap_mul + a.tap_add;
-      const int64_t off = (int64_t)shift * a.ldx + c0;
+      if (kt < nk) {
+        if (c0 == 0) {
+          const int shift = tap * a.tap_mul + a.tap_add;
 #pragma unroll
-      for (int v = 0; v < CF::AH; ++v) {
-        const int st = a_t[h][v] + shift;
-        const bool ok = kt < nk && st >= 0 && st < a_tin[h][v];
-        const f16* src = ok ? a_p[h][v] + (int64_t)a_t[h][v] * a.ldx + off : zsrc;
-        g3_dma(src, dst + a_rb[h][v] * 128);
+          for (int v = 0; v < CF::AH; ++v) {
+            const int st = a_t[h][v] + shift;
+            a_voff[h][v] = st >= 0 && st < a_tin[h][v] ? a_row[h][v] + (uint32_t)(shift * a.ldx * 2) : G3_OOR;
+          }
+        }
+#pragma unroll
+        for (int v = 0; v < CF::AH; ++v) g3_bdma(rx, a_voff[h][v], (uint32_t)(c0 * 2), dst + a_rb[h][v] * 128);
+      } else {
+#pragma unroll
+        for (int v = 0; v < CF::AH; ++v) g3_bdma(rx, G3_OOR, 0u, dst + a_rb[h][v] * 128);
       }
     } else {
 #pragma unroll
@@ -173,9 +199,16 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   };
   auto issue_b = [&](int h, int kt) {
     unsigned char* dst = b_img(kt);
-    const int koff = kt * 64;
+    if constexpr (CP64) {
 #pragma unroll
-    for (int v = 0; v < CF::BH; ++v) g3_dma(kt < nk ? (const void*)(b_p[h][v] + koff) : (const void*)zsrc, dst + b_rb[h][v] * 128);
+      for (int v = 0; v < CF::BH; ++v)
+        g3_bdma(rw, kt < nk ? b_voff[h][v] : G3_OOR, (uint32_t)(kt * 128), dst + b_rb[h][v] * 128);
+    } else {
+      const int koff = kt * 64;
+#pragma unroll
+      for (int v = 0; v < CF::BH; ++v)
+        g3_dma(kt < nk ? (const void*)(b_p[h][v] + koff) : (const void*)zsrc, dst + b_rb[h][v] * 128);
+    }
   };
 
   floatx4 acc[2][2][CF::FQM][CF::FQN];
@@ -442,7 +475,9 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "conv_gemm3: bad grid");
   SVC_REQUIRE((int64_t)a.ntiles_n * BN <= std::max(round_up(a.N, 256), round_up(a.N, 384)),
               "conv_gemm3: weights not padded for BN=%d", BN);
-  const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad;
+  // the buffer-descriptor (CP64) form: one tap per K-tile, and X / W extents addressable by 32-bit offsets
+  const bool cp64 = a.Cp % 64 == 0 && a.K == a.Kpad && (int64_t)a.B * a.T_in * a.ldx * 2 < (1ll << 30) &&
+                    (int64_t)a.ntiles_n * BN * a.Kpad * 2 < (1ll << 30);
   const int bf = a.bf16 ? 1 : 0;
 #define G3_FORMS(BFV)                                                                                    \
   {{(const void*)conv_gemm3_kernel<BM, BN, false, PAIR, G3_LDS, BFV>,                                    \
