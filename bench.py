@@ -405,6 +405,8 @@ def main():
         if ents:
             big = max(ents, key=lambda v: v["workgroups"])
             roof["mfma_busy_pmc"] = round(big["mfma_busy"], 3)
+            if "valu_per_mfma" in big:
+                roof["valu_per_mfma_pmc"] = round(big["valu_per_mfma"], 2)
             roof["mfma_busy_source"] = os.path.relpath(pmc_k, REPO) + f" ({big['workgroups']}-workgroup launches)"
     # the production sub-batch launches of the dominant call site (sampler_streams concurrent sub-batches): their
     # rocprof per-dispatch average from the committed trace summary, when it holds that grid
@@ -424,6 +426,11 @@ def main():
                                   "hbm_bytes_per_launch": g.get("hbm_bytes_per_launch"),
                                   "source": os.path.relpath(args.pmc_json, REPO) + " (" + pmc.get("source_run", "?") +
                                   f", {wg}-workgroup launches, {streams} concurrent sampler streams)"}
+            if os.path.exists(pmc_k):  # MFMA busy of the same grid in the serialised PMC passes
+                pe = [v for v in json.load(open(pmc_k)).values()
+                      if v.get("kernel") == dom_name and v.get("workgroups") == wg and "mfma_busy" in v]
+                if pe:
+                    roof["production"]["mfma_busy_pmc"] = round(pe[0]["mfma_busy"], 3)
     # per-kernel breakdown of the fully profiled warmup step
     total_flops = sum(v["flops"] for v in prof_all.values())
     calls = (1000 // args.speedup + 1) if fast else 1000

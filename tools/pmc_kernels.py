@@ -2,7 +2,7 @@
 and HBM bytes. MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs): the share of SIMD
 cycles with the matrix core busy (MI355X_MICROARCH.md: the MFMA counter counts cycles, GRBM_GUI_ACTIVE is summed over the
 8 XCDs). HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 (the gfx950 FETCH_SIZE 1/2 correction). LDS bank conflicts as a
-share of LDS-active cycles. Usage: python tools/pmc_kernels.py gpurun_out/<tag> [json_out]"""
+share of LDS-active cycles; VALU instructions per MFMA (MFMAs estimated as busy cycles / 16). Usage: python tools/pmc_kernels.py gpurun_out/<tag> [json_out]"""
 import collections
 import csv
 import glob
@@ -31,6 +31,12 @@ def main():
             d["mfma_busy"] = m["SQ_VALU_MFMA_BUSY_CYCLES"] / (m["GRBM_GUI_ACTIVE"] / 8 * 256 * 4)
             d["gpu_cycles"] = m["GRBM_GUI_ACTIVE"] / 8
         d["kernel"] = k
+        if m.get("SQ_VALU_MFMA_BUSY_CYCLES") and "SQ_INSTS_VALU" in m:
+            # MFMA instructions ~ busy cycles / 16 (v_mfma_f32_16x16x32_f16 / _bf16 keep the matrix pipe 16 cycles);
+            # SQ_INSTS_VALU counts them too
+            n_mfma = m["SQ_VALU_MFMA_BUSY_CYCLES"] / 16.0
+            d["mfma_insts_est"] = n_mfma
+            d["valu_per_mfma"] = (m["SQ_INSTS_VALU"] - n_mfma) / n_mfma
         if "SQ_LDS_BANK_CONFLICT" in m and m.get("SQ_LDS_IDX_ACTIVE"):
             d["lds_conflict_share"] = m["SQ_LDS_BANK_CONFLICT"] / m["SQ_LDS_IDX_ACTIVE"]
         if "FETCH_SIZE" in m and "WRITE_SIZE" in m:
@@ -40,7 +46,8 @@ def main():
         rows.append((d.get("gpu_cycles", 0) * n, k, g, d))
     for _, k, g, d in sorted(rows, key=lambda r: -r[0]):
         print(f"{k:34s} wg={g:6d} n={d['dispatches']:5d} mfma_busy={d.get('mfma_busy', float('nan')):.3f} "
-              f"cycles={d.get('gpu_cycles', 0):9.0f} lds_conflict={d.get('lds_conflict_share', float('nan')):.3f} "
+              f"cycles={d.get('gpu_cycles', 0):9.0f} valu/mfma={d.get('valu_per_mfma', float('nan')):5.2f} "
+              f"lds_conflict={d.get('lds_conflict_share', float('nan')):.3f} "
               f"hbm_MB={d.get('hbm_bytes', 0) / 1e6:8.1f}")
     if len(sys.argv) > 2:
         json.dump(out, open(sys.argv[2], "w"), indent=1)
