@@ -18,6 +18,7 @@ are synthetic harmonic clips. Rank 0 prints one JSON line.
 """
 import argparse
 import json
+import re
 import os
 import socket
 import subprocess
@@ -415,7 +416,9 @@ def main():
         ent = pmc.get("kernels", {}).get(dom_name)
         T_frames = int((d24.shape[1] + 768 - 1024) // 256 + 1)
         sub_rows = -(-B // streams) * T_frames  # the largest sub-batch
-        wg = -(-sub_rows // 128) * 6           # 128 x 128 tiles over the 768 packed gate / filter columns
+        m_bm = re.match(r"conv_gemm4<(\d+),", dom_name)
+        bm = int(m_bm.group(1)) if m_bm else 128
+        wg = -(-sub_rows // bm) * 6            # bm x 128 tiles over the 768 packed gate / filter columns
         g = ent.get("by_grid", {}).get(str(wg * 256)) if ent else None
         if g and "rocprof_trace_avg_us" in g:
             fl = 2.0 * sub_rows * 768 * 1152
