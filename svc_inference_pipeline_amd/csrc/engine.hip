@@ -106,6 +106,8 @@ int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s, bool bf);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
+int res_proj(const f16* g, const f16* W, int ldw, const float* bias, const float* sub, const float* add, float div,
+             f16* hi, f16* lo, int M, bool bf16, int grid_cap, hipStream_t s);
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
               int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
               bool bf16);
@@ -303,7 +305,7 @@ static int* tuning_field(T& t, const char* name) {
   } ints[] = {{"gemm_variant", &t.gemm_variant},       {"gemm3_direct", &t.gemm3_direct},
               {"whisper_streams", &t.whisper_streams}, {"sampler_streams", &t.sampler_streams},
               {"vocoder_streams", &t.vocoder_streams}, {"diff_head", &t.diff_head},
-              {"amp_maxc", &t.amp_maxc}};
+              {"amp_maxc", &t.amp_maxc},               {"res_proj", &t.res_proj}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) return it.v;
   return nullptr;
@@ -311,7 +313,7 @@ static int* tuning_field(T& t, const char* name) {
 
 void Tuning::from_env() {
   for (const char* name : {"gemm_variant", "gemm3_direct", "whisper_streams", "sampler_streams", "vocoder_streams",
-                           "diff_head", "amp_maxc"}) {
+                           "diff_head", "amp_maxc", "res_proj"}) {
     std::string env = "SVC_";
     for (const char* q = name; *q; ++q) env += (char)toupper((unsigned char)*q);
     if (const char* v = getenv(env.c_str())) *tuning_field(*this, name) = atoi(v);
@@ -2026,6 +2028,15 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
     // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step):
     // x_i = (y16 + lo16) - dproj_i, and x_{i+1} + dproj_{i+1} goes back split into y16 / lo16
+    if (tuning().res_proj && C == 384 && c->outres[i].N == C && c->outres[i].K == C && c->outres[i].Kpad >= C) {
+      // weight-stationary row stream (res_proj.hip), bit-identical to the tiled GEMM below
+      prof_site("diffsvc.outproj");
+      if ((st = res_proj(bb.g16 + (size_t)i * bb.g_ls, c->outres[i].W, c->outres[i].Kpad, c->outres[i].bias,
+                         dp + (size_t)i * C, dp + (size_t)(i + 1) * C, 1.41421356237309515f, bb.y16, bb.lo16, rows,
+                         c->outres[i].bf16, tuning().res_proj > 1 ? tuning().res_proj : 0, s)))
+        return st;
+      continue;
+    }
     EpiArgs r = epi();
     r.ld_acc = C;
     r.acc_div = 1.41421356237309515f;
@@ -2722,7 +2733,9 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters != 0, "gemm_bench: bad args");
   SVC_REQUIRE(epi_kind < 3 || epi_kind == 6 || variant == 24,
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
-  SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24, "gemm_bench: variant %d", variant);
+  SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24 ||
+                  (variant == 30 && epi_kind == 6 && N == 384 && Cin == 384 && taps == 1),
+              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap)", variant);
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float *bias, *R = nullptr;
@@ -2770,6 +2783,8 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   if (const char* fm = getenv("SVC_BENCH_FLUSH_MB")) flush_bytes = (size_t)atoi(fm) << 20;  // (bench tool only)
   if (cold) SVC_HIP_CHECK(hipMalloc(&flush, flush_bytes));
   auto run = [&]() {
+    if (variant == 30)
+      return res_proj(X, W, Kpad, bias, bias, bias, e.acc_div, Y, reinterpret_cast<f16*>(R), M, false, 0, 0);
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
     return conv_gemm3(a, e, zero_page(), variant - 10, 0);
   };

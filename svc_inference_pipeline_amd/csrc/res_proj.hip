@@ -1,0 +1,253 @@
+// DiffSVC residual projection as a weight-stationary row stream (modules/diffsvc.py:228-232), round 3.
+//
+// Per layer i < 19 of every denoiser call the split residual stream x + dproj_i = hi + lo (two fp16 halves, engine.hip
+// denoise) is updated in place from the layer's gate output g (f16 [M][384]):
+//   v  = g W_res^T + b_res                                    (residual half of output_projection, K = N = 384)
+//   x' = (((hi + lo) - dproj_i) + v) / sqrt(2)                (modules/diffsvc.py:232)
+//   hi = f16(x' + dproj_{i+1}),  lo = f16((x' + dproj_{i+1}) - hi)
+// The GEMM is small (0.3 MFLOP per row) and the row's bytes are large (768 B of g in, 1536 B of hi / lo in and out), so
+// the kernel is an HBM stream: 57.6 MB per 15 k-row sampler sub-batch. conv_gemm3's 128 x 128 tiles ran it as six
+// dependent K-tile DMA round trips plus an epilogue read-modify-write per tile (latency-bound: 0.18 of HBM in situ).
+// Here instead:
+//   * W_res lives in VGPRs for the whole launch: a workgroup owns one half of the output columns (192), and each of its
+//     12 waves holds one 16-column block's 384 x 16 f16 weights as 12 MFMA fragments (48 VGPRs), loaded once;
+//   * the two workgroups of a row lane (one per half) walk the lane's 16-row tiles and LDS-DMA each tile's g rows and
+//     their half of the hi / lo rows (24 KiB) into a ring of RP_D slots, RP_D - 1 tiles ahead of the tile being
+//     computed: the loop issues no per-lane address arithmetic (a per-tile buffer descriptor carries the row base;
+//     rows past M fall outside its range and read as 0);
+//   * per tile a wave runs 12 v_mfma_f32_16x16x32 (operands swapped, so a lane's accumulator holds 4 consecutive
+//     columns of one row) and applies the split-residual update in registers, storing hi / lo with range-checked buffer
+//     stores (rows past M are dropped by the hardware), 8 B per lane and half.
+// (A first form held all 384 columns per workgroup, 144 VGPRs of W per wave: loading 288 KiB of W into every CU took
+// ~10 us per launch, longer than the sampler sub-batch's whole stream; measured 35 vs 23 us full batch.)
+// K order (k = 0..383 in 32-deep MFMA steps into one accumulator) and the epilogue's arithmetic are conv_gemm3's, so the
+// result is bit-identical to the tiled GEMM with its LDS-staged split epilogue (tests/test_gpu_ops.py).
+#include "common.h"
+
+// rp_dma clobbers m0 (reserved for the compiler's own LDS-DMA and indexing uses, which all set it right before use)
+#pragma clang diagnostic ignored "-Winline-asm"
+
+namespace svc {
+
+constexpr int RP_C = 384;                 // channels: K = N = 384
+constexpr int RP_H = 192;                 // output columns per workgroup (one half of N)
+constexpr int RP_ROWS = 16;               // rows per tile (one MFMA block)
+constexpr int RP_NW = 12;                 // waves per workgroup, one 16-column MFMA block each
+constexpr int RP_NT = 64 * RP_NW;
+constexpr int RP_GB = RP_ROWS * RP_C * 2;  // g image of a tile: 12 KiB = 12 DMA wave-instructions
+constexpr int RP_HB = RP_ROWS * RP_H * 2;  // hi (or lo) image of a tile's half: 6 KiB = 6
+constexpr int RP_SLOT = RP_GB + 2 * RP_HB;  // 24 KiB: 24 DMA wave-instructions, 2 per wave
+constexpr int RP_ND = 2, RP_NS = 2;       // per wave and tile: DMA wave-instructions, stores
+constexpr uint32_t RP_CFG = 0x00020000u;  // buffer descriptor dword 3 (raw, 32-bit data format)
+
+struct ResProjArgs {
+  const f16* g;       // [M][384] gate outputs of the layer
+  const f16* W;       // packed W_res [>= 384][ldw], W[n][k]
+  int ldw;
+  const float* bias;  // [384]
+  const float* sub;   // dproj_i [384]
+  const float* add;   // dproj_{i+1} [384]
+  float div;          // sqrt(2)
+  f16* hi;            // [M][384] split residual stream, updated in place
+  f16* lo;
+  int M;
+  int lanes;          // row lanes = gridDim.x / 2 (each lane's two workgroups take the two halves of N)
+  int iters;          // tiles per workgroup: ceil(ceil(M / 16) / lanes)
+};
+
+// LDS images, 16-B chunks: g row r (< 16) chunk q (< 48) at r * 48 + (q ^ r); hi / lo row r chunk q (< 24) at
+// r * 24 + (q ^ ((r >> 1) & 7)). The MFMA operand reads (16 rows x one chunk per lane quarter, ds_read_b128) and the
+// epilogue's 8-B hi / lo reads (16 rows x 2 halves of one chunk per half-wave, ds_read_b64) are then conflict-free.
+__device__ __forceinline__ int rp_gchunk(int r, int q) { return r * 48 + (q ^ r); }
+__device__ __forceinline__ int rp_hchunk(int r, int q) { return r * 24 + (q ^ ((r >> 1) & 7)); }
+
+// LDS-DMA of 16 B per lane (lane i's bytes land at lds + 16 i) through a buffer descriptor, in inline asm: the compiler
+// does not see it, so it neither drains it before every LDS read it cannot prove disjoint (it did, for the hi / lo
+// reads of the ring) nor counts it; the loop's own vmcnt waits (rp_wait_tile) order the ring
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 rp_desc(const f16* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, (uint32_t)(bytes > 0 ? bytes : 0), RP_CFG};
+}
+__device__ __forceinline__ void rp_dma(u32x4 d, uint32_t voff, unsigned char* lds) {
+  const uint32_t m0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               ::"s"(m0), "v"(voff), "s"(d) : "memory", "m0");
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rp_rsrc(const f16* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(base), (short)0, (int)(bytes > 0 ? bytes : 0), RP_CFG);
+}
+
+// wait until at most N of this wave's vector-memory operations are outstanding (loads, LDS-DMAs and stores count
+// together, in issue order)
+template <int N>
+__device__ __forceinline__ void rp_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Every wave issues RP_ND DMA wave-instructions and RP_NS buffer stores per iteration, whatever the rows (tiles past
+// the end DMA zeros, stores past M are dropped by the range check), so the number of its vector-memory operations
+// younger than its DMAs of tile t is a compile-time count:
+//   t < D - 1 (DMA(t) issued in the prologue): (D - 2 - t) ND + t (ND + NS);  t >= D - 1: NS + (D - 2) (ND + NS)
+template <int D, int T>
+__device__ __forceinline__ void rp_wait_case() {
+  constexpr int n = T < D - 1 ? (D - 2 - T) * RP_ND + T * (RP_ND + RP_NS) : RP_NS + (D - 2) * (RP_ND + RP_NS);
+  rp_vmwait<n>();
+}
+template <int D>
+__device__ __forceinline__ void rp_wait_tile(int t) {
+  static_assert(D >= 3 && D <= 5, "ring depth");
+  if (t == 0) rp_wait_case<D, 0>();
+  else if (t == 1) rp_wait_case<D, 1>();
+  else if (D >= 4 && t == 2) rp_wait_case<D, (D >= 4 ? 2 : D - 1)>();
+  else if (D >= 5 && t == 3) rp_wait_case<D, (D >= 5 ? 3 : D - 1)>();
+  else rp_wait_case<D, D - 1>();
+}
+
+// RP_D: ring slots (tiles); DMAs run RP_D - 1 tiles ahead
+template <bool BF, int RP_D>
+__global__ __launch_bounds__(RP_NT, 1) void res_proj_kernel(ResProjArgs p) {
+  using O = Op16<BF>;
+  extern __shared__ __align__(16) unsigned char smr[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fk = lane >> 4;
+  // workgroups b and b + 8 (one XCD under round-robin placement) take the two halves of the same row tiles, so the
+  // second read of each g tile is an L2 hit (speed only)
+  const int b = blockIdx.x;
+  const int half = (b >> 3) & 1, rlane = (b & 7) | ((b >> 4) << 3);
+  const int n0 = half * RP_H + 16 * wave;  // this wave's output columns n0 .. n0 + 15; the lane's: n0 + 4 fk .. + 3
+
+  // W fragments of the swapped MFMA (its A operand): w[kc] = W[n0 + fr][kc * 32 + fk * 8 .. + 8]
+  half8 w[12];
+#pragma unroll
+  for (int kc = 0; kc < 12; ++kc)
+    w[kc] = *reinterpret_cast<const half8*>(p.W + (int64_t)(n0 + fr) * p.ldw + kc * 32 + fk * 8);
+  const float4 bi = *reinterpret_cast<const float4*>(p.bias + n0 + 4 * fk);
+  const float4 sb = *reinterpret_cast<const float4*>(p.sub + n0 + 4 * fk);
+  const float4 ad = *reinterpret_cast<const float4*>(p.add + n0 + 4 * fk);
+
+  // this wave's DMA wave-instructions f = wave and wave + 12: f < 12 g piece f; 12..17 hi piece f - 12; 18..23 lo
+  uint32_t voff[2];
+  int dst[2], img[2];
+  const f16* src[2];  // image base (row 0 of this half)
+  int hoff[2];        // bytes of that base past the row start
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const int f = wave + 12 * v;
+    img[v] = f < 12 ? 0 : (f < 18 ? 1 : 2);
+    const int piece = f < 12 ? f : (f < 18 ? f - 12 : f - 18);
+    const int c = 64 * piece + lane;
+    if (img[v] == 0) {
+      const int r = c / 48, q = (c % 48) ^ r;
+      voff[v] = (uint32_t)(r * RP_C * 2 + q * 16);
+      dst[v] = piece * 1024;
+      src[v] = p.g;
+      hoff[v] = 0;
+    } else {
+      const int r = c / 24, q = (c % 24) ^ ((r >> 1) & 7);
+      voff[v] = (uint32_t)(r * RP_C * 2 + q * 16);
+      dst[v] = RP_GB + (img[v] - 1) * RP_HB + piece * 1024;
+      src[v] = (img[v] == 1 ? p.hi : p.lo) + half * RP_H;
+      hoff[v] = half * RP_H * 2;
+    }
+  }
+  auto issue = [&](int t) {  // tile t of this workgroup into slot t % RP_D (tiles past the end read zeros)
+    const int row0 = (rlane + t * p.lanes) * RP_ROWS;
+    const bool live = row0 < p.M;
+    const int64_t bytes = live ? (int64_t)(p.M - row0) * RP_C * 2 : 0;
+    const int64_t off = live ? (int64_t)row0 * RP_C : 0;
+    unsigned char* slot = smr + (t % RP_D) * RP_SLOT;
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      rp_dma(rp_desc(src[v] + off, bytes - hoff[v]), voff[v], slot + dst[v]);
+    }
+  };
+  const __amdgpu_buffer_rsrc_t sh = rp_rsrc(p.hi, (int64_t)p.M * RP_C * 2), sl = rp_rsrc(p.lo, (int64_t)p.M * RP_C * 2);
+
+#pragma unroll
+  for (int t = 0; t < RP_D - 1; ++t) issue(t);
+  for (int t = 0; t < p.iters; ++t) {
+    rp_wait_tile<RP_D>(t);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // every wave's DMAs of tile t have landed; slot (t - 1) % RP_D is free
+    __builtin_amdgcn_sched_barrier(0);
+    issue(t + RP_D - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned char* slot = smr + (t % RP_D) * RP_SLOT;
+    half8 a[12];
+#pragma unroll
+    for (int kc = 0; kc < 12; ++kc) a[kc] = *reinterpret_cast<const half8*>(slot + rp_gchunk(fr, kc * 4 + fk) * 16);
+    // this lane's hi / lo: row fr, columns n0 + 4 fk .. + 3 = chunk 2 wave + (fk >> 1) of the half, 8-B half fk & 1
+    const int hb = rp_hchunk(fr, 2 * wave + (fk >> 1)) * 16 + (fk & 1) * 8;
+    union { uint2 u; f16 h[4]; } hi, lo, ph, pl;
+    hi.u = *reinterpret_cast<const uint2*>(slot + RP_GB + hb);
+    lo.u = *reinterpret_cast<const uint2*>(slot + RP_GB + RP_HB + hb);
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kc = 0; kc < 12; ++kc) acc = O::mfma(w[kc], a[kc], acc);  // acc[r] = C[row fr][n0 + 4 fk + r]
+    // split-residual update (engine.hip epilogue_pass arithmetic, same order)
+    const float v[4] = {acc[0] + bi.x, acc[1] + bi.y, acc[2] + bi.z, acc[3] + bi.w};
+    const float s4[4] = {sb.x, sb.y, sb.z, sb.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float ac = (O::dec(hi.h[r]) + O::dec(lo.h[r])) - s4[r];
+      float x = ac + v[r];
+      x = x / p.div;
+      const float wv = x + a4[r];
+      ph.h[r] = O::enc(wv);
+      pl.h[r] = O::enc_lo(wv - O::dec(ph.h[r]));
+    }
+    const int row = (rlane + t * p.lanes) * RP_ROWS + fr;
+    const uint32_t vo = (uint32_t)row * (RP_C * 2) + (uint32_t)(n0 + 4 * fk) * 2;
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, ph.u), sh,
+                                          vo, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, pl.u), sl,
+                                          vo, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  rp_vmwait<0>();  // (the remaining DMAs of tiles past the end land before the workgroup's LDS is released)
+}
+
+// M rows of the split residual update for one layer; W: packed [>= 384][ldw] weights of the residual half.
+// lanes_cap > 0: that many row lanes (2 workgroups each) instead of one workgroup per CU
+int res_proj(const f16* g, const f16* W, int ldw, const float* bias, const float* sub, const float* add, float div,
+             f16* hi, f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s) {
+  SVC_REQUIRE(M >= 0 && ldw >= RP_C && ldw % 8 == 0, "res_proj: M %d ldw %d", M, ldw);
+  if (M == 0) return SVC_OK;
+  SVC_REQUIRE((int64_t)M * RP_C * 2 < (1ll << 31) - (1 << 20), "res_proj: %d rows exceed the 32-bit buffer range", M);
+  SVC_REQUIRE(((uintptr_t)g & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)hi & 15) == 0 &&
+                  ((uintptr_t)lo & 15) == 0,
+              "res_proj: 16-B alignment");
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    SVC_HIP_CHECK(hipGetDevice(&dev));
+    SVC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int tiles = cdiv(M, RP_ROWS);
+  // row lanes in groups of 8 (the b / b + 8 pairing above): one workgroup per CU by default
+  int lanes = lanes_cap > 0 ? lanes_cap : ncu / 2;
+  lanes = std::max(8, std::min(lanes, (int)round_up(tiles, 8)));
+  lanes = (int)round_up(lanes, 8);
+  ResProjArgs a{g, W, ldw, bias, sub, add, div, hi, lo, M, lanes, cdiv(tiles, lanes)};
+  // ring depth 3 (two tiles in flight): 4 and 5 slots measured no faster alone or in the sampler (r03k)
+  constexpr int depth = 3;
+  const void* fn = bf16 ? (const void*)res_proj_kernel<true, depth> : (const void*)res_proj_kernel<false, depth>;
+  const int lds = depth * RP_SLOT;
+  static bool attr[2] = {};
+  if (!attr[bf16]) {
+    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr[bf16] = true;
+  }
+  const int tok = prof_begin("res_proj<16x192>", 2.0 * M * RP_C * RP_C, (double)M * RP_C * 10.0, s);
+  void* args[] = {&a};
+  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3(2 * lanes), dim3(RP_NT), args, lds, s));
+  prof_end(tok, s);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+}  // namespace svc

@@ -187,6 +187,26 @@ def test_fused_head(engine, states, cfg, B, T, tune):
     assert rel_l2(out["fused"][1].cpu().numpy(), ref) < 5e-3
 
 
+@pytest.mark.parametrize("B,T", [(1, 5), (1, 93), (3, 50), (2, 700), (5, 937)])
+def test_res_proj_bit_identical(engine, B, T, tune):
+    """res_proj.hip (the DiffSVC residual projection as a weight-stationary row stream: W_res in VGPRs, 16-row tiles of
+    g / hi / lo LDS-DMA'd through a ring) against the tiled conv_gemm3 GEMM with its LDS-staged split epilogue
+    (res_proj = 0): the same 32-deep K order and epilogue arithmetic, so bit for bit equal. One workgroup per CU and
+    capped grids of 8 / 24 row lanes (many ring iterations per workgroup, the steady-state vmcnt waits); tiny and
+    ragged row counts (M < 16, rows past M inside the last tile read as zero and are not stored)."""
+    rng = np.random.default_rng(B * 17 + T)
+    cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
+    x = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
+    tune(engine, res_proj=0)
+    ref = [engine.diffsvc_eps(cond, x, t).cpu().numpy() for t in (250, 7)]
+    for v in (1, 8, 24):
+        tune(engine, res_proj=v)
+        out = [engine.diffsvc_eps(cond, x, t).cpu().numpy() for t in (250, 7)]
+        for k in range(2):
+            assert np.isfinite(out[k]).all()
+            assert np.array_equal(out[k], ref[k]), (v, k, rel_l2(out[k], ref[k]))
+
+
 def test_fused_head_plms(engine, golden, tune):
     """The fused head through PLMS-4 against the reference-generated golden (same bound as test_plms_and_ddpm)."""
     g = golden("samplers")
@@ -437,6 +457,11 @@ def test_bf16_eps_vs_emulated_oracle(engine_bf16, engine, states, cfg, B, T):
             emu = OM.diffsvc_forward(states["mapper"], cfg.mapper, torch.from_numpy(x), torch.from_numpy(cond), t,
                                      table).numpy()
     eps_bf = engine_bf16.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()
+    engine_bf16.tune(res_proj=0)  # the bf16 residual projection stream equals the tiled GEMM bit for bit
+    try:
+        assert np.array_equal(engine_bf16.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy(), eps_bf)
+    finally:
+        engine_bf16.tune(reset=1)
     eps_h = engine.diffsvc_eps(dev(cond), dev(x), 250).cpu().numpy()
     d_bf, d_emu, d_h = rel_l2(eps_bf, ref), rel_l2(emu, ref), rel_l2(eps_h, ref)
     assert np.isfinite(eps_bf).all()

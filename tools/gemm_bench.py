@@ -1,5 +1,5 @@
 """GEMM kernel microbenchmark (GPU): TFLOP/s of the implicit-GEMM variants on the hot-path shapes.
-Usage: python tools/gemm_bench.py [variant ...]"""
+Usage: python tools/gemm_bench.py [variant ...]   (30: res_proj.hip, on the split residual shapes only)"""
 import ctypes
 import os
 import sys
@@ -15,6 +15,7 @@ SHAPES = [  # name, M, N, Cin, taps, epi
     ("diffsvc.outproj(rmw,sub)", 9995, 384, 384, 1, 2),
     ("diffsvc.outproj(split)", 29984, 384, 384, 1, 6),  # the default split-fp16 residual RMW (hi / lo halves)
     ("diffsvc.outproj(split,sub)", 9995, 384, 384, 1, 6),
+    ("diffsvc.outproj(split,sub2)", 14992, 384, 384, 1, 6),  # 2-stream sampler sub-batch
     ("diffsvc.skipsum", 29984, 384, 7680, 1, 0),
     ("bigvgan.s2 k11", 32 * 14992, 384, 384, 11, 0),
     ("whisper.fc1", 48000, 4096, 1024, 1, 0),

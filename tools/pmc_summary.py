@@ -41,6 +41,8 @@ def short(name):
     m = re.search(r"activation1d_rs_kernel", name)
     if m:
         return "activation1d"
+    if "res_proj_kernel" in name:
+        return "res_proj<16x192>"
     for k, v in NAME_MAP.items():
         if k in name:
             return v
