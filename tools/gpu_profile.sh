@@ -10,6 +10,10 @@ R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
+# a profiled pass writes nothing until it ends: tick a file under gpurun_out/ so the run is not taken for hung
+( while sleep 30; do date +%s >> $R/gpurun_out/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
 STEPS=${STEPS:-3}
 if [ -z "${PMC_ONLY:-}" ]; then
 timeout -k 10 900 python3 bench.py --steps $STEPS --warmup 1 > $OUT/bench.json 2> $OUT/bench.err

@@ -5,7 +5,11 @@
 #   TAG: output dir under gpurun_out; KRE: kernel regex
 set -uo pipefail
 R=$(pwd); TAG=${TAG:-pmc}; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
-KRE=${KRE:-conv_gemm4_kernel|conv_gemm3_kernel|attention_kernel|amp_conv_kernel|activation1d}
+# a profiled pass writes nothing until it ends: tick a file under gpurun_out/ so the run is not taken for hung
+( while sleep 30; do date +%s >> $R/gpurun_out/heartbeat; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
+KRE=${KRE:-conv_gemm4_kernel|conv_gemm3_kernel|res_proj_kernel|attention_kernel|amp_conv_kernel|activation1d}
 i=0
 for set in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
