@@ -98,7 +98,7 @@ __device__ __forceinline__ void rp_wait_case() {
 }
 template <int D>
 __device__ __forceinline__ void rp_wait_tile(int t) {
-  static_assert(D >= 3 && D <= 5, "ring depth");
+  static_assert(D >= 2 && D <= 5, "ring depth");
   if (t == 0) rp_wait_case<D, 0>();
   else if (t == 1) rp_wait_case<D, 1>();
   else if (D >= 4 && t == 2) rp_wait_case<D, (D >= 4 ? 2 : D - 1)>();
@@ -228,12 +228,16 @@ int res_proj(const f16* g, const f16* W, int ldw, const float* bias, const float
     SVC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   }
   const int tiles = cdiv(M, RP_ROWS);
-  // row lanes in groups of 8 (the b / b + 8 pairing above): one workgroup per CU by default
-  int lanes = lanes_cap > 0 ? lanes_cap : ncu / 2;
+  // row lanes in groups of 8 (the b / b + 8 pairing above). Default: 3/8 of the CU count (96 lanes = 192 workgroups
+  // on 256 CUs): end to end 810.4-810.8 audio-s/s against 800.6-806.1 with one workgroup per CU, 804-805 with 80 lanes
+  // and 807-808 with 112 (r03p, three alternating rounds): the CUs it leaves free run the other sampler stream's gate
+  // GEMM, and fewer workgroups load W fewer times
+  int lanes = lanes_cap > 0 ? lanes_cap : ncu * 3 / 8;
   lanes = std::max(8, std::min(lanes, (int)round_up(tiles, 8)));
   lanes = (int)round_up(lanes, 8);
   ResProjArgs a{g, W, ldw, bias, sub, add, div, hi, lo, M, lanes, cdiv(tiles, lanes)};
-  // ring depth 3 (two tiles in flight): 4 and 5 slots measured no faster alone or in the sampler (r03k)
+  // ring depth 3 (two tiles in flight): 4 / 5 slots measured no faster alone or in the sampler (r03k), 2 slots 4 % slower
+  // end to end (r03o)
   constexpr int depth = 3;
   const void* fn = bf16 ? (const void*)res_proj_kernel<true, depth> : (const void*)res_proj_kernel<false, depth>;
   const int lds = depth * RP_SLOT;
