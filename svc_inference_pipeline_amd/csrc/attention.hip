@@ -12,10 +12,12 @@
 // A operand is read with gfx950's transposing ds_read_b64_tr_b16 (a 16-lane group reads 4 keys x 16 head columns and
 // each lane receives its column), from an image whose 16-B chunks are XOR-swizzled so those reads are conflict-free.
 // Softmax VALU work per score: the score MFMAs accumulate onto -m (the running max as their C operand), so S - m
-// comes out of the matrix core and goes straight into v_exp_f32; the lane's max of S - m is a v_max3_f32 tree, and
-// only when some lane of the wave sees S - m > ATT_DEFER (rare after the first tile) is the running max moved: the
-// cross-lane column max, O / l rescaled, S - m shifted. The first tile sets m exactly; the key mask runs on the last
-// tile only. The kernel is VALU-issue bound (round 2 PMC: ~9.6 VALU instructions per MFMA, 0.30 MFMA busy).
+// comes out of the matrix core and goes straight into v_exp_f32 and an f16 conversion. The row sum l is a fifth P.V
+// product against a block of ones (round 3): 4 MFMAs per tile instead of 16 packed f32 adds per lane and a final
+// cross-lane reduction. The same tile sums bound every P of their column, so the deferred rescale needs no per-tile max:
+// only when some column's tile sum exceeds ATT_PSUM (rare after the first tile) does the running max move (its v_max3
+// tree, the cross-lane column max, O / l rescaled, P made again). The first tile sets m exactly; the key mask runs on the
+// last tile only. The kernel is VALU-issue bound (round 2 PMC: ~9.6 VALU instructions per MFMA, 0.30 MFMA busy).
 #include <type_traits>
 
 #include "common.h"
@@ -24,7 +26,7 @@ namespace svc {
 
 constexpr int ATT_QT = 128;   // queries per workgroup
 constexpr int ATT_KT = 64;    // keys per tile
-constexpr float ATT_DEFER = 8.0f * ATT_LOG2E;  // deferred-rescale threshold of the running max (exp2 units: e^8)
+constexpr float ATT_PSUM = 16384.0f;  // deferred rescale: a tile's P column sum above this moves the running max
 
 __device__ __forceinline__ int kswz(int row, int kv) { return row * 64 + ((kv ^ ((row >> 1) & 7)) << 3); }
 // V image: [key][64 f16] rows, 16-B chunk c of row r stored at chunk c ^ (((r >> 1) & 3) << 1). A transposing read of
@@ -106,8 +108,13 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
     for (int f = 0; f < 2; ++f) o[df][f] = (floatx4){0.f, 0.f, 0.f, 0.f};
   // running max m (exp2 units; set exactly by the first tile), its negation as the score MFMAs' C operand, and the
   // lane's share of the row sum
-  float mrun[2] = {0.f, 0.f}, lrun[2] = {0.f, 0.f};
+  float mrun[2] = {0.f, 0.f};
   floatx4 negm[2] = {(floatx4){0.f, 0.f, 0.f, 0.f}, (floatx4){0.f, 0.f, 0.f, 0.f}};
+  // the row sum l = P . 1 on the matrix core: a 16-row block of ones as V^T's A operand, so every r of ol[f] holds the
+  // column's sum over all keys so far (of the rounded P that the P.V MFMAs use; no VALU adds, no final cross-lane sum)
+  floatx4 ol[2] = {(floatx4){0.f, 0.f, 0.f, 0.f}, (floatx4){0.f, 0.f, 0.f, 0.f}};
+  const half8 ones = BF ? __builtin_bit_cast(half8, (bf16x8){1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f})
+                        : (half8){1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f};
 
   const int ntiles = (L + ATT_KT - 1) / ATT_KT;
   u32x4 kreg[2], vreg[2];  // (a native vector type: the uint4 struct copies were kept in scratch)
@@ -163,6 +170,47 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
     // ---- online softmax per query column
     const bool tail = TAIL && k0 + ATT_KT > L;  // keys past L only in the last tile (wave-uniform)
     half8 pb[2][2];  // P^T as B operand: [f][ks'] element j <-> key 32ks' + 4g + (j&3) + 16(j>>2)
+    // P = 2^(S - m) straight from the accumulators, converted to f16 in packed pairs
+    auto make_p = [&](int f) {
+      half2v ph[4][2];
+#pragma unroll
+      for (int kf = 0; kf < 4; ++kf)
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          float2v a;
+          a.x = __builtin_amdgcn_exp2f(s[kf][f][2 * hh]);
+          a.y = __builtin_amdgcn_exp2f(s[kf][f][2 * hh + 1]);
+          if constexpr (BF)
+            ph[kf][hh] = __builtin_bit_cast(half2v, __builtin_convertvector(a, bf16x2));
+          else
+            ph[kf][hh] = __builtin_convertvector(a, half2v);
+        }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        pb[f][ks] = (half8){ph[2 * ks][0].x, ph[2 * ks][0].y, ph[2 * ks][1].x, ph[2 * ks][1].y,
+                            ph[2 * ks + 1][0].x, ph[2 * ks + 1][0].y, ph[2 * ks + 1][1].x, ph[2 * ks + 1][1].y};
+    };
+    // move column f's running max by its tile max where that grew (all of it on the first tile): the lane's max of
+    // its 16 scores as a v_max3_f32 tree, the column's by two lane swaps
+    auto move_max = [&](int f, auto first_c) {
+      constexpr bool F1 = decltype(first_c)::value;
+      const float x0 = max3f(s[0][f][0], s[0][f][1], s[0][f][2]), x1 = max3f(s[0][f][3], s[1][f][0], s[1][f][1]);
+      const float x2 = max3f(s[1][f][2], s[1][f][3], s[2][f][0]), x3 = max3f(s[2][f][1], s[2][f][2], s[2][f][3]);
+      const float x4 = max3f(s[3][f][0], s[3][f][1], s[3][f][2]);
+      const float mx = fmaxf(max3f(x0, x1, x2), max3f(x3, x4, s[3][f][3]));
+      const float cm = max_xor32(max_xor16(mx));   // the column's max of S - m over the tile
+      const float d = F1 ? cm : fmaxf(cm, 0.f);     // how far m moves (0: this column keeps its max)
+      if constexpr (!F1) {
+        const float alpha = __builtin_amdgcn_exp2f(-d);  // exactly 1 where d = 0
+        ol[f] *= alpha;
+#pragma unroll
+        for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
+      }
+      mrun[f] += d;
+      negm[f] = (floatx4){-mrun[f], -mrun[f], -mrun[f], -mrun[f]};
+#pragma unroll
+      for (int kf = 0; kf < 4; ++kf) s[kf][f] -= d;
+    };
 #pragma unroll
     for (int f = 0; f < 2; ++f) {
       if (TAIL && tail) {
@@ -172,49 +220,34 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
           for (int r = 0; r < 4; ++r)
             if (k0 + kf * 16 + 4 * g + r >= L) s[kf][f][r] = -INFINITY;
       }
-      // the lane's max of its 16 scores: a v_max3_f32 tree (8 instructions)
-      const float x0 = max3f(s[0][f][0], s[0][f][1], s[0][f][2]), x1 = max3f(s[0][f][3], s[1][f][0], s[1][f][1]);
-      const float x2 = max3f(s[1][f][2], s[1][f][3], s[2][f][0]), x3 = max3f(s[2][f][1], s[2][f][2], s[2][f][3]);
-      const float x4 = max3f(s[3][f][0], s[3][f][1], s[3][f][2]);
-      const float mx = fmaxf(max3f(x0, x1, x2), max3f(x3, x4, s[3][f][3]));
-      // deferred rescale (cdna_hip_programming.md T13): after the first tile the running max moves only when some
-      // lane's S - m exceeds ATT_DEFER, so P = 2^(S - m) stays <= e^8 (2981, exact to f16's relative precision) and the
-      // cross-lane max, the O / l rescale and its v_exp run on a few tiles instead of every one
-      if (FIRST || __ballot(!(mx <= ATT_DEFER))) {
-        const float cm = max_xor32(max_xor16(mx));  // the column's max of S - m over the tile
-        const float d = FIRST ? cm : fmaxf(cm, 0.f);  // how far m moves (0: this column keeps its max)
-        if constexpr (!FIRST) {
-          const float alpha = __builtin_amdgcn_exp2f(-d);  // exactly 1 where d = 0
-          lrun[f] *= alpha;
+    }
+    if constexpr (FIRST) {
 #pragma unroll
-          for (int df = 0; df < 4; ++df) o[df][f] *= alpha;
-        }
-        mrun[f] += d;
-        negm[f] = (floatx4){-mrun[f], -mrun[f], -mrun[f], -mrun[f]};
-#pragma unroll
-        for (int kf = 0; kf < 4; ++kf) s[kf][f] -= d;
+      for (int f = 0; f < 2; ++f) {
+        move_max(f, std::true_type{});
+        make_p(f);
       }
-      // P = 2^(S - m) straight from the accumulators; row sum and f16 conversion on packed f32 pairs
-      float2v psum2;
-      half2v ph[4][2];
+    } else {
+      // deferred rescale (cdna_hip_programming.md T13) without a per-tile max: P is made against the running max, and
+      // the tile's column sums (the ones-block MFMAs, needed for l anyway) bound every P of the column. While they stay
+      // <= ATT_PSUM (2^14, so no P reaches f16's 65504) the tile is taken as is; otherwise (rare after the first tile)
+      // the running max moves and P is made again
 #pragma unroll
-      for (int kf = 0; kf < 4; ++kf)
+      for (int f = 0; f < 2; ++f) make_p(f);
+      floatx4 ts[2];
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          float2v a;
-          a.x = __builtin_amdgcn_exp2f(s[kf][f][2 * hh]);
-          a.y = __builtin_amdgcn_exp2f(s[kf][f][2 * hh + 1]);
-          psum2 = kf == 0 && hh == 0 ? a : psum2 + a;
-          if constexpr (BF)
-            ph[kf][hh] = __builtin_bit_cast(half2v, __builtin_convertvector(a, bf16x2));
-          else
-            ph[kf][hh] = __builtin_convertvector(a, half2v);
+      for (int f = 0; f < 2; ++f)
+        ts[f] = O::mfma(ones, pb[f][1], O::mfma(ones, pb[f][0], (floatx4){0.f, 0.f, 0.f, 0.f}));
+      if (__ballot(!(ts[0][0] <= ATT_PSUM && ts[1][0] <= ATT_PSUM))) {
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {
+          move_max(f, std::false_type{});
+          make_p(f);
+          ts[f] = O::mfma(ones, pb[f][1], O::mfma(ones, pb[f][0], (floatx4){0.f, 0.f, 0.f, 0.f}));
         }
-      lrun[f] += psum2.x + psum2.y;
+      }
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        pb[f][ks] = (half8){ph[2 * ks][0].x, ph[2 * ks][0].y, ph[2 * ks][1].x, ph[2 * ks][1].y,
-                            ph[2 * ks + 1][0].x, ph[2 * ks + 1][0].y, ph[2 * ks + 1][1].x, ph[2 * ks + 1][1].y};
+      for (int f = 0; f < 2; ++f) ol[f] += ts[f];
     }
     // ---- O^T += V^T P^T
 #pragma unroll
@@ -230,6 +263,12 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
         for (int f = 0; f < 2; ++f) o[df][f] = O::mfma(va, pb[f][ks], o[df][f]);
       }
     }
+    if constexpr (FIRST) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int f = 0; f < 2; ++f) ol[f] = O::mfma(ones, pb[f][ks], ol[f]);
+    }
     if (kt + 1 < ntiles) lstore((kt + 1) & 1);  // that buffer was last read in iteration kt - 1, before its barrier
     __syncthreads();
   };
@@ -244,9 +283,7 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
   // ---- normalise and store: lane holds O[q = f*16 + c16][d = df*16 + 4g + r]
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
-    float l = lrun[f];
-    l = sum_xor32(sum_xor16(l));
-    const float inv = 1.0f / l;
+    const float inv = 1.0f / ol[f][0];
     const int q = qw0 + f * 16 + c16;
     if (q >= L) continue;
     f16* orow = out + ((int64_t)b * L + q) * D + h * 64;

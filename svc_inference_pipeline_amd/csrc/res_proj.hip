@@ -107,6 +107,27 @@ __device__ __forceinline__ void rp_wait_tile(int t) {
 }
 
 // RP_D: ring slots (tiles); DMAs run RP_D - 1 tiles ahead
+// x / sqrt(2) (f32 sqrt(2)) exactly as the IEEE division rounds it, in one multiply and two FMAs (q0 = x r,
+// e = x - q0 sqrt(2) exactly, q0 + e r): equal to the division bit for bit for every float x with 2^-100 <= |x| < inf
+// (all 2^32 inputs checked against x86 fmaf / division; the differing inputs are |x| <= 2.2e-32 and +-inf). Those
+// lanes take the division, behind a branch no wave takes in practice. Replaces the ~10-instruction division sequence
+// (v_div_scale x2, v_rcp, 4 FMAs, v_div_fmas, v_div_fixup) of the epilogue's four elements per lane.
+constexpr float RP_SQRT2 = 1.41421356237309515f;
+__device__ __forceinline__ float rp_div_sqrt2(float x) {
+  constexpr float r = 1.0f / RP_SQRT2;
+  float q;
+  if (__builtin_expect(fabsf(x) >= 0x1p-100f && fabsf(x) <= 3.402823466e38f, 1)) {
+    const float q0 = x * r;
+    q = fmaf(fmaf(-q0, RP_SQRT2, x), r, q0);
+  } else {
+    q = x / RP_SQRT2;  // (NaN too) the IEEE division for this lane
+  }
+  return q;
+}
+
+// 101-104 VGPRs as built (keep it at or under 104): three waves per SIMD (312 registers) then fit beside one gate GEMM
+// workgroup (184), which is what
+// lets the other sampler stream's gate GEMM and this stream share a CU (r03o / r03p)
 template <bool BF, int RP_D>
 __global__ __launch_bounds__(RP_NT, 1) void res_proj_kernel(ResProjArgs p) {
   using O = Op16<BF>;
@@ -177,9 +198,7 @@ __global__ __launch_bounds__(RP_NT, 1) void res_proj_kernel(ResProjArgs p) {
     issue(t + RP_D - 1);
     __builtin_amdgcn_sched_barrier(0);
     const unsigned char* slot = smr + (t % RP_D) * RP_SLOT;
-    half8 a[12];
-#pragma unroll
-    for (int kc = 0; kc < 12; ++kc) a[kc] = *reinterpret_cast<const half8*>(slot + rp_gchunk(fr, kc * 4 + fk) * 16);
+
     // this lane's hi / lo: row fr, columns n0 + 4 fk .. + 3 = chunk 2 wave + (fk >> 1) of the half, 8-B half fk & 1
     const int hb = rp_hchunk(fr, 2 * wave + (fk >> 1)) * 16 + (fk & 1) * 8;
     union { uint2 u; f16 h[4]; } hi, lo, ph, pl;
@@ -187,15 +206,14 @@ __global__ __launch_bounds__(RP_NT, 1) void res_proj_kernel(ResProjArgs p) {
     lo.u = *reinterpret_cast<const uint2*>(slot + RP_GB + RP_HB + hb);
     floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kc = 0; kc < 12; ++kc) acc = O::mfma(w[kc], a[kc], acc);  // acc[r] = C[row fr][n0 + 4 fk + r]
+    for (int kc = 0; kc < 12; ++kc)  // acc[r] = C[row fr][n0 + 4 fk + r]
+      acc = O::mfma(w[kc], *reinterpret_cast<const half8*>(slot + rp_gchunk(fr, kc * 4 + fk) * 16), acc);
     // split-residual update (engine.hip epilogue_pass arithmetic, same order)
     const float v[4] = {acc[0] + bi.x, acc[1] + bi.y, acc[2] + bi.z, acc[3] + bi.w};
     const float s4[4] = {sb.x, sb.y, sb.z, sb.w}, a4[4] = {ad.x, ad.y, ad.z, ad.w};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float ac = (O::dec(hi.h[r]) + O::dec(lo.h[r])) - s4[r];
-      float x = ac + v[r];
-      x = x / p.div;
+      const float x = rp_div_sqrt2(((O::dec(hi.h[r]) + O::dec(lo.h[r])) - s4[r]) + v[r]);
       const float wv = x + a4[r];
       ph.h[r] = O::enc(wv);
       pl.h[r] = O::enc_lo(wv - O::dec(ph.h[r]));
@@ -216,6 +234,7 @@ __global__ __launch_bounds__(RP_NT, 1) void res_proj_kernel(ResProjArgs p) {
 int res_proj(const f16* g, const f16* W, int ldw, const float* bias, const float* sub, const float* add, float div,
              f16* hi, f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s) {
   SVC_REQUIRE(M >= 0 && ldw >= RP_C && ldw % 8 == 0, "res_proj: M %d ldw %d", M, ldw);
+  SVC_REQUIRE(div == RP_SQRT2, "res_proj: the residual divisor is sqrt(2) (modules/diffsvc.py:232)");
   if (M == 0) return SVC_OK;
   SVC_REQUIRE((int64_t)M * RP_C * 2 < (1ll << 31) - (1 << 20), "res_proj: %d rows exceed the 32-bit buffer range", M);
   SVC_REQUIRE(((uintptr_t)g & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)hi & 15) == 0 &&

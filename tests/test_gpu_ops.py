@@ -142,6 +142,34 @@ def test_attention(B, L, D):
     assert rel_l2(out.cpu().view(B, L, D).numpy(), ref.numpy()) < 3e-3
 
 
+@pytest.mark.parametrize("mode", ["ramp", "outlier"])
+def test_attention_rescale(mode):
+    """The deferred online-softmax rescale (attention.hip: the running max moves only when a tile's P column sum exceeds
+    ATT_PSUM) on inputs that make it fire: key norms ramping up along the sequence (the max grows on many tiles), and
+    one outlier key per head far past the first tile (P of a column jumps from <= 1 to ~2^40 in one tile). Against the
+    fp32 torch reference at the Whisper-medium head layout (L = 1500, 4 heads)."""
+    B, L, D = 2, 1500, 256
+    g = torch.Generator().manual_seed(11)
+    q, k, v = (torch.randn(B, L, D, generator=g) for _ in range(3))
+    if mode == "ramp":
+        k = k * torch.linspace(0.5, 4.0, L)[None, :, None]
+    else:
+        k[:, 1100] *= 12.0
+        q = q + 0.5 * k[:, 1100:1101]
+    H = D // 64
+    sc = 64 ** -0.25
+    qh = q.view(B, L, H, 64).permute(0, 2, 1, 3) * sc
+    kh = k.view(B, L, H, 64).permute(0, 2, 3, 1) * sc
+    vh = v.view(B, L, H, 64).permute(0, 2, 1, 3)
+    ref = (F.softmax(qh @ kh, dim=-1) @ vh).permute(0, 2, 1, 3).reshape(B, L, D)
+    out = torch.empty(B * L, D, device="cuda")
+    qd, kd, vd = dev(q.reshape(B * L, D)), dev(k.reshape(B * L, D)), dev(v.reshape(B * L, D))
+    call("svc_op_attention", ptr(qd), ptr(kd), ptr(vd), B, L, D, ptr(out), stream())
+    o = out.cpu().view(B, L, D).numpy()
+    assert np.isfinite(o).all()
+    assert rel_l2(o, ref.numpy()) < 3e-3
+
+
 def test_layernorm():
     g = torch.Generator().manual_seed(4)
     x = torch.randn(300, 1024, generator=g) * 3 + 1
