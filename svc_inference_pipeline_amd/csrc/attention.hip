@@ -124,15 +124,28 @@ __global__ __launch_bounds__(256, 3) void attention_kernel(const f16* __restrict
   const char* kbase = reinterpret_cast<const char*>(base + D + h * 64);
   const char* vbase = reinterpret_cast<const char*>(base + 2 * D + h * 64);
   const int krow = tid >> 3, kvv = tid & 7;  // vectors tid + 256 i: key row krow + 32 i, 16-B column chunk kvv
+  // per-lane offsets of the two rows within a tile (loop-invariant); the tile's row base is a wave-uniform add
+  uint32_t loff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) loff[i] = (uint32_t)((krow + 32 * i) * ld + kvv * 8) * 2u;
   auto gload = [&](int kt) {
     const int k0 = kt * ATT_KT;
+    if (k0 + ATT_KT > L) {  // last tile only (wave-uniform)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      int key = k0 + krow + 32 * i;
-      if (k0 + ATT_KT > L) key = min(key, L - 1);
-      const uint32_t off = (uint32_t)(key * ld + kvv * 8) * 2u;
-      kreg[i] = *reinterpret_cast<const u32x4*>(kbase + off);
-      vreg[i] = *reinterpret_cast<const u32x4*>(vbase + off);
+      for (int i = 0; i < 2; ++i) {
+        const int key = min(k0 + krow + 32 * i, L - 1);
+        const uint32_t off = (uint32_t)(key * ld + kvv * 8) * 2u;
+        kreg[i] = *reinterpret_cast<const u32x4*>(kbase + off);
+        vreg[i] = *reinterpret_cast<const u32x4*>(vbase + off);
+      }
+    } else {
+      const char* kb = kbase + (size_t)k0 * ld * 2;
+      const char* vb = vbase + (size_t)k0 * ld * 2;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        kreg[i] = *reinterpret_cast<const u32x4*>(kb + loff[i]);
+        vreg[i] = *reinterpret_cast<const u32x4*>(vb + loff[i]);
+      }
     }
   };
   auto lstore = [&](int buf) {  // K and V row-major (swizzled)
