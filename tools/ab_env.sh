@@ -1,7 +1,7 @@
 # Sampler probe and quick benches per environment setting, alternating (run from the repo root via gpurun).
 # SETTINGS: space-separated "VAR=val,VAR=val" ("-" = defaults); ROUNDS: bench rounds; TESTK: optional parity tests first
 set -o pipefail
-O=gpurun_out/${TAG:-r03benv}; mkdir -p $O
+O=gpurun_out/${TAG:-ab_env}; mkdir -p $O
 if [ -n "${TESTK:-}" ]; then
   env ${TESTENV:-} timeout -k 10 600 python -u -m pytest tests/test_gpu_stages.py tests/test_gpu_ragged.py -m gpu -x -q --timeout 300 \
     --timeout-method thread -k "$TESTK" > $O/tests.log 2>&1

@@ -1,19 +1,36 @@
-# A/B of two builds of libsvc_hip.so on one box: ab/libsvc_hip_base.so (reference build) against the in-tree library,
-# alternating, N rounds (default 2). Prints audio-s/s and the per-site kernel times named in SITES.
+# Same-box A/B of ab/libsvc_hip_base.so against the in-tree library (run from the repo root via gpurun):
+# parity tests on the new build ($TESTS, -k $TESTK), then alternating microbenchmarks ($MICRO: att, gate, outproj)
+# and quick benches (ROUNDS).
 set -o pipefail
-mkdir -p gpurun_out
-ROUNDS=${ROUNDS:-2}
-SITES=${SITES:-diffsvc.outproj,bigvgan.amp_c2,bigvgan.amp_c1,whisper.out,whisper.fc2}
-for r in $(seq 1 $ROUNDS); do
+O=gpurun_out/${TAG:-ab_lib}; mkdir -p $O
+if [ -n "${TESTS:-}" ]; then
+  timeout -k 10 600 python -u -m pytest $TESTS -m gpu -x -q --timeout 300 --timeout-method thread ${TESTK:+-k "$TESTK"} > $O/tests.log 2>&1
+  rc=$?; tail -3 $O/tests.log; [ $rc -ne 0 ] && { tail -40 $O/tests.log; exit $rc; }
+fi
+for r in 1 2; do
   for lib in base new; do
     if [ $lib = base ]; then L=$PWD/ab/libsvc_hip_base.so; else L=$PWD/svc_inference_pipeline_amd/libsvc_hip.so; fi
-    SVC_HIP_LIB=$L timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > gpurun_out/ab_$lib.json 2> gpurun_out/ab_$lib.err || exit $?
-    python3 - $lib "$SITES" <<'PY'
+    for m in ${MICRO:-}; do
+      case $m in
+        att) SVC_HIP_LIB=$L timeout -k 10 120 python3 tools/att_bench.py > $O/m.txt 2>&1 || exit $? ;;
+        gate) SVC_HIP_LIB=$L GEMM_BENCH_SHAPES="dilated(gate)" timeout -k 10 120 python3 tools/gemm_bench.py 24 > $O/m.txt 2>&1 || exit $? ;;
+        outproj) SVC_HIP_LIB=$L GEMM_BENCH_TORCH=0 GEMM_BENCH_SHAPES="outproj(split" timeout -k 10 120 python3 tools/gemm_bench.py 15 30 > $O/m.txt 2>&1 || exit $? ;;
+        g3) SVC_HIP_LIB=$L GEMM_BENCH_SHAPES="outproj(split,whisper.fc,skipsum,bigvgan.s2" timeout -k 10 180 python3 tools/gemm_bench.py 15 > $O/m.txt 2>&1 || exit $? ;;
+      esac
+      grep -v amdgpu $O/m.txt | sed "s/^/$lib $m: /"
+    done
+  done
+done
+for r in $(seq 1 ${ROUNDS:-2}); do
+  for lib in base new; do
+    if [ $lib = base ]; then L=$PWD/ab/libsvc_hip_base.so; else L=$PWD/svc_inference_pipeline_amd/libsvc_hip.so; fi
+    SVC_HIP_LIB=$L timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 > $O/b_$lib.json 2> $O/b_$lib.err || exit $?
+    python3 - $O/b_$lib.json $lib <<'PY'
 import json, sys
-d = json.loads(open(f"gpurun_out/ab_{sys.argv[1]}.json").read().strip().splitlines()[-1])
-sites = sys.argv[2].split(",")
-ks = {s: round(sum(v["ms_per_step"] for k, v in d["kernels"].items() if k.endswith("@" + s)), 3) for s in sites}
-print(sys.argv[1], d["value"], d["ms_per_step"], ks, flush=True)
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+k = d["kernels"]
+pick = lambda s: round(sum(v["ms_per_step"] for kk, v in k.items() if kk.endswith("@" + s)), 3)
+print(sys.argv[2], d["value"], d["ms_per_step"], "att", pick("whisper.qkv"), "dil", pick("diffsvc.dilated"), "outproj", pick("diffsvc.outproj"), "roof_us", d["roofline"].get("avg_launch_us"), flush=True)
 PY
   done
 done

@@ -1,4 +1,4 @@
-# Round-3 profile of record at HEAD (run from the repo root via gpurun): bench line with the CPU baseline, rocprofv3
+# Profile of record at HEAD (run from the repo root via gpurun): bench line with the CPU baseline, rocprofv3
 # kernel-trace stats, FETCH_SIZE / WRITE_SIZE passes on the roofline kernel (tools/gpu_profile.sh), then the per-kernel
 # PMC passes (MFMA busy, VALU / MFMA, LDS conflicts, HBM bytes: tools/pmc_kernels.sh).
 set -o pipefail
