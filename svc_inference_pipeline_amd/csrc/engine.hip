@@ -106,8 +106,10 @@ int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s, bool bf);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
-int res_proj(const f16* g, const f16* W, int ldw, const float* bias, const float* sub, const float* add, float div,
-             f16* hi, f16* lo, int M, bool bf16, int grid_cap, hipStream_t s);
+int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, const float* add, float div, f16* hi,
+             f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s);
+int res_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
+size_t res_proj_pack_elems();
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
               int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
               bool bf16);
@@ -236,6 +238,7 @@ struct PackedGemm {
   int N = 0, Npad = 0, K = 0, Kpad = 0, Cp = 0, Cin = 0, taps = 0;
   int tap_mul = 1, tap_add = 0, istride = 1;
   bool bf16 = false;  // W (and so the GEMM's operands) in bfloat16 (the bf16 operand variant, common.h Op16)
+  f16* Wfrag = nullptr;  // the DiffSVC residual projections: W in res_proj's fragment order (res_proj.hip)
 };
 
 // host-side rounding of a weight to the 16-bit operand format: binary16 (default) or bfloat16 (round to nearest even)
@@ -1040,6 +1043,15 @@ int build_mapper(svc_ctx* c) {
     if ((st = pack_conv1d(c, c->dil[i], dw->host, db->host, 2 * C, C, 3, C, d, d, 1, &perm))) return st;
     // rows 0..C-1 of output_projection are the residual, C..2C-1 the skip (modules/diffsvc.py:229-231)
     if ((st = pack_conv1d(c, c->outres[i], ow->host, ob->host, C, C, 1, C, 1, 0, 1))) return st;
+    if (C == 384) {  // res_proj's shape: its weights once more, in MFMA fragment order
+      void* wf = nullptr;
+      SVC_HIP_CHECK(hipMalloc(&wf, res_proj_pack_elems() * sizeof(f16)));
+      c->allocs.push_back(wf);
+      c->weight_bytes += (int64_t)(res_proj_pack_elems() * sizeof(f16));
+      c->outres[i].Wfrag = reinterpret_cast<f16*>(wf);
+      if ((st = res_proj_pack(c->outres[i].W, c->outres[i].Kpad, c->outres[i].Wfrag, 0))) return st;
+      SVC_HIP_CHECK(hipStreamSynchronize(0));
+    }
     opw_l[i] = ow;
     opb_l[i] = ob;
   }
@@ -2028,10 +2040,10 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
     // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step):
     // x_i = (y16 + lo16) - dproj_i, and x_{i+1} + dproj_{i+1} goes back split into y16 / lo16
-    if (tuning().res_proj && C == 384 && c->outres[i].N == C && c->outres[i].K == C && c->outres[i].Kpad >= C) {
+    if (tuning().res_proj && C == 384 && c->outres[i].Wfrag && c->outres[i].N == C && c->outres[i].K == C) {
       // weight-stationary row stream (res_proj.hip), bit-identical to the tiled GEMM below
       prof_site("diffsvc.outproj");
-      if ((st = res_proj(bb.g16 + (size_t)i * bb.g_ls, c->outres[i].W, c->outres[i].Kpad, c->outres[i].bias,
+      if ((st = res_proj(bb.g16 + (size_t)i * bb.g_ls, c->outres[i].Wfrag, c->outres[i].bias,
                          dp + (size_t)i * C, dp + (size_t)(i + 1) * C, 1.41421356237309515f, bb.y16, bb.lo16, rows,
                          c->outres[i].bf16, tuning().res_proj > 1 ? tuning().res_proj : 0, s)))
         return st;
@@ -2770,6 +2782,11 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
       e.ld_acc = N; e.acc_div = 1.41421356237309515f; e.add16 = bias;
     }
   }
+  f16* Wf = nullptr;  // variant 30: res_proj's fragment-order weights
+  if (variant == 30) {
+    SVC_HIP_CHECK(hipMalloc(&Wf, res_proj_pack_elems() * sizeof(f16)));
+    if (int stp = res_proj_pack(W, Kpad, Wf, 0)) return stp;
+  }
   hipEvent_t e0, e1;
   SVC_HIP_CHECK(hipEventCreate(&e0));
   SVC_HIP_CHECK(hipEventCreate(&e1));
@@ -2783,8 +2800,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   if (const char* fm = getenv("SVC_BENCH_FLUSH_MB")) flush_bytes = (size_t)atoi(fm) << 20;  // (bench tool only)
   if (cold) SVC_HIP_CHECK(hipMalloc(&flush, flush_bytes));
   auto run = [&]() {
-    if (variant == 30)
-      return res_proj(X, W, Kpad, bias, bias, bias, e.acc_div, Y, reinterpret_cast<f16*>(R), M, false, 0, 0);
+    if (variant == 30) return res_proj(X, Wf, bias, bias, bias, e.acc_div, Y, reinterpret_cast<f16*>(R), M, false, 0, 0);
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
     return conv_gemm3(a, e, zero_page(), variant - 10, 0);
   };
@@ -2813,6 +2829,6 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   *ms_out = ms / iters;
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
-  for (void* p : {(void*)X, (void*)W, (void*)Y, (void*)cp, (void*)bias, (void*)R}) if (p) (void)hipFree(p);
+  for (void* p : {(void*)X, (void*)W, (void*)Y, (void*)cp, (void*)bias, (void*)R, (void*)Wf}) if (p) (void)hipFree(p);
   return st;
 }

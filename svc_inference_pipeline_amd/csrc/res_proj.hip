@@ -42,8 +42,7 @@ constexpr uint32_t RP_CFG = 0x00020000u;  // buffer descriptor dword 3 (raw, 32-
 
 struct ResProjArgs {
   const f16* g;       // [M][384] gate outputs of the layer
-  const f16* W;       // packed W_res [>= 384][ldw], W[n][k]
-  int ldw;
+  const f16* Wf;      // W_res in fragment order (res_proj_pack)
   const float* bias;  // [384]
   const float* sub;   // dproj_i [384]
   const float* add;   // dproj_{i+1} [384]
@@ -141,11 +140,12 @@ __global__ __launch_bounds__(RP_NT, 1) void res_proj_kernel(ResProjArgs p) {
   const int half = (b >> 3) & 1, rlane = (b & 7) | ((b >> 4) << 3);
   const int n0 = half * RP_H + 16 * wave;  // this wave's output columns n0 .. n0 + 15; the lane's: n0 + 4 fk .. + 3
 
-  // W fragments of the swapped MFMA (its A operand): w[kc] = W[n0 + fr][kc * 32 + fk * 8 .. + 8]
+  // W fragments of the swapped MFMA (its A operand): w[kc] = W[n0 + fr][kc * 32 + fk * 8 .. + 8], stored in fragment
+  // order by res_proj_pack so that each of the 12 loads is one contiguous KiB per wave
   half8 w[12];
+  const f16* wf = p.Wf + (size_t)(half * RP_NW + wave) * 12 * 64 * 8 + lane * 8;
 #pragma unroll
-  for (int kc = 0; kc < 12; ++kc)
-    w[kc] = *reinterpret_cast<const half8*>(p.W + (int64_t)(n0 + fr) * p.ldw + kc * 32 + fk * 8);
+  for (int kc = 0; kc < 12; ++kc) w[kc] = *reinterpret_cast<const half8*>(wf + kc * 64 * 8);
   const float4 bi = *reinterpret_cast<const float4*>(p.bias + n0 + 4 * fk);
   const float4 sb = *reinterpret_cast<const float4*>(p.sub + n0 + 4 * fk);
   const float4 ad = *reinterpret_cast<const float4*>(p.add + n0 + 4 * fk);
@@ -229,15 +229,33 @@ __global__ __launch_bounds__(RP_NT, 1) void res_proj_kernel(ResProjArgs p) {
   rp_vmwait<0>();  // (the remaining DMAs of tiles past the end land before the workgroup's LDS is released)
 }
 
-// M rows of the split residual update for one layer; W: packed [>= 384][ldw] weights of the residual half.
+// W_res (packed [>= 384][ldw], W[n][k]) -> fragment order Wf[half][wave][kc][lane][8]: 16 B per thread
+__global__ void res_proj_pack_kernel(const f16* __restrict__ W, int ldw, f16* __restrict__ Wf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= RP_C * RP_C / 8) return;
+  const int lane = i & 63, kc = (i >> 6) % 12, hw = (i >> 6) / 12, wave = hw % RP_NW, half = hw / RP_NW;
+  const int n = half * RP_H + 16 * wave + (lane & 15), k = kc * 32 + (lane >> 4) * 8;
+  *reinterpret_cast<uint4*>(Wf + (size_t)i * 8) = *reinterpret_cast<const uint4*>(W + (size_t)n * ldw + k);
+}
+
+int res_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s) {
+  SVC_REQUIRE(ldw >= RP_C && ldw % 8 == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)Wf & 15) == 0,
+              "res_proj_pack: ldw %d", ldw);
+  hipLaunchKernelGGL(res_proj_pack_kernel, dim3(cdiv(RP_C * RP_C / 8, 256)), dim3(256), 0, s, W, ldw, Wf);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+size_t res_proj_pack_elems() { return (size_t)RP_C * RP_C; }
+
+// M rows of the split residual update for one layer; Wf: W_res in fragment order (res_proj_pack).
 // lanes_cap > 0: that many row lanes (2 workgroups each) instead of one workgroup per CU
-int res_proj(const f16* g, const f16* W, int ldw, const float* bias, const float* sub, const float* add, float div,
-             f16* hi, f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s) {
-  SVC_REQUIRE(M >= 0 && ldw >= RP_C && ldw % 8 == 0, "res_proj: M %d ldw %d", M, ldw);
+int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, const float* add, float div, f16* hi,
+             f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s) {
+  SVC_REQUIRE(M >= 0 && Wf, "res_proj: M %d, packed weights %p", M, (const void*)Wf);
   SVC_REQUIRE(div == RP_SQRT2, "res_proj: the residual divisor is sqrt(2) (modules/diffsvc.py:232)");
   if (M == 0) return SVC_OK;
   SVC_REQUIRE((int64_t)M * RP_C * 2 < (1ll << 31) - (1 << 20), "res_proj: %d rows exceed the 32-bit buffer range", M);
-  SVC_REQUIRE(((uintptr_t)g & 15) == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)hi & 15) == 0 &&
+  SVC_REQUIRE(((uintptr_t)g & 15) == 0 && ((uintptr_t)Wf & 15) == 0 && ((uintptr_t)hi & 15) == 0 &&
                   ((uintptr_t)lo & 15) == 0,
               "res_proj: 16-B alignment");
   static int ncu = 0;
@@ -254,7 +272,7 @@ int res_proj(const f16* g, const f16* W, int ldw, const float* bias, const float
   int lanes = lanes_cap > 0 ? lanes_cap : ncu * 3 / 8;
   lanes = std::max(8, std::min(lanes, (int)round_up(tiles, 8)));
   lanes = (int)round_up(lanes, 8);
-  ResProjArgs a{g, W, ldw, bias, sub, add, div, hi, lo, M, lanes, cdiv(tiles, lanes)};
+  ResProjArgs a{g, Wf, bias, sub, add, div, hi, lo, M, lanes, cdiv(tiles, lanes)};
   // ring depth 3 (two tiles in flight): 4 / 5 slots measured no faster alone or in the sampler (r03k), 2 slots 4 % slower
   // end to end (r03o)
   constexpr int depth = 3;

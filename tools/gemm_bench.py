@@ -45,8 +45,10 @@ def main():
             iters = -10 if os.environ.get("GEMM_BENCH_COLD") == "1" else 10
             try:
                 _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, iters, ctypes.byref(ms))
-            except _lib.SVCError:  # the library rejects this (variant, epilogue) pair before launching
+            except _lib.SVCError as err:  # the library rejects this (variant, epilogue) pair before launching
                 row.append(f"v{v}: {'n/a':>27s}")
+                if os.environ.get("GEMM_BENCH_VERBOSE"):
+                    print(f"  (v{v} on {name}: {err})", file=sys.stderr)
                 continue
             tf = 2.0 * M * N * Cin * taps / (ms.value * 1e-3) / 1e12
             row.append(f"v{v}: {ms.value * 1000:8.1f} us {tf:7.1f} TF")
