@@ -2769,7 +2769,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   a.tap_mul = 1; a.tap_add = -(taps / 2); a.istride = 1; a.B = 1; a.T_out = M; a.N = N;
   EpiArgs e = epi();
   e.bias = bias; e.T_ostore = M; e.ostride = 1;
-  if (epi_kind == 1 || epi_kind >= 3) {  // diagnostics: 3 = no cp read, no y store; 4 = no cp read; 5 = no y store
+  if (epi_kind == 1 || (epi_kind >= 3 && epi_kind <= 5)) {  // diagnostics: 3 = no cp read, no y store; 4 = no cp read; 5 = no y store
     e.kind = EPI_GATE; e.cp = (epi_kind == 3 || epi_kind == 4) ? nullptr : cp; e.ld_cp = N;
     e.y16 = (epi_kind == 3 || epi_kind == 5) ? nullptr : Y;
     e.ldy16 = N / 2;
