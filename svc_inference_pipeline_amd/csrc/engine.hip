@@ -699,6 +699,10 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
       }
   }
   if (variant == 15 && pair) variant = 24;
+  // The skip-sum GEMM of a sampler sub-batch (K = 20 x 384, M <= 20 k rows) takes conv_gemm3's 256 x 128 tile although
+  // pick3's fit prefers narrower-M tiles alone: beside the other sampler stream it measured +1.5 % end to end (826-828
+  // vs 813-818 audio-s/s in three alternating rounds, profiles/r03w_skipsum_tile_ab.txt)
+  if (variant == 15 && site && strcmp(site, "diffsvc.skipsum") == 0 && (int64_t)B * T_out <= 20000) variant = 12;
   SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24, "gemm_variant %d: 10..15, 20 or 24",
               variant);
   // N <= 64 (the last BigVGAN up-sampling phases, 48 / 24 channels) takes conv_gemm3's 128 x 128 tile: 1.9 vs
