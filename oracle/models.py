@@ -307,6 +307,8 @@ def bigvgan_forward(sd, vcfg, mel):
                     continue
                 xt = _act(sd, rb + f"activations.{2 * l}", xr, ls)
                 xt = F.conv1d(xt, _wn(sd, rb + f"convs1.{l}"), _t(sd, rb + f"convs1.{l}.bias"), dilation=d, padding=(kk * d - d) // 2)
+                if _STORE16[0]:  # (fp16 emulation only: the HIP path stores this intermediate as saturating f16)
+                    xt = xt.clamp(-65504.0, 65504.0).half().float()
                 xt = _act(sd, rb + f"activations.{2 * l + 1}", xt, ls)
                 xt = F.conv1d(xt, _wn(sd, rb + f"convs2.{l}"), _t(sd, rb + f"convs2.{l}.bias"), padding=(kk - 1) // 2)
                 xr = xt + xr
@@ -318,6 +320,9 @@ def bigvgan_forward(sd, vcfg, mel):
 
 
 # ============================================================================ fp16-operand emulation
+_STORE16 = [False]  # set inside Fp16Operands: BigVGAN's AMPBlock1 intermediate rounded to f16 as the HIP path stores it
+
+
 class OperandRounding:
     """Context manager: dense convolutions (and, with `linear=True`, F.linear and the attention matmuls of
     the functional encoders) round their input and weight to `dtype` (float16 / bfloat16) and accumulate in
@@ -357,7 +362,16 @@ class OperandRounding:
 
 
 class Fp16Operands(OperandRounding):
-    """fp16 conv operands (the BigVGAN tolerance derivation)."""
+    """fp16 conv operands (the BigVGAN tolerance derivation), and the f16 storage of AMPBlock1's convs1 output that the
+    HIP vocoder uses (engine.hip, round 3)."""
 
     def __init__(self):
         super().__init__(torch.float16, linear=False)
+
+    def __enter__(self):
+        _STORE16[0] = True
+        return super().__enter__()
+
+    def __exit__(self, *a):
+        _STORE16[0] = False
+        return super().__exit__(*a)

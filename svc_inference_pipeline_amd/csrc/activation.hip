@@ -1,5 +1,5 @@
-// BigVGAN Activation1d (anti-aliased SnakeBeta) on gfx950, HBM-bound: read x (f32) once, write y (f16)
-// once. modules/bigvgan.py:234-307 + SnakeBeta :146-159, per channel sequence x[0..L-1]:
+// BigVGAN Activation1d (anti-aliased SnakeBeta) on gfx950, HBM-bound: read x (f32, or f16 for an AMPBlock1
+// intermediate) once, write y (f16) once. modules/bigvgan.py:234-307 + SnakeBeta :146-159, per channel sequence x[0..L-1]:
 //   u[2q]   = 2 * sum_{a=0..5} x[clamp(q-3+a)] * f[11-2a]      (UpSample1d: replicate pad 5, crop 15)
 //   u[2q+1] = 2 * sum_{a=0..5} x[clamp(q-2+a)] * f[10-2a]
 //   s[j]    = u + 1/(exp(beta)+1e-9) * sin(u*exp(alpha))^2
@@ -18,8 +18,8 @@ namespace svc {
 // barriers; loads are coalesced across lanes (adjacent lanes = adjacent channel groups). Window values
 // are computed from replicate-clamped x loads, which is exact for every upsampled index inside [0, 2L-1];
 // indices outside take their neighbour's value (the low-pass filter's replicate padding).
-template <int VEC, int P, int R>
-__global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __restrict__ x, f16* __restrict__ y,
+template <int VEC, int P, int R, typename TX = float>
+__global__ __launch_bounds__(256) void activation1d_rs_kernel(const TX* __restrict__ x, f16* __restrict__ y,
                                                               int B, int L, int C, int ldy,
                                                               const float* __restrict__ alpha_log,
                                                               const float* __restrict__ beta_log,
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
   const int64_t rest = gid / ngroups;
   const int run = (int)(rest % nruns), b = (int)(rest / nruns);
   const int c = g * VEC;
-  const float* xb = x + (int64_t)b * L * C + c;
+  const TX* xb = x + (int64_t)b * L * C + c;
   f16* yb = y + (int64_t)b * L * ldy + c;
   // ragged batches: this utterance's sequence ends at Lb (replicate padding there); rows keep the stride L
   const int Lb = tv ? min(L, tv[b] * tv_mul) : L;
@@ -131,23 +131,28 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const float* __res
   }
 }
 
-template <int VEC, int P, int R>
-static void launch_rs(const float* x, f16* y, int B, int L, int C, int ldy, const float* al, const float* bl,
+template <int VEC, int P, int R, typename TX>
+static void launch_rs(const TX* x, f16* y, int B, int L, int C, int ldy, const float* al, const float* bl,
                       const float* filt, const int* tv, int tv_mul, hipStream_t s) {
   const int64_t n = (int64_t)B * cdiv(L, R) * (C / VEC);
-  hipLaunchKernelGGL((activation1d_rs_kernel<VEC, P, R>), dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, y, B, L,
-                     C, ldy, al, bl, filt, tv, tv_mul);
+  hipLaunchKernelGGL((activation1d_rs_kernel<VEC, P, R, TX>), dim3((unsigned)cdiv64(n, 256)), dim3(256), 0, s, x, y, B,
+                     L, C, ldy, al, bl, filt, tv, tv_mul);
 }
 
-// tv / tv_mul (optional): ragged batches, utterance b's sequence is min(L, tv[b] * tv_mul) rows long
+// tv / tv_mul (optional): ragged batches, utterance b's sequence is min(L, tv[b] * tv_mul) rows long.
+// x is f32 (the generator's residual stream) or f16 (x16: an AMPBlock1 convs1 output, stored f16)
 int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const float* alpha_log, const float* beta_log,
-                 const float* filt, hipStream_t s, const int* tv, int tv_mul) {
+                 const float* filt, hipStream_t s, const int* tv, int tv_mul, const f16* x16) {
   SVC_REQUIRE(L >= 1 && C >= 4 && C % 4 == 0 && ldy % 4 == 0, "activation1d: L=%d C=%d ldy=%d", L, C, ldy);
-  SVC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0, "activation1d: alignment");
-  const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * (4 + 2), s);
+  SVC_REQUIRE(((uintptr_t)(x16 ? (const void*)x16 : (const void*)x) & 15) == 0 && ((uintptr_t)y & 7) == 0,
+              "activation1d: alignment");
+  const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * ((x16 ? 2 : 4) + 2), s);
   // 2 channels per thread, 8-output blocks, 128-output runs: the fastest of the register-streaming shapes and of an
   // LDS-tiled form measured in rounds 1-2 (4.0-4.1 TB/s; the others were removed in round 3)
-  launch_rs<2, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
+  if (x16)
+    launch_rs<2, 8, 128>(x16, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
+  else
+    launch_rs<2, 8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;

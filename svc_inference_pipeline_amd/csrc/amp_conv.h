@@ -15,6 +15,7 @@ struct AmpConvArgs {
   const float* bias;
   const int* tv = nullptr;  // ragged batches: utterance b has min(L, tv[b] * tv_mul) rows (NULL = all L)
   int tv_mul = 1;
+  const f16* x16 = nullptr;  // when set, the activation input is this f16 tensor instead of x (an AMPBlock1 intermediate)
 };
 
 bool amp_conv_supported(int C, int k, int d);

@@ -14,6 +14,8 @@
 //      bias, residual add (add_row), resblock mean accumulation (acc32 / acc_div), f32 and/or f16 stores as 16-B /
 //      8-B vectors. No C staging, so LDS holds only the activation image and more workgroups share a CU.
 // The activation never round-trips through HBM, and every HBM access is a coalesced 16-byte stream.
+#include <type_traits>
+
 #include "common.h"
 #include "snake.h"
 #include "amp_conv.h"
@@ -41,7 +43,7 @@ constexpr int AMP_NT = 256;
 // The activation of C <= 48 runs on channel pairs with packed f32 FMAs (v_pk_fma_f32) in 4-row blocks, C = 96 on
 // single channels in 8-row blocks. Round 1 measured these forms 7-20 % faster per launch than the unbounded
 // single-channel form (tools/amp_bench.py); the earlier forms were removed in round 3.
-template <int C>
+template <int C, bool X16 = false>
 __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
   using CF = AmpCfg<C>;
   extern __shared__ __align__(16) unsigned char amp_sm[];
@@ -71,7 +73,8 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
     const int nr_fit = max(1, AMP_NT / ngrp);
     const int RUN = ((rows + nr_fit - 1) / nr_fit + BLK - 1) / BLK * BLK;
     const int nruns = (rows + RUN - 1) / RUN;
-    const float* xb = p.x + (int64_t)b * L * C;
+    using TX = typename std::conditional<X16, f16, float>::type;
+    const TX* xb = (X16 ? (const TX*)(const void*)p.x16 : (const TX*)(const void*)p.x) + (int64_t)b * L * C;
     for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
       const int cg = task % ngrp, ru = task / ngrp;
       const int c = cg * VEC;
@@ -254,27 +257,28 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
   }
 }
 
-template <int C>
+template <int C, bool X16>
 static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   using CF = AmpCfg<C>;
   static bool attr = false;
   if (!attr) {
-    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)amp_conv_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      CF::LDS));
+    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)amp_conv_kernel<C, X16>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS));
     attr = true;
   }
   const int64_t grid = (int64_t)p.B * cdiv(p.L, CF::BT);
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "amp_conv: bad grid");
   const double elems = (double)p.B * p.L * C;
-  // algorithmic bytes: x in (f32), output out (f32 and/or f16), epilogue operands in (f32)
-  const double bytes = elems * (4.0 + (e.out32 ? 4 : 0) + (e.out16 ? 2 : 0) + (e.add_row ? 4 : 0) + (e.acc32 ? 4 : 0));
+  // algorithmic bytes: x in (f32 or f16), output out (f32 and/or f16), epilogue operands in (f32)
+  const double bytes =
+      elems * ((X16 ? 2.0 : 4.0) + (e.out32 ? 4 : 0) + (e.out16 ? 2 : 0) + (e.add_row ? 4 : 0) + (e.acc32 ? 4 : 0));
   const char* tag = C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>");
   const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
   // the activation image needs BT + 2P rows, not BT + 2 MAXP: sized per launch, C = 48 fits 5 workgroups per CU
   // (instead of 4) for every conv with P <= 15
   const int P = (p.k - 1) / 2 * p.d;
   const int lds = (CF::BT + 2 * P) * CF::LDA * 2;
-  hipLaunchKernelGGL((amp_conv_kernel<C>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, p, e);
+  hipLaunchKernelGGL((amp_conv_kernel<C, X16>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, p, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
@@ -291,10 +295,16 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
   SVC_REQUIRE((!e.out32 || e.ld32 == C) && (!e.out16 || e.ld16 == C) && (!e.add_row || e.ld_add_row == C) &&
                   (!e.acc32 || e.ld_acc == C) && !e.add16 && e.act == ACT_NONE && e.kind == EPI_GENERIC,
               "amp_conv: epilogue must be contiguous rows of C channels (bias / add_row / acc32 / out32 / out16)");
-  SVC_REQUIRE(((uintptr_t)p.x & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "amp_conv: alignment");
-  if (C == 24) return launch_amp<24>(p, e, s);
-  if (C == 48) return launch_amp<48>(p, e, s);
-  return launch_amp<96>(p, e, s);
+  const void* xin = p.x16 ? (const void*)p.x16 : (const void*)p.x;
+  SVC_REQUIRE(((uintptr_t)xin & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "amp_conv: alignment");
+  if (p.x16) {
+    if (C == 24) return launch_amp<24, true>(p, e, s);
+    if (C == 48) return launch_amp<48, true>(p, e, s);
+    return launch_amp<96, true>(p, e, s);
+  }
+  if (C == 24) return launch_amp<24, false>(p, e, s);
+  if (C == 48) return launch_amp<48, false>(p, e, s);
+  return launch_amp<96, false>(p, e, s);
 }
 
 }  // namespace svc

@@ -78,7 +78,7 @@ int layernorm_f16(const float* x, const float* g, const float* b, f16* y, int ro
                   bool bf);
 int layernorm_f32(const float* x, const float* g, const float* b, float* y, int rows, int D, int ldy, hipStream_t s);
 int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const float* alpha_log, const float* beta_log,
-                 const float* filt, hipStream_t s, const int* tv = nullptr, int tv_mul = 1);
+                 const float* filt, hipStream_t s, const int* tv = nullptr, int tv_mul = 1, const f16* x16 = nullptr);
 int f32_to_f16(const float* x, int ldx, f16* y, int ldy, int rows, int C, int Cpad, hipStream_t s, bool bf);
 int denorm_mel(const float* x, f16* y, float* y32, int ldy, int rows, int C, const float* mn, const float* mx,
                hipStream_t s);
@@ -2484,13 +2484,17 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
           // AMPBlock1: tmp = c1(a1(x)), x' = x + c2(a2(tmp)); AMPBlock2: x' = x + c(a(x)) with c = c2[l] (dilation d)
           const bool rb2 = c->v_rb2;
           const int d2 = rb2 ? S.rd[j][l] : 1;
-          const float* act_in = rb2 ? src : tmph;  // input of the activation before the second (or only) conv
+          // AMPBlock1's intermediate c1(a1(x)) is stored f16 (tmp16, in tmp's memory): it is read once, by a2, whose
+          // output is rounded to the f16 MFMA operand anyway; 4 B less per element read and written (round 3)
+          f16* tmp16 = reinterpret_cast<f16*>(tmph);
+          const float* act_in = rb2 ? src : nullptr;  // input of the activation before the second (or only) conv
+          const f16* act_in16 = rb2 ? nullptr : tmp16;
           // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
           const bool fuse = ch <= amp_maxc && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
           if (!rb2) {
             EpiArgs e1 = epi();
-            e1.out32 = tmph;
-            e1.ld32 = ch;
+            e1.out16 = tmp16;
+            e1.ld16 = ch;
             if (fuse) {
               const PackedGemm& g1 = S.c1[j][l];
               AmpConvArgs p1{src, Bh, L, S.rk[j], S.rd[j][l], a1.alpha, a1.beta, a1.filt, g1.W, g1.Kpad, g1.bias};
@@ -2503,7 +2507,8 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
               if ((st = run_gemm(S.c1[j][l], a16h, ch, ch, Bh, L, L, e1, sh, "bigvgan.amp_c1", tvh, mul))) return st;
             }
           }
-          if (!fuse && (st = activation1d(act_in, a16h, Bh, L, ch, ch, a2.alpha, a2.beta, a2.filt, sh, tvh, mul)))
+          if (!fuse &&
+              (st = activation1d(act_in, a16h, Bh, L, ch, ch, a2.alpha, a2.beta, a2.filt, sh, tvh, mul, act_in16)))
             return st;
           EpiArgs e2 = epi();
           e2.add_row = src;
@@ -2536,6 +2541,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
             AmpConvArgs p2{act_in, Bh, L, S.rk[j], d2, a2.alpha, a2.beta, a2.filt, g2.W, g2.Kpad, g2.bias};
             p2.tv = tvh;
             p2.tv_mul = mul;
+            p2.x16 = act_in16;
             prof_site("bigvgan.amp_c2");
             if ((st = amp_conv(p2, ch, e2, sh))) return st;
           } else if ((st = run_gemm(S.c2[j][l], a16h, ch, ch, Bh, L, L, e2, sh, "bigvgan.amp_c2", tvh, mul))) {
