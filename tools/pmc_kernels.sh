@@ -15,7 +15,7 @@ for set in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "$KRE" -f csv -d $O/p$i -o run -- \
+  timeout -k 10 ${PASS_TIMEOUT:-300} rocprofv3 --pmc $set --kernel-include-regex "$KRE" -f csv -d $O/p$i -o run -- \
     python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline > $O/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 $O/p$i.log; exit 1; }
   echo "pass $i done"
 done
