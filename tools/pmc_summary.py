@@ -58,6 +58,9 @@ def counter_rows(d):
     return rows
 
 
+WG_SIZE = {}  # kernel tag -> threads per workgroup, from the counter rows
+
+
 def per_kernel(rows, counter):
     """{kernel tag: {grid size in threads: [counter value per dispatch]}}"""
     acc = {}
@@ -65,6 +68,7 @@ def per_kernel(rows, counter):
         if r.get("Counter_Name") != counter:
             continue
         k = short(r.get("Kernel_Name", ""))
+        WG_SIZE[k] = int(r.get("Workgroup_Size") or 256)
         acc.setdefault(k, {}).setdefault(int(r.get("Grid_Size", 0)), []).append(float(r["Counter_Value"]))
     return acc
 
@@ -102,7 +106,7 @@ def main():
         for g in grids:
             f, w = fetch.get(k, {}).get(g, []), write.get(k, {}).get(g, [])
             fk, wk = mean(f), mean(w)
-            e = {"workgroups": g // 256, "dispatches": max(len(f), len(w)), "fetch_kib_per_launch": fk,
+            e = {"workgroups": g // WG_SIZE.get(k, 256), "dispatches": max(len(f), len(w)), "fetch_kib_per_launch": fk,
                  "write_kib_per_launch": wk, "hbm_bytes_per_launch": (2 * fk + wk) * 1024.0}
             if g in trace.get(k, {}):
                 e["rocprof_trace_dispatches"], ns = trace[k][g]
