@@ -1,5 +1,5 @@
 # Same-box A/B of ab/libsvc_hip_base.so against the in-tree library (run from the repo root via gpurun):
-# parity tests on the new build ($TESTS, -k $TESTK), then alternating microbenchmarks ($MICRO: att, gate, outproj)
+# parity tests on the new build ($TESTS, -k $TESTK), then alternating microbenchmarks ($MICRO: att, gate, outproj, g3, amp)
 # and quick benches (ROUNDS).
 set -o pipefail
 O=gpurun_out/${TAG:-ab_lib}; mkdir -p $O
@@ -15,6 +15,7 @@ for r in 1 2; do
         att) SVC_HIP_LIB=$L timeout -k 10 120 python3 tools/att_bench.py > $O/m.txt 2>&1 || exit $? ;;
         gate) SVC_HIP_LIB=$L GEMM_BENCH_SHAPES="dilated(gate)" timeout -k 10 120 python3 tools/gemm_bench.py 24 > $O/m.txt 2>&1 || exit $? ;;
         outproj) SVC_HIP_LIB=$L GEMM_BENCH_TORCH=0 GEMM_BENCH_SHAPES="outproj(split" timeout -k 10 120 python3 tools/gemm_bench.py 15 30 > $O/m.txt 2>&1 || exit $? ;;
+        amp) SVC_HIP_LIB=$L timeout -k 10 180 python3 tools/amp_bench.py > $O/m.txt 2>&1 || exit $? ;;
         g3) SVC_HIP_LIB=$L GEMM_BENCH_SHAPES="outproj(split,whisper.fc,skipsum,bigvgan.s2" timeout -k 10 180 python3 tools/gemm_bench.py 15 > $O/m.txt 2>&1 || exit $? ;;
       esac
       grep -v amdgpu $O/m.txt | sed "s/^/$lib $m: /"
