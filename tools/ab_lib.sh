@@ -31,7 +31,8 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 k = d["kernels"]
 pick = lambda s: round(sum(v["ms_per_step"] for kk, v in k.items() if kk.endswith("@" + s)), 3)
-print(sys.argv[2], d["value"], d["ms_per_step"], "att", pick("whisper.qkv"), "dil", pick("diffsvc.dilated"), "outproj", pick("diffsvc.outproj"), "roof_us", d["roofline"].get("avg_launch_us"), flush=True)
+kind = lambda s: round(sum(v["ms_per_step"] for kk, v in k.items() if kk.startswith(s)), 3)
+print(sys.argv[2], d["value"], d["ms_per_step"], "att", pick("whisper.qkv"), "dil", pick("diffsvc.dilated"), "outproj", pick("diffsvc.outproj"), "roof_us", d["roofline"].get("avg_launch_us"), "act", kind("activation1d"), "amp", kind("amp_conv"), flush=True)
 PY
   done
 done
