@@ -1,5 +1,8 @@
 """GEMM kernel microbenchmark (GPU): TFLOP/s of the implicit-GEMM variants on the hot-path shapes.
-Usage: python tools/gemm_bench.py [variant ...]   (30: res_proj.hip, on the split residual shapes only)"""
+Usage: python tools/gemm_bench.py [variant ...]   (30: res_proj.hip, on the split residual shapes only)
+GEMM_BENCH_WARM=1: each measurement (ours and torch.mm) follows 30 untimed launches of the same GEMM, so it is taken at
+sustained clocks (the default times 10 launches after 2 warm-ups, while the clocks may still be ramping).
+GEMM_BENCH_COLD=1: each launch after a 1 GiB memset (operands not cache-resident, as in the sampler)."""
 import ctypes
 import os
 import sys
@@ -44,6 +47,8 @@ def main():
             # GEMM_BENCH_COLD=1: each launch after a 1 GiB memset (operands not cache-resident, as in the sampler)
             iters = -10 if os.environ.get("GEMM_BENCH_COLD") == "1" else 10
             try:
+                if os.environ.get("GEMM_BENCH_WARM") == "1":
+                    _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, 30, ctypes.byref(ms))
                 _lib.call("svc_gemm_bench", M, N, Cin, taps, epi, v, iters, ctypes.byref(ms))
             except _lib.SVCError as err:  # the library rejects this (variant, epilogue) pair before launching
                 row.append(f"v{v}: {'n/a':>27s}")
@@ -56,7 +61,8 @@ def main():
             # hipBLASLt yardstick (plain GEMM, K = taps * Cin, no epilogue), same shape
             a = torch.randn(M, Cin * taps, device="cuda", dtype=torch.float16)
             b = torch.randn(Cin * taps, N, device="cuda", dtype=torch.float16)
-            torch.mm(a, b)
+            for _ in range(30 if os.environ.get("GEMM_BENCH_WARM") == "1" else 1):
+                torch.mm(a, b)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(10):
