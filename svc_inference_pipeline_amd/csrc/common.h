@@ -286,6 +286,7 @@ struct Tuning {
   int amp_maxc = 48;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none)
   int res_proj = 1;         // DiffSVC residual projection on the weight-stationary stream (res_proj.hip; 0: conv_gemm3;
                             // > 1: that many row lanes of 2 workgroups instead of 3/8 of the CU count)
+  int gate_ws = 0;          // DiffSVC dilated conv + gate on the weight-stationary row stream (gate_ws.hip; 0: conv_gemm4)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only, A/B runs)
   void from_env();
   bool set(const char* name, double v);  // false: unknown name ("reset" restores the creation-time values)

@@ -106,6 +106,8 @@ int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
 int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s, bool bf);
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
+bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e);
+int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
 int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, const float* add, float div, f16* hi,
              f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s);
 int res_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
@@ -308,7 +310,8 @@ static int* tuning_field(T& t, const char* name) {
   } ints[] = {{"gemm_variant", &t.gemm_variant},       {"gemm3_direct", &t.gemm3_direct},
               {"whisper_streams", &t.whisper_streams}, {"sampler_streams", &t.sampler_streams},
               {"vocoder_streams", &t.vocoder_streams}, {"diff_head", &t.diff_head},
-              {"amp_maxc", &t.amp_maxc},               {"res_proj", &t.res_proj}};
+              {"amp_maxc", &t.amp_maxc},               {"res_proj", &t.res_proj},
+              {"gate_ws", &t.gate_ws}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) return it.v;
   return nullptr;
@@ -316,7 +319,7 @@ static int* tuning_field(T& t, const char* name) {
 
 void Tuning::from_env() {
   for (const char* name : {"gemm_variant", "gemm3_direct", "whisper_streams", "sampler_streams", "vocoder_streams",
-                           "diff_head", "amp_maxc", "res_proj"}) {
+                           "diff_head", "amp_maxc", "res_proj", "gate_ws"}) {
     std::string env = "SVC_";
     for (const char* q = name; *q; ++q) env += (char)toupper((unsigned char)*q);
     if (const char* v = getenv(env.c_str())) *tuning_field(*this, name) = atoi(v);
@@ -698,6 +701,8 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
         break;
       }
   }
+  // the DiffSVC dilated conv + gate: the weight-stationary row stream (gate_ws.hip) where it fits, else conv_gemm4
+  if (variant == 15 && pair && tu.gate_ws && gate_ws_fits(a, e)) return gate_ws(a, e, s);
   if (variant == 15 && pair) variant = 24;
   // The skip-sum GEMM of a sampler sub-batch (K = 20 x 384, M <= 20 k rows) takes conv_gemm3's 256 x 128 tile although
   // pick3's fit prefers narrower-M tiles alone: beside the other sampler stream it measured +1.5 % end to end (826-828
@@ -2756,8 +2761,10 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_REQUIRE(epi_kind < 3 || epi_kind == 6 || variant == 24,
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
   SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24 ||
-                  (variant == 30 && epi_kind == 6 && N == 384 && Cin == 384 && taps == 1),
-              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap)", variant);
+                  (variant == 30 && epi_kind == 6 && N == 384 && Cin == 384 && taps == 1) ||
+                  (variant == 40 && epi_kind == 1 && N == 768 && Cin == 384 && taps == 3),
+              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap; 40: gate_ws, gate "
+              "epilogue, N = 768, Cin = 384, 3 taps)", variant);
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float *bias, *R = nullptr;
@@ -2774,9 +2781,15 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   hipLaunchKernelGGL(fill_f16_kernel, dim3(cdiv((int64_t)M * Cin, 256)), dim3(256), 0, 0, X, (int64_t)M * Cin, 1u);
   hipLaunchKernelGGL(fill_f16_kernel, dim3(cdiv((int64_t)Npad * Kpad, 256)), dim3(256), 0, 0, W, (int64_t)Npad * Kpad, 2u);
   hipLaunchKernelGGL(fill_f16_kernel, dim3(cdiv((int64_t)M * N, 256)), dim3(256), 0, 0, cp, (int64_t)M * N, 3u);
+  // Y is also the residual hi half of the split epilogue (epi 6 / res_proj): defined values, no NaN / Inf patterns
+  hipLaunchKernelGGL(fill_f16_kernel, dim3(cdiv((int64_t)M * N, 256)), dim3(256), 0, 0, Y, (int64_t)M * N, 4u);
   ConvGemmArgs a{};
   a.X = X; a.ldx = Cin; a.T_in = M; a.Cp = Cin; a.Cvalid = Cin; a.W = W; a.K = K; a.Kpad = Kpad;
   a.tap_mul = 1; a.tap_add = -(taps / 2); a.istride = 1; a.B = 1; a.T_out = M; a.N = N;
+  if (const char* dv = getenv("SVC_BENCH_DIL")) {  // (bench tool only) the dilated conv's tap shift
+    a.tap_mul = atoi(dv);
+    a.tap_add = -(taps / 2) * a.tap_mul;
+  }
   EpiArgs e = epi();
   e.bias = bias; e.T_ostore = M; e.ostride = 1;
   if (epi_kind == 1 || (epi_kind >= 3 && epi_kind <= 5)) {  // diagnostics: 3 = no cp read, no y store; 4 = no cp read; 5 = no y store
@@ -2793,14 +2806,14 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
     }
   }
   f16* Wf = nullptr;  // variant 30: res_proj's fragment-order weights
+  int st = SVC_OK;
   if (variant == 30) {
     SVC_HIP_CHECK(hipMalloc(&Wf, res_proj_pack_elems() * sizeof(f16)));
-    if (int stp = res_proj_pack(W, Kpad, Wf, 0)) return stp;
+    st = res_proj_pack(W, Kpad, Wf, 0);  // (on failure: no launches below, the buffers are freed at the end)
   }
   hipEvent_t e0, e1;
   SVC_HIP_CHECK(hipEventCreate(&e0));
   SVC_HIP_CHECK(hipEventCreate(&e1));
-  int st = SVC_OK;
   // iters < 0: |iters| launches each after a 1 GiB (SVC_BENCH_FLUSH_MB) memset (operands evicted from L2 and the 256 MiB Infinity Cache,
   // as inside the sampler, where other layers' buffers stream between two launches of one GEMM), timed one by one
   const bool cold = iters < 0;
@@ -2812,9 +2825,19 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   auto run = [&]() {
     if (variant == 30) return res_proj(X, Wf, bias, bias, bias, e.acc_div, Y, reinterpret_cast<f16*>(R), M, false, 0, 0);
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
+    if (variant == 40) return gate_ws(a, e, 0);
     return conv_gemm3(a, e, zero_page(), variant - 10, 0);
   };
   for (int w = 0; w < 2 && !st; ++w) st = run();
+  if (const char* dump = getenv("SVC_BENCH_DUMP")) {  // (bench tool only) the gate output of the warm-up launches
+    SVC_HIP_CHECK(hipDeviceSynchronize());
+    std::vector<f16> hy((size_t)M * N / 2);
+    SVC_HIP_CHECK(hipMemcpy(hy.data(), Y, hy.size() * sizeof(f16), hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(dump, "wb")) {
+      fwrite(hy.data(), sizeof(f16), hy.size(), f);
+      fclose(f);
+    }
+  }
   float ms = 0;
   if (cold) {
     for (int i = 0; i < iters && !st; ++i) {

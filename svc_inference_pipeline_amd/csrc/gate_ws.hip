@@ -1,0 +1,355 @@
+// DiffSVC dilated conv + gate as a weight-stationary row stream (modules/diffsvc.py:212-227, `ResidualBlock.forward`
+// lines 220-227: y = dilated_conv(x + dproj) + conditioner_projection(cond); sigmoid(gate) * tanh(filter)), round 4.
+//
+// Per layer of every denoiser call: y[m][c] = sigmoid(g + cp_g) * tanh(f + cp_f), with
+//   [g | f] = conv1d_k3,dil(x16)  (K = 3 taps x 384 channels = 1152, 768 packed output columns, engine.hip pair_perm).
+// conv_gemm4 runs this as 128 x 128 output tiles, two 4-wave workgroups per CU, each K-tile DMA'd one step ahead: every
+// tile streams its A rows and its 128 weight columns through LDS (64 FLOP per operand byte), which at the MFMA rate is the
+// whole L2 -> LDS bandwidth of a CU (64 B per clock), so its K-loop runs at ~0.4 of the MFMA peak.
+// Here the weights stay put instead:
+//   * a workgroup owns 128 packed columns = 64 output channels, as 4 column sets of 16 gate + 16 filter columns; each set
+//     belongs to a PAIR of waves on one SIMD (waves w and w + 4): wave w holds the set's weights for K-steps 0..17 (tap
+//     0 and the first half of tap 1), wave w + 4 for K-steps 18..35, as MFMA fragments in VGPRs (36 x half8 = 144
+//     registers each: two waves per SIMD), loaded once per launch;
+//   * the workgroup walks its share of the rows in 16-row blocks: in step k the first wave of a pair runs K-steps 0..17
+//     of block k and hands its two f32 accumulators to its partner through LDS, which continues them over K-steps
+//     18..35 for block k - 1 (the partial sums are the partner's MFMA C operand, so the K order is one sequential chain,
+//     exactly conv_gemm4's) and applies the gate in registers; one workgroup barrier per step;
+//   * the input rows come through a ring of 160 rows in LDS, DMA'd in 32-row groups (25 KiB) once each: the three taps
+//     of a block read its rows at offsets -dil, 0, +dil, so no row is fetched twice, and a group is issued 5 steps
+//     before its first reader (the depth an HBM first touch under load needs at ~0.5 us per step);
+//   * an A fragment (ds_read_b128, 16 rows x 32 channels) feeds the set's gate and filter MFMA (v_mfma_f32_16x16x32,
+//     operands swapped so a lane's accumulator holds 4 consecutive columns of one row and a channel's gate and filter
+//     values sit in the same lane): 128 B per clock of LDS reads per CU at the MFMA rate, half the LDS's.
+// Roles: the first waves issue the ring DMAs (their only vector-memory operations after the prologue, so their vmcnt
+// waits are exact); the second waves load the conditioner projection (two blocks ahead), apply the gate and store.
+// Operand bytes per FLOP: the CU takes in 768 B per row for 128 x 1152 x 2 FLOP (384 FLOP per byte, 6x conv_gemm4).
+// The 6 column groups x 42 row parts = 252 workgroups fill a 256-CU chip once; the 6 workgroups of a row part are placed
+// on one XCD (blocks b, b + 8, ... share one under the observed round-robin placement, speed only), so each input row
+// is fetched into one L2.
+// Zero padding: an (output row, tap) whose input row lies outside its utterance (or past a ragged utterance's valid rows,
+// ConvGemmArgs::tv) reads its A fragments from a 768-B zero row in LDS, so every ring row serves all three taps and no
+// fragment needs a select.
+// Bit-identical to conv_gemm4<128,128,gate> (tests/test_gpu_stages.py test_gate_ws_bit_identical).
+#include "common.h"
+
+// gw_dma clobbers m0 (reserved for the compiler's own LDS-DMA and indexing uses, which all set it right before use)
+#pragma clang diagnostic ignored "-Winline-asm"
+
+namespace svc {
+
+constexpr int GW_C = 384;             // channels per tap
+constexpr int GW_N = 768;             // packed output columns (gate | filter per 64-column block)
+constexpr int GW_K = 3 * GW_C;        // 1152 = 36 K-steps of 32
+constexpr int GW_KH = 18;             // K-steps per wave of a pair
+constexpr int GW_HALO = 8;            // largest tap shift (dilation 8): ring row 0 = input row r_begin - 8
+constexpr int GW_GR = 32;             // rows per DMA group
+constexpr int GW_NG = 5;              // ring slots (groups): 160 rows
+constexpr int GW_RROWS = GW_NG * GW_GR;
+constexpr int GW_STRIDE = 800;        // ring row stride: 768 B + 32 B, so a row adds 2 bank slots (of 16 B) and the
+                                      // 16-row fragment reads are conflict-free at any row offset (tap shift, ring wrap)
+constexpr int GW_GBYTES = GW_GR * GW_STRIDE;  // 25,600 B = 25 DMA pieces of 1 KiB
+constexpr int GW_GPIECES = GW_GBYTES / 1024;
+constexpr int GW_PART = GW_NG * GW_GBYTES;    // partial accumulators: [2 buffers][4 pairs][2 blocks][64 lanes][16 B]
+constexpr int GW_ZERO = GW_PART + 2 * 4 * 2048;  // 768 B of zeros
+constexpr int GW_TVT = GW_ZERO + 768;  // ragged batches: valid input rows per utterance
+constexpr int GW_MAXB = 1024;
+constexpr int GW_LDS = GW_TVT + GW_MAXB * 4;  // 149,248 B
+constexpr int GW_PARTS = 42;          // row parts (x 6 column groups)
+constexpr int GW_GRID = 256;
+constexpr int GW_NT = 512;
+constexpr uint32_t GW_OOR = 0x80000000u;  // a voffset past every descriptor's range (loads return 0, stores drop)
+constexpr uint32_t GW_CFG = 0x00020000u;  // buffer descriptor dword 3 (raw, 32-bit data format)
+static_assert(GW_GBYTES % 1024 == 0 && GW_STRIDE % 16 == 0, "ring geometry");
+
+struct GateWsArgs {
+  const f16* X;       // [M][384] layer input (the split residual stream's high half)
+  const f16* W;       // packed [768][1152]
+  const float* bias;  // [768] packed
+  const f16* cp;      // [M][ld_cp] conditioner projection (packed order)
+  int ld_cp;
+  f16* y;             // [M][ldy] gate output
+  int ldy;
+  int M, T;           // rows = utterances x T
+  int dil;            // tap shift (tap_mul; tap_add = -dil)
+  const int* tv;      // ragged: utterance b has min(T, tv[b] * tv_mul) valid input rows (NULL = T)
+  int tv_mul, B;
+  float invT;
+  int dbg;            // diagnostics (SVC_GWS_DBG, timing only): 2 no MFMAs, 4 no gate arithmetic
+};
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4 gw_desc(const void* base, int64_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, (uint32_t)(bytes > 0 ? bytes : 0), GW_CFG};
+}
+// LDS-DMA of 16 B per lane (lane i's bytes land at lds + 16 i), in inline asm: the compiler neither counts it nor drains
+// it before the LDS reads of other ring slots; the first waves' counted vmcnt waits order it
+__device__ __forceinline__ void gw_dma(u32x4 d, uint32_t voff, unsigned char* lds) {
+  const uint32_t m0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds);
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               ::"s"(m0), "v"(voff), "s"(d) : "memory", "m0");
+}
+template <int N>
+__device__ __forceinline__ void gw_vmwait() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// workgroup barrier behind this wave's LDS writes (the partial accumulators, the prologue's tables)
+__device__ __forceinline__ void gw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+union GwH4 { uint2 u; f16 h[4]; };
+
+// LDS byte offsets of a lane's three tap rows for row block j of the part (output row m = r_begin + 16 j + fr): ring
+// row (8 + 16 j + fr + (tap - 1) dil) mod 160, or the zero row when the tap's input frame lies outside the utterance's
+// valid rows
+__device__ __forceinline__ void gw_tap_bases(const GateWsArgs& a, const int* tvt, int m, int j, int fr, int fk,
+                                             int base[3]) {
+  int bb = (int)((float)m * a.invT);
+  int t = m - bb * a.T;
+  if (t < 0) {
+    --bb;
+    t += a.T;
+  } else if (t >= a.T) {
+    ++bb;
+    t -= a.T;
+  }
+  const bool row_ok = m < a.M;
+  const int tvb = a.tv ? (row_ok ? tvt[bb] : 0) : a.T;
+  const int r0 = (16 * j) % GW_RROWS + GW_HALO + fr;  // < 160 + 23
+#pragma unroll
+  for (int tap = 0; tap < 3; ++tap) {
+    const int tp = t + (tap - 1) * a.dil;
+    const bool ok = row_ok && tp >= 0 && tp < tvb;
+    int rr = r0 + (tap - 1) * a.dil;  // in [0, 160 + 31)
+    rr = rr >= GW_RROWS ? rr - GW_RROWS : rr;
+    base[tap] = (ok ? rr * GW_STRIDE : GW_ZERO) + fk * 16;
+  }
+}
+
+template <bool BF>
+__global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
+  using O = Op16<BF>;
+  extern __shared__ __align__(16) unsigned char smw[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int pair = wave & 3, kh = wave >> 2;
+  const int fr = lane & 15, fk = lane >> 4;
+
+  // workgroup -> (column group, row part): the 6 groups of parts 0..39 on one XCD each; parts 40, 41 on the spares
+  const int b = blockIdx.x, x = b & 7, j = b >> 3;
+  int type, part;
+  if (j < 30) {
+    type = j % 6;
+    part = x * 5 + j / 6;
+  } else {
+    const int s = (j - 30) * 8 + x;
+    if (s >= 12) return;
+    type = s % 6;
+    part = 40 + s / 6;
+  }
+  const int nblk = (a.M + 15) >> 4;
+  const int blk0 = (int)((int64_t)part * nblk / GW_PARTS);
+  const int nsub = (int)((int64_t)(part + 1) * nblk / GW_PARTS) - blk0;
+  if (nsub <= 0) return;
+  const int r_begin = blk0 * 16;
+  const int r_end = min(a.M, r_begin + nsub * 16);
+
+  // this pair's columns: packed 64-column block q, half h: gate ng .. ng + 15, filter ng + 32 .. ng + 47
+  const int q = 2 * type + (pair >> 1), h = pair & 1;
+  const int ng = 64 * q + 16 * h, nf = ng + 32;
+  const int ch = 32 * q + 16 * h + 4 * fk;  // the lane's 4 output channels (second waves)
+
+  if (a.tv) {
+    int* tvt = reinterpret_cast<int*>(smw + GW_TVT);
+    for (int i = tid; i < a.B; i += GW_NT) tvt[i] = min(a.T, a.tv[i] * a.tv_mul);
+  }
+  for (int i = tid; i < 768 / 16; i += GW_NT) *reinterpret_cast<uint4*>(smw + GW_ZERO + i * 16) = make_uint4(0, 0, 0, 0);
+  const int* tvt = reinterpret_cast<const int*>(smw + GW_TVT);
+  unsigned char* const part_buf = smw + GW_PART + pair * 2048;  // + (k & 1) * 8192
+
+  // W fragments of the swapped MFMA (its first operand): w[s] = W[n + fr][32 (18 kh + s) + 8 fk .. + 8]
+  half8 wg[GW_KH], wf[GW_KH];
+  auto load_w = [&]() {
+    const f16* pg = a.W + (size_t)(ng + fr) * GW_K + kh * GW_KH * 32 + fk * 8;
+    const f16* pf = a.W + (size_t)(nf + fr) * GW_K + kh * GW_KH * 32 + fk * 8;
+#pragma unroll
+    for (int s = 0; s < GW_KH; ++s) {
+      wg[s] = *reinterpret_cast<const half8*>(pg + s * 32);
+      wf[s] = *reinterpret_cast<const half8*>(pf + s * 32);
+    }
+  };
+
+  if (kh == 0) {
+    // ------------------------------------------------------------------ first waves: K-steps 0..17 + ring DMAs
+    const u32x4 dx = gw_desc(a.X, (int64_t)a.M * GW_C * 2);
+    // group g = input rows r_begin - 8 + 32 g .. + 31 into ring slot g % 5; its 25 pieces go to the four first waves
+    // round robin (piece p = pair + 4 v): pair 0 issues 7 per group, the others 6. A lane's unit u of piece p -> row
+    // u / 50 of the group, 16-B chunk u % 50 (48, 49: the row's padding, read as nothing)
+    constexpr int PV = (GW_GPIECES + 3) / 4;  // 7
+    uint32_t pc[PV];
+#pragma unroll
+    for (int v = 0; v < PV; ++v) {
+      const int u = (pair + 4 * v) * 64 + lane;
+      const int r = u / 50, c = u - r * 50;
+      pc[v] = c < 48 ? (uint32_t)(r * GW_C * 2 + c * 16) : GW_OOR;
+    }
+    const bool seven = pair + 4 * (PV - 1) < GW_GPIECES;  // this wave issues PV pieces per group (else PV - 1)
+    // every group index is issued, past the part's rows too (harmless rows or zeros), so each wave's count of DMAs
+    // younger than a given group is the same at every step: the waits below are compile-time vmcnt values
+    auto issue = [&](int g) {
+      const uint32_t base = (uint32_t)((r_begin - GW_HALO + g * GW_GR) * (GW_C * 2));  // (negative: wraps, out of range)
+      unsigned char* dst = smw + (g % GW_NG) * GW_GBYTES + pair * 1024;
+#pragma unroll
+      for (int v = 0; v < PV; ++v)
+        if (v < PV - 1 || seven) gw_dma(dx, base + pc[v], dst + v * 4096);
+    };
+    issue(0);
+    issue(1);
+    load_w();
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0) through the builtin, so the compiler knows W has landed too
+    issue(2);
+    issue(3);
+    issue(4);
+    gw_barrier();  // groups 0 and 1, the zero row and the length table
+    // Block j reads groups j / 2 .. (j + 1) / 2, so group G's last reader is block 2 G + 1 (the second wave, step
+    // 2 G + 2). Group g = (k + 7) / 2 >= 5 is issued at the start of odd steps k >= 3, into the slot of group g - 5,
+    // whose last reader finished in step k - 1; its first reader is block 2 g - 1, 5 steps later. At the end of step k,
+    // block k + 1's groups (up to (k + 2) / 2) must have landed: the groups issued after them are the 3 newest on odd
+    // steps and the 2 newest on even ones (3 on step 0: waiting for 2 there is merely early)
+    for (int k = 0; k <= nsub; ++k) {
+      if (k < nsub) {
+        if ((k & 1) && k >= 3) issue((k + 7) / 2);
+        int base[3];
+        gw_tap_bases(a, tvt, r_begin + k * 16 + fr, k, fr, fk, base);
+        floatx4 ag = {0.f, 0.f, 0.f, 0.f}, af = {0.f, 0.f, 0.f, 0.f};
+        if (!(a.dbg & 2)) {
+#pragma unroll
+          for (int s = 0; s < GW_KH; ++s) {  // K-steps 0..11: tap 0; 12..17: tap 1 channels 0..191
+            const half8 av = *reinterpret_cast<const half8*>(smw + base[s / 12] + (s % 12) * 64);
+            ag = O::mfma(wg[s], av, ag);
+            af = O::mfma(wf[s], av, af);
+          }
+        }
+        unsigned char* pb = part_buf + (k & 1) * 8192 + lane * 16;
+        *reinterpret_cast<floatx4*>(pb) = ag;
+        *reinterpret_cast<floatx4*>(pb + 1024) = af;
+        if (k & 1) {
+          if (seven) gw_vmwait<3 * PV>(); else gw_vmwait<3 * (PV - 1)>();
+        } else {
+          if (seven) gw_vmwait<2 * PV>(); else gw_vmwait<2 * (PV - 1)>();
+        }
+      }
+      gw_barrier();  // the partial sums of block k; every first wave's pieces of block k + 1's groups
+    }
+    gw_vmwait<0>();  // (the groups issued past the part land before the workgroup's LDS is released)
+  } else {
+    // ------------------------------------------------------------------ second waves: K-steps 18..35 + gate epilogue
+    const __amdgpu_buffer_rsrc_t rcp =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.cp), (short)0, a.M * a.ld_cp * 2, GW_CFG);
+    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y, (short)0, a.M * a.ldy * 2, GW_CFG);
+    load_w();
+    const float4 bg = *reinterpret_cast<const float4*>(a.bias + ng + 4 * fk);
+    const float4 bfv = *reinterpret_cast<const float4*>(a.bias + nf + 4 * fk);
+    // conditioner projection of blocks blk (in use), blk + 1 and blk + 2 (in flight) in three register sets with
+    // fixed roles (blocks = 0, 1, 2 mod 3; the step loop is unrolled by 3), so no register move waits on a load
+    auto load_cp = [&](int blk, GwH4* dst) {
+      const uint32_t vo = (uint32_t)(r_begin + blk * 16 + fr) * (uint32_t)(a.ld_cp * 2);  // rows past M read 0
+      dst[0].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (ng + 4 * fk) * 2, 0, 0));
+      dst[1].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (nf + 4 * fk) * 2, 0, 0));
+    };
+    GwH4 c0[2], c1[2], c2[2];
+    load_cp(0, c0);
+    load_cp(1, c1);
+    gw_barrier();  // (pairs with the first waves' prologue barrier)
+    // block blk: its partial sums and ring groups are in since the barrier ending step blk (the first waves' block)
+    auto step = [&](int blk, const GwH4* cur, GwH4* next2) {
+      load_cp(blk + 2, next2);
+      const int m = r_begin + blk * 16 + fr;
+      int base[3];
+      gw_tap_bases(a, tvt, m, blk, fr, fk, base);
+      const unsigned char* pb = part_buf + (blk & 1) * 8192 + lane * 16;
+      floatx4 ag = *reinterpret_cast<const floatx4*>(pb);
+      floatx4 af = *reinterpret_cast<const floatx4*>(pb + 1024);
+      if (!(a.dbg & 2)) {
+#pragma unroll
+        for (int s = 0; s < GW_KH; ++s) {  // K-steps 18..23: tap 1 channels 192..383; 24..35: tap 2
+          const int ks = GW_KH + s;
+          const half8 av = *reinterpret_cast<const half8*>(smw + base[ks / 12] + (ks % 12) * 64);
+          ag = O::mfma(wg[s], av, ag);
+          af = O::mfma(wf[s], av, af);
+        }
+      }
+      // gate in registers (conv_gemm4's DIRECT epilogue arithmetic, same order); rows past the part are dropped
+      const GwH4 cg = cur[0], cf = cur[1];
+      GwH4 pk;
+      if (a.dbg & 4) {
+        pk.h[0] = (f16)(ag[0] + af[1]);
+        pk.h[1] = (f16)(ag[1] + af[2]);
+        pk.h[2] = (f16)(ag[2] + af[3]);
+        pk.h[3] = (f16)(ag[3] + af[0]);
+      } else {
+        pk.h[0] = O::enc_lo(gate_act(ag[0] + bg.x + O::dec(cg.h[0]), af[0] + bfv.x + O::dec(cf.h[0])));
+        pk.h[1] = O::enc_lo(gate_act(ag[1] + bg.y + O::dec(cg.h[1]), af[1] + bfv.y + O::dec(cf.h[1])));
+        pk.h[2] = O::enc_lo(gate_act(ag[2] + bg.z + O::dec(cg.h[2]), af[2] + bfv.z + O::dec(cf.h[2])));
+        pk.h[3] = O::enc_lo(gate_act(ag[3] + bg.w + O::dec(cg.h[3]), af[3] + bfv.w + O::dec(cf.h[3])));
+      }
+      const uint32_t vo = m < r_end ? (uint32_t)m * (uint32_t)(a.ldy * 2) + (uint32_t)ch * 2 : GW_OOR;
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, pk.u), ry,
+                                            vo, 0, 0);
+      gw_barrier();
+    };
+    gw_barrier();  // step 0 (the first waves' block 0)
+    for (int blk = 0; blk < nsub; blk += 3) {
+      step(blk, c0, c2);
+      if (blk + 1 < nsub) step(blk + 1, c1, c0);
+      if (blk + 2 < nsub) step(blk + 2, c2, c1);
+    }
+  }
+}
+
+// Does gate_ws take this launch? (the DiffSVC dilated-conv shape: 384 channels, 3 centred taps of dilation 1/2/4/8)
+bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e) {
+  const int d = a.tap_mul;
+  return e.kind == EPI_GATE && e.cp && e.y16 && e.bias && a.Cp == GW_C && a.Cvalid == GW_C && a.ldx == GW_C &&
+         a.K == GW_K && a.Kpad == GW_K && a.N == GW_N && (d == 1 || d == 2 || d == 4 || d == 8) && a.tap_add == -d &&
+         a.istride == 1 && a.T_in == a.T_out && (!a.tv || a.B <= GW_MAXB) && e.ld_cp % 4 == 0 && e.ldy16 % 4 == 0 &&
+         (int64_t)a.B * a.T_out * std::max(e.ld_cp, std::max(e.ldy16, GW_C)) * 2 < (1ll << 30);
+}
+
+int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
+  SVC_REQUIRE(gate_ws_fits(a, e), "gate_ws: not the DiffSVC dilated-conv gate shape");
+  SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0 && ((uintptr_t)e.cp & 7) == 0 &&
+                  ((uintptr_t)e.y16 & 7) == 0 && ((uintptr_t)e.bias & 15) == 0,
+              "gate_ws: alignment");
+  const int M = a.B * a.T_out;
+  if (M == 0) return SVC_OK;
+  static const int dbg = getenv("SVC_GWS_DBG") ? atoi(getenv("SVC_GWS_DBG")) : 0;  // (diagnostics, read once)
+  GateWsArgs g{a.X, a.W, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
+               1.0f / (float)a.T_out, dbg};
+  const int bf = a.bf16 ? 1 : 0;
+  const void* fn = bf ? (const void*)gate_ws_kernel<true> : (const void*)gate_ws_kernel<false>;
+  // the dynamic-LDS attribute is set per device
+  static bool attr[16][2] = {};
+  int dev = 0;
+  SVC_HIP_CHECK(hipGetDevice(&dev));
+  SVC_REQUIRE(dev >= 0 && dev < 16, "gate_ws: device %d", dev);
+  if (!attr[dev][bf]) {
+    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, GW_LDS));
+    attr[dev][bf] = true;
+  }
+  const int tok = prof_begin("gate_ws<16x128>", 2.0 * M * (double)GW_N * GW_K, 0.0, s);
+  void* args[] = {&g};
+  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3(GW_GRID), dim3(GW_NT), args, GW_LDS, s));
+  prof_end(tok, s);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
+}  // namespace svc

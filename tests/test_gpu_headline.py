@@ -9,6 +9,8 @@ BigVGAN, B = 32 x 10 s, in the engine's default precision mode (the one bench.py
   shared x_T / step noise (PLMS on random weights diverges to |x| ~ 1e2, so its mel is not a meaningful L1 target).
 - The full B = 32 x 10 s conversion: shapes, finiteness, and per-utterance bit-equality with single-clip runs.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -75,6 +77,40 @@ def test_plms100_vs_golden(engine, golden):
     x = engine.diffsvc_sample(cond, fast_inference=True, speedup=10, x_T=dev(g["x_T"]))
     # measured 1.3e-4 (round 2)
     assert rel_l2(x[0].cpu().numpy().T, g["plms100"]) < 1e-3, rel_l2(x[0].cpu().numpy().T, g["plms100"])
+
+
+@pytest.mark.parametrize("B", [2, 32])
+def test_plms100_headline_shape_vs_golden(cfg, B):
+    """The headline sampler at the headline shape against the reference: PLMS speedup 10
+    (modules/diffsvcrepo_inference.py:216-231) over T = 937 frames, batched, in the production engine's default
+    precision mode and sub-stream split, against tests/golden/plms100_headline.npz: the reference's own
+    svc_model_inference on the same seeded weights (eps head x 3, so the denoiser's eps carries 80 % of the output's
+    norm), conditioning and x_T, one utterance per run (tools/make_goldens_headline.py). The batch holds the golden's
+    two utterances (B = 32: repeated, one copy per sampler sub-stream and utterance position) and each is compared:
+    rel-L2 <= 1e-3 on x_0 and on its eps-induced part x_0 - x_0|eps=0 (measured: see the printed line)."""
+    import headline_golden as HG
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "plms100_headline.npz"))
+    ms = HG.headline_mapper_state(cfg.mapper)
+    eng = SVCEngine(cfg, 0, mapper_state=ms)
+    try:
+        us = [u % 2 for u in range(B)]
+        cond = dev(np.concatenate([HG.headline_cond(u) for u in us]))
+        xT = np.concatenate([HG.headline_x_T(u) for u in us])
+        x = eng.diffsvc_sample(cond, fast_inference=True, speedup=10, x_T=dev(xT)).cpu().numpy()
+    finally:
+        eng.close()
+    consts = OM.schedule_constants(C.noise_schedule(cfg.mapper))
+    worst = 0.0
+    for u in (0, 1):
+        ref = g[f"plms100_u{u}"]
+        triv = OM.sample_plms(lambda x_, t: torch.zeros_like(x_), torch.from_numpy(HG.headline_x_T(u)), 1, HG.T, 1000,
+                              10, consts)[0].numpy()
+        for b in [b for b in range(B) if us[b] == u]:
+            r_all = rel_l2(x[b], ref)
+            r_eps = rel_l2(x[b] - triv, ref - triv)
+            worst = max(worst, r_all, r_eps)
+            assert r_all <= 1e-3 and r_eps <= 1e-3, (b, u, r_all, r_eps)
+    print(f"PLMS-100 headline shape B={B}: worst rel-L2 {worst:.3e}")
 
 
 @pytest.mark.parametrize("seconds", [

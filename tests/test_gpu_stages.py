@@ -165,6 +165,27 @@ def test_gate_gemm_ragged(engine, states, cfg, variant, B, T, tune):
     assert rel_l2(eps, ref) < 5e-3
 
 
+@pytest.mark.parametrize("B,T,frames", [(1, 5, None), (1, 93, None), (3, 50, None), (2, 700, None), (5, 937, None),
+                                         (16, 937, None), (4, 301, [301, 17, 160, 299]), (3, 40, [9, 40, 1])])
+def test_gate_ws_bit_identical(engine, B, T, frames, tune):
+    """gate_ws.hip (the DiffSVC dilated conv + gate as a weight-stationary row stream: W in VGPRs, one LDS image per
+    64-row super-block shared by the three taps, the K chain split over a wave pair through the MFMA C operand) against
+    conv_gemm4<128,128,gate> (gate_ws = 0): the same 32-deep K order, MFMA operand order and epilogue arithmetic, so the
+    eps of every layer's dilation (1, 2, 4, 8) is bit for bit equal. Tiny (M < 16), ragged row counts (parts of 16-row
+    blocks, partial super-blocks, empty row parts), utterance boundaries inside blocks, ragged frame counts (taps past an
+    utterance's valid rows read the zero row), one of them a single frame."""
+    rng = np.random.default_rng(B * 29 + T)
+    cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
+    x = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
+    tune(engine, gate_ws=0)
+    ref = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
+    tune(engine, gate_ws=1)
+    out = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
+    for k in range(2):
+        assert np.isfinite(out[k]).all()
+        assert np.array_equal(out[k], ref[k]), (k, rel_l2(out[k], ref[k]))
+
+
 @pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700), (5, 937)])
 def test_fused_head(engine, states, cfg, B, T, tune):
     """diff_head.hip (relu(skip_projection) + output_projection in one launch, u kept on chip) against the

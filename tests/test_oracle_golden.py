@@ -110,6 +110,30 @@ def test_plms_samplers(golden, mapper_sd):
     assert np.abs(x100[0].numpy().T - ref).max() <= 1e-4 * np.abs(ref).max()
 
 
+def test_plms100_headline_shape(golden):
+    """The oracle's PLMS-100 at the headline length (T = 937) against the reference's own svc_model_inference on the
+    same seeded weights (eps head x 3), conditioning and x_T (tools/make_goldens_headline.py, utterance 0): max |d| <=
+    1e-5 of max |x_0|, and the eps-induced part x_0 - x_0|eps=0 (the sampler run with a zero denoiser) within rel-L2
+    1e-5."""
+    import headline_golden as HG
+    g = golden("plms100_headline")
+    mcfg = C.load_config().mapper
+    mcfg.input_content_dim["whisper"] = 1024
+    sd = HG.headline_mapper_state(mcfg)
+    consts = OM.schedule_constants(C.noise_schedule(mcfg))
+    cond = torch.from_numpy(HG.headline_cond(0))
+    table = W.step_embedding_table(1000)
+    cache = {}
+    den = lambda x, t: OM.diffsvc_forward(sd, mcfg, x, cond, t, table, cp_cache=cache)
+    xT = torch.from_numpy(HG.headline_x_T(0))
+    x = OM.sample_plms(den, xT, 1, HG.T, 1000, 10, consts)[0].numpy()
+    x_triv = OM.sample_plms(lambda x, t: torch.zeros_like(x), xT, 1, HG.T, 1000, 10, consts)[0].numpy()
+    ref = g["plms100_u0"]
+    assert np.abs(x - ref).max() <= 1e-5 * np.abs(ref).max()
+    d, r = (x - x_triv).ravel(), (ref - x_triv).ravel()
+    assert np.linalg.norm(d - r) <= 1e-5 * np.linalg.norm(r), np.linalg.norm(d - r) / np.linalg.norm(r)
+
+
 @pytest.mark.slow
 def test_ddpm1000(golden, mapper_sd):
     mcfg, sd = mapper_sd
