@@ -27,6 +27,7 @@ import time
 
 import numpy as np
 import torch
+import torch.distributed as torchdist
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -189,6 +190,7 @@ def dry_run(args, dist):
     dist.barrier()
     t0 = time.time()
     out = None
+    gather_s = []
     for i in range(args.steps):
         if args.fault and dist.rank == args.fault_rank and i == min(1, args.steps - 1):
             # fault injection (tests/test_parallel.py): this rank fails mid-run, by an exception or by hanging
@@ -196,16 +198,21 @@ def dry_run(args, dist):
             if args.fault == "raise":
                 raise RuntimeError(f"injected fault on rank {dist.rank} at step {i}")
             time.sleep(3600)
+        tg = time.perf_counter()
         out, lens = dist.gather_waveforms(wav, return_lengths=True)
+        gather_s.append(time.perf_counter() - tg)
     dist.barrier()
     per_rank = [r[0] for r in dist.all_gather_floats([time.time() - t0])]
+    gather_ms = [r[0] for r in dist.all_gather_floats([1000.0 * sum(gather_s) / max(len(gather_s), 1)])]
     elapsed = max(per_rank)
     if dist.rank == 0:
         assert out.shape[0] == dist.world * B and bool(torch.isfinite(out).all())
         if args.dump:
             np.save(args.dump, out.numpy())
         print(json.dumps({"metric": "dry-run gather (identity conversion, CPU)", "n_gpus": args.gpus,
-                          "dist_world": dist.world, "backend": dist.backend or "none", "steps": args.steps,
+                          "dist_world": dist.world, "backend": dist.backend or "none",
+                          "rccl_world": torchdist.get_world_size() if torchdist.is_initialized() else 1,
+                          "gather_ms_per_step": [round(v, 3) for v in gather_ms], "steps": args.steps,
                           "per_rank_s": [round(t, 4) for t in per_rank], "elapsed_s": round(elapsed, 4),
                           "gathered": list(out.shape), "lengths": lens.tolist()}), flush=True)
     dist.close()
@@ -231,6 +238,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads for the CPU baseline (default: every CPU available to the process)")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--no-isolated-pass", action="store_true",
+                    help="skip the untimed single-stream pass of the dominant call site (profiling runs: every launch "
+                         "of the dominant kernel in the trace is then a production launch)")
     ap.add_argument("--content", choices=["whisper", "contentvec"], default="whisper",
                     help="content encoder (BASELINE config 5: contentvec = the HuBERT/ContentVec variant)")
     ap.add_argument("--sampler", choices=["plms", "ddpm"], default="plms",
@@ -285,10 +295,17 @@ def main():
     utt = torch.from_numpy(uids.astype(np.int32)).cuda()
     log(f"rank {dist.rank}/{dist.world}: setup {time.time() - t_setup:.1f}s, weights {eng.memory()[0] / 1e9:.2f} GB")
 
+    gather_s = []  # the RCCL gather's own wall time per step (convert finished first: synchronized on both sides)
+
     def step():
         res = pipe.convert(d24, d16, singer, fast_inference=fast, speedup=args.speedup, seed=1234, utt_ids=utt,
                            wav16_float=d16 if hs is not None else None)
-        return dist.gather_waveforms(res.wav)
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        out = dist.gather_waveforms(res.wav)
+        torch.cuda.synchronize()
+        gather_s.append(time.perf_counter() - tg)
+        return out
 
     # Warmup. The last warmup step runs with every launch profiled (HIP events around each kernel): that
     # gives the per-kernel breakdown and picks the dominant kernel. The timed steps then record events
@@ -317,7 +334,7 @@ def main():
     # extra untimed step with the sampler on a single stream gives the dominant call site's isolated per-launch rate.
     streams = int(eng.get_config("tune.sampler_streams"))
     isolated = None
-    if streams > 1 and dom_site.startswith("diffsvc."):
+    if streams > 1 and dom_site.startswith("diffsvc.") and not args.no_isolated_pass:
         eng.tune(sampler_streams=1)
         _lib.profile_enable(True)
         step()
@@ -337,6 +354,7 @@ def main():
     torch.cuda.synchronize()
     _lib.profile_filter(dom_name)
     _lib.profile_enable(True)
+    gather_s.clear()
     t0 = time.time()
     for i in range(args.steps):
         out = step()
@@ -345,6 +363,7 @@ def main():
     torch.cuda.synchronize()
     dist.barrier()
     per_rank = [r[0] for r in dist.all_gather_floats([time.time() - t0])]
+    gather_ms = [r[0] for r in dist.all_gather_floats([1000.0 * sum(gather_s) / max(len(gather_s), 1)])]
     elapsed = max(per_rank)
     prof = _lib.profile_read()
     _lib.profile_enable(False)
@@ -355,7 +374,11 @@ def main():
     if out is not None:
         assert out.shape[0] == dist.world * B and bool(torch.isfinite(out).all())
 
-    # roofline for the dominant kernel, from its launches in the timed region (sites are "kernel@site")
+    # Roofline of the dominant kernel AS THE TIMED REGION RUNS IT (its production launches: at a diffsvc.* site the
+    # sampler's utterance-aligned sub-batches on `streams` concurrent streams), HIP events around each launch on its
+    # launch stream. A launch's event span then includes time its waves share the CUs with the other stream's kernels
+    # (and the event markers' own gap); rocprof's per-dispatch duration of the same launches, from the
+    # committed profile of record, stands beside it, and so does the untimed single-stream pass (full batch per launch).
     dom = dict(ms=0.0, launches=0, flops=0.0, bytes=0.0)
     for name, v in prof.items():
         if name.split("@")[0] == dom_name:
@@ -370,74 +393,55 @@ def main():
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s"}
     roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
     roof["kernel"] = dom_name
+    roof["site"] = dom_site
     roof["avg_launch_us"] = round(per_launch_s * 1e6, 2)
     roof["launches_timed"] = dom["launches"]
+    roof["algorithmic_per_launch"] = round(dom["flops"] / dom["launches"] if dom["flops"] > 0 else
+                                           dom["bytes"] / dom["launches"], 1)
     roof["share_of_kernel_time"] = round(share, 3)
-    roof["site"] = dom_site
     roof["sampler_streams"] = streams
-    roof["measured"] = "timed region, HIP events on the launch stream"
+    T_frames = int((d24.shape[1] + 768 - 1024) // 256 + 1)
+    if dom_site.startswith("diffsvc."):
+        roof["rows_per_launch"] = -(-B // streams) * T_frames  # the largest sub-batch
+    roof["measured"] = "production launches in the timed region, HIP events on the launch stream"
     if isolated:
-        # With concurrent sampler streams a launch's event-bracketed span includes the time its waves wait
-        # behind the other streams' kernels, so it cannot be compared with rocprof's per-dispatch hardware
-        # duration. The headline roofline is then the dominant call site on ONE stream (full batch per
-        # launch), whose per-launch time rocprof reproduces; the concurrent figures stay beside it.
-        concurrent = {k: roof.pop(k) for k in ("achieved", "frac", "kernel", "avg_launch_us", "launches_timed",
-                                               "sampler_streams", "measured")}
-        roof.update({k: isolated[k] for k in ("achieved", "frac", "kernel", "avg_launch_us", "sampler_streams")})
-        roof["launches_measured"] = isolated["launches"]
-        roof["measured"] = "untimed single-stream pass of the dominant call site, HIP events on the launch stream"
-        roof["concurrent"] = concurrent
-    dom_name = roof["kernel"]
+        roof["isolated_single_stream"] = {k: isolated[k] for k in ("kernel", "avg_launch_us", "achieved", "launches")}
+        roof["isolated_single_stream"]["frac"] = isolated["frac"]
+        roof["isolated_single_stream"]["rows_per_launch"] = B * T_frames
+        roof["isolated_single_stream"]["measured"] = ("untimed single-stream pass of the dominant call site (full "
+                                                      "batch per launch), HIP events on the launch stream")
+    # committed profile of record (tools/gpu_profile.sh: rocprofv3 trace + separate FETCH_SIZE / WRITE_SIZE passes of
+    # bench.py --no-isolated-pass, so every dispatch of the kernel there is a production launch)
     roof["traffic"] = None
     if os.path.exists(args.pmc_json):
         pmc = json.load(open(args.pmc_json))
-        if dom_name in pmc.get("kernels", {}):
-            ent = pmc["kernels"][dom_name]
+        ent = pmc.get("kernels", {}).get(dom_name)
+        if ent:
             roof["traffic"] = ent.get("hbm_bytes_per_launch")
-            roof["traffic_source"] = os.path.relpath(args.pmc_json, REPO) + " (" + pmc.get("source_run", "?") + \
+            src = os.path.relpath(args.pmc_json, REPO) + " (" + pmc.get("source_run", "?") + \
                 (f", {ent['workgroups']}-workgroup launches" if "workgroups" in ent else "") + ")"
+            roof["traffic_source"] = src
             if "rocprof_trace_avg_us" in ent:
-                roof["rocprof_avg_launch_us"] = ent["rocprof_trace_avg_us"]
-    # MFMA utilisation of the roofline kernel's largest grid from the serialised PMC passes (tools/pmc_kernels.sh):
+                roof["rocprof_avg_launch_us"] = round(ent["rocprof_trace_avg_us"], 2)
+                if dom["flops"] > 0:
+                    roof["rocprof_achieved"] = round(dom["flops"] / dom["launches"] /
+                                                     (ent["rocprof_trace_avg_us"] * 1e-6) / 1e12, 2)
+                    roof["rocprof_frac"] = round(roof["rocprof_achieved"] / PEAK_F16_TFLOPS, 4)
+    # MFMA utilisation of the roofline kernel's production grid from the serialised PMC passes (tools/pmc_kernels.sh):
     # SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE x 1024 SIMDs, per dispatch
     pmc_k = os.path.join(os.path.dirname(args.pmc_json), "pmc_kernels.json")  # latest tools/pmc_kernels.sh summary
     if os.path.exists(pmc_k):
         ents = [v for v in json.load(open(pmc_k)).values() if v.get("kernel") == dom_name and "mfma_busy" in v]
         if ents:
-            big = max(ents, key=lambda v: v["workgroups"])
+            big = max(ents, key=lambda v: v.get("dispatches", 0))  # the production grid has the most dispatches
             roof["mfma_busy_pmc"] = round(big["mfma_busy"], 3)
             if "valu_per_mfma" in big:
                 roof["valu_per_mfma_pmc"] = round(big["valu_per_mfma"], 2)
             roof["mfma_busy_source"] = os.path.relpath(pmc_k, REPO) + f" ({big['workgroups']}-workgroup launches)"
-    # the production sub-batch launches of the dominant call site (sampler_streams concurrent sub-batches): their
-    # rocprof per-dispatch average from the committed trace summary, when it holds that grid
-    if os.path.exists(args.pmc_json) and dom_site.startswith("diffsvc.") and streams > 1:
-        pmc = json.load(open(args.pmc_json))
-        ent = pmc.get("kernels", {}).get(dom_name)
-        T_frames = int((d24.shape[1] + 768 - 1024) // 256 + 1)
-        sub_rows = -(-B // streams) * T_frames  # the largest sub-batch
-        m_bm = re.match(r"conv_gemm4<(\d+),", dom_name)
-        bm = int(m_bm.group(1)) if m_bm else 128
-        wg = -(-sub_rows // bm) * 6            # bm x 128 tiles over the 768 packed gate / filter columns
-        g = ent.get("by_grid", {}).get(str(wg * 256)) if ent else None
-        if g and "rocprof_trace_avg_us" in g:
-            fl = 2.0 * sub_rows * 768 * 1152
-            tf = fl / (g["rocprof_trace_avg_us"] * 1e-6) / 1e12
-            roof["production"] = {"sub_batch_rows": sub_rows, "workgroups": wg,
-                                  "rocprof_avg_launch_us": round(g["rocprof_trace_avg_us"], 2),
-                                  "achieved": round(tf, 2), "frac": round(tf / PEAK_F16_TFLOPS, 4),
-                                  "hbm_bytes_per_launch": g.get("hbm_bytes_per_launch"),
-                                  "source": os.path.relpath(args.pmc_json, REPO) + " (" + pmc.get("source_run", "?") +
-                                  f", {wg}-workgroup launches, {streams} concurrent sampler streams)"}
-            if os.path.exists(pmc_k):  # MFMA busy of the same grid in the serialised PMC passes
-                pe = [v for v in json.load(open(pmc_k)).values()
-                      if v.get("kernel") == dom_name and v.get("workgroups") == wg and "mfma_busy" in v]
-                if pe:
-                    roof["production"]["mfma_busy_pmc"] = round(pe[0]["mfma_busy"], 3)
     # per-kernel breakdown of the fully profiled warmup step
     total_flops = sum(v["flops"] for v in prof_all.values())
     calls = (1000 // args.speedup + 1) if fast else 1000
-    alg_tf = survey_algorithmic_tflops(dist.world * B, int((d24.shape[1] + 768 - 1024) // 256 + 1), calls,
+    alg_tf = survey_algorithmic_tflops(dist.world * B, T_frames, calls,
                                        "whisper" if hs is None else "contentvec")
     kernels = {k: {"ms_per_step": round(v["ms"], 3), "launches_per_step": v["launches"],
                    "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 1) if v["flops"] else None,
@@ -455,6 +459,10 @@ def main():
             "metric": "converted audio sec/sec (RTF^-1) end-to-end, 10 s clips",
             "value": round(value, 2), "unit": "audio-s/s", "n_gpus": dist.world, "steps": args.steps,
             "dist_world": dist.world, "backend": dist.backend or "none",
+            # the process group's own size (torch.distributed.get_world_size(); 1 without a group) and the gather's
+            # wall time per step on each rank (rank 0 receives; world 1: no collective)
+            "rccl_world": torchdist.get_world_size() if torchdist.is_initialized() else 1,
+            "gather_ms_per_step": [round(v, 3) for v in gather_ms],
             "per_rank_ms_per_step": [round(1000.0 * t / args.steps, 2) for t in per_rank],
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.operands, "data": "synthetic",

@@ -365,13 +365,15 @@ class Fp16Operands(OperandRounding):
     """fp16 conv operands (the BigVGAN tolerance derivation), and the f16 storage of AMPBlock1's convs1 output that the
     HIP vocoder uses (engine.hip, round 3)."""
 
-    def __init__(self):
+    def __init__(self, store16=True):
         super().__init__(torch.float16, linear=False)
+        self.store16 = store16  # False: operand rounding only (the pre-round-3 emulation, tests/test_gpu_stages.py)
 
     def __enter__(self):
-        _STORE16[0] = True
+        self._prev_store16 = _STORE16[0]  # (nested / repeated contexts restore what they found)
+        _STORE16[0] = self.store16
         return super().__enter__()
 
     def __exit__(self, *a):
-        _STORE16[0] = False
+        _STORE16[0] = self._prev_store16
         return super().__exit__(*a)

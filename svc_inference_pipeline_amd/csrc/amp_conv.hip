@@ -260,12 +260,7 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
 template <int C, bool X16>
 static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   using CF = AmpCfg<C>;
-  static bool attr = false;
-  if (!attr) {
-    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)amp_conv_kernel<C, X16>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, CF::LDS));
-    attr = true;
-  }
+  if (int st = ensure_dyn_lds((const void*)amp_conv_kernel<C, X16>, CF::LDS)) return st;
   const int64_t grid = (int64_t)p.B * cdiv(p.L, CF::BT);
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "amp_conv: bad grid");
   const double elems = (double)p.B * p.L * C;

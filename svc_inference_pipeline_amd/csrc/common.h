@@ -91,7 +91,11 @@ __device__ __forceinline__ float gate_act(float a, float b) {
   const float e1 = __builtin_amdgcn_exp2f(t1);
   const float e2 = __builtin_amdgcn_exp2f(-2.8853900817779268f * fabsf(b));
   const float d1 = 1.0f + e1;
-  const float r = (1.0f - e2) * __builtin_amdgcn_rcpf(fmaf(d1, e2, d1));
+  float r = (1.0f - e2) * __builtin_amdgcn_rcpf(fmaf(d1, e2, d1));
+  // the product is rounded to f32 here, then to f16 by the caller's store: the empty asm keeps hipcc from fusing the
+  // multiply with that conversion into one v_fma_mixlo_f16 (one rounding), which it did in some kernels and not in
+  // others (the last f16 bit differed in ~1e-5 of the outputs and broke gate_ws / conv_gemm4 bit identity, r04f)
+  asm("" : "+v"(r));
   return copysignf(r, b);
 }
 
@@ -298,6 +302,10 @@ struct TuningScope {
   ~TuningScope();
   const Tuning* prev;
 };
+
+// The dynamic-LDS limit of a kernel (hipFuncSetAttribute) is a per-device function attribute: set it once per (kernel,
+// device) on the current device before launching with more than 64 KiB (engine.hip)
+int ensure_dyn_lds(const void* fn, int bytes);
 
 // live per-kernel timing (bench roofline): when enabled, launches are bracketed by hipEvents and
 // aggregated by kernel name together with their algorithmic FLOPs / bytes.

@@ -244,11 +244,7 @@ int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "diff_head: bad grid");
   DiffHeadArgs p{s16, Wsp, bsp, Wout, bout, eps, ld_eps, Nout, M};
   const void* fn = bf16 ? (const void*)diff_head_kernel<true> : (const void*)diff_head_kernel<false>;
-  static bool attr[2] = {};
-  if (!attr[bf16]) {
-    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, DH_LDS));
-    attr[bf16] = true;
-  }
+  if (int st = ensure_dyn_lds(fn, DH_LDS)) return st;
   const double flops = 2.0 * M * (double)DL_C * 3 * DL_C + 2.0 * M * (double)Nout * 3 * DL_C;
   const int tok = prof_begin("diff_head<128>", flops, 0.0, s);
   void* args[] = {&p, const_cast<const f16**>(&zpage)};

@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <map>
+#include <mutex>
+#include <set>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -349,6 +351,18 @@ const Tuning& tuning() {
 }
 TuningScope::TuningScope(const Tuning* t) : prev(t_tuning) { t_tuning = t; }
 TuningScope::~TuningScope() { t_tuning = prev; }
+int ensure_dyn_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::tuple<const void*, int, int>> done;
+  int dev = 0;
+  SVC_HIP_CHECK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.count({fn, dev, bytes})) return SVC_OK;
+  SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done.insert({fn, dev, bytes});
+  return SVC_OK;
+}
+
 }  // namespace svc
 
 using namespace svc;

@@ -248,12 +248,7 @@ static int launch_dft_mel(const DftArgs& a, int B, hipStream_t s) {
   using P = FftPlan<N>;
   const size_t lds = MelLds<N>::bytes(a.fb_len, a.n_mels);
   SVC_REQUIRE(lds <= 160 * 1024, "dft_mel: %zu B of LDS", lds);
-  static bool attr = false;
-  if (!attr) {
-    SVC_HIP_CHECK(hipFuncSetAttribute((const void*)dft_mel_kernel<N>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024));
-    attr = true;
-  }
+  if (int st = ensure_dyn_lds((const void*)dft_mel_kernel<N>, 160 * 1024)) return st;
   DftArgs p = a;
   dim3 grid(cdiv(a.n_frames, P::FR), B);
   hipLaunchKernelGGL(dft_mel_kernel<N>, grid, dim3(P::TPF * P::FR), lds, s, p);

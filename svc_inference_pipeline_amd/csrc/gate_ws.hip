@@ -277,6 +277,9 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       const unsigned char* pb = part_buf + (blk & 1) * 8192 + lane * 16;
       floatx4 ag = *reinterpret_cast<const floatx4*>(pb);
       floatx4 af = *reinterpret_cast<const floatx4*>(pb + 1024);
+      // the second wave's MFMAs go first on the SIMD (priority 1), so its gate epilogue (VALU) runs beside the first
+      // wave's remaining MFMAs instead of after them (+6 % on the kernel in the round-4 super-block form, r04c)
+      __builtin_amdgcn_s_setprio(1);
       if (!(a.dbg & 2)) {
 #pragma unroll
         for (int s = 0; s < GW_KH; ++s) {  // K-steps 18..23: tap 1 channels 192..383; 24..35: tap 2
@@ -286,6 +289,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
           af = O::mfma(wf[s], av, af);
         }
       }
+      __builtin_amdgcn_s_setprio(0);
       // gate in registers (conv_gemm4's DIRECT epilogue arithmetic, same order); rows past the part are dropped
       const GwH4 cg = cur[0], cf = cur[1];
       GwH4 pk;
@@ -335,15 +339,7 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
                1.0f / (float)a.T_out, dbg};
   const int bf = a.bf16 ? 1 : 0;
   const void* fn = bf ? (const void*)gate_ws_kernel<true> : (const void*)gate_ws_kernel<false>;
-  // the dynamic-LDS attribute is set per device
-  static bool attr[16][2] = {};
-  int dev = 0;
-  SVC_HIP_CHECK(hipGetDevice(&dev));
-  SVC_REQUIRE(dev >= 0 && dev < 16, "gate_ws: device %d", dev);
-  if (!attr[dev][bf]) {
-    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, GW_LDS));
-    attr[dev][bf] = true;
-  }
+  if (int st = ensure_dyn_lds(fn, GW_LDS)) return st;
   const int tok = prof_begin("gate_ws<16x128>", 2.0 * M * (double)GW_N * GW_K, 0.0, s);
   void* args[] = {&g};
   SVC_HIP_CHECK(hipLaunchKernel(fn, dim3(GW_GRID), dim3(GW_NT), args, GW_LDS, s));

@@ -506,11 +506,7 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
   const void* fn = fns[bf][cp64][form];
   // the register forms need only the operand ring (no C staging)
   const int lds = form == G3_LDS ? CF::LDS : CF::RING;
-  static bool attr[2][2][4] = {};
-  if (!attr[bf][cp64][form]) {
-    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    attr[bf][cp64][form] = true;
-  }
+  if (int st = ensure_dyn_lds(fn, lds)) return st;
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
   const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);
   const float inv = 1.0f / (float)a.Cp;

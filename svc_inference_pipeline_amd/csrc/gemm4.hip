@@ -313,11 +313,7 @@ int conv_gemm4(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, hipSt
   const void* fns[2][2][2][2] = {G4_FORMS(false), G4_FORMS(true)};
 #undef G4_FORMS
   const void* fn = fns[bf][cp64][pair][direct];
-  static bool attr[2][2][2][2] = {};
-  if (!attr[bf][cp64][pair][direct]) {
-    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, G4_LDS));
-    attr[bf][cp64][pair][direct] = true;
-  }
+  if (int st = ensure_dyn_lds(fn, G4_LDS)) return st;
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
   const char* tag = direct ? "conv_gemm4<128,128,gate>" : pair ? "conv_gemm4<128,128,pair>" : "conv_gemm4<128,128>";
   const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);

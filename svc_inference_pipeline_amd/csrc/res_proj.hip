@@ -258,12 +258,13 @@ int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, c
   SVC_REQUIRE(((uintptr_t)g & 15) == 0 && ((uintptr_t)Wf & 15) == 0 && ((uintptr_t)hi & 15) == 0 &&
                   ((uintptr_t)lo & 15) == 0,
               "res_proj: 16-B alignment");
-  static int ncu = 0;
-  if (!ncu) {
-    int dev = 0;
-    SVC_HIP_CHECK(hipGetDevice(&dev));
-    SVC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
+  // the CU count (it sizes the row-lane grid) per device
+  static int ncu_dev[16] = {};
+  int dev = 0;
+  SVC_HIP_CHECK(hipGetDevice(&dev));
+  SVC_REQUIRE(dev >= 0 && dev < 16, "res_proj: device %d", dev);
+  int& ncu = ncu_dev[dev];
+  if (!ncu) SVC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   const int tiles = cdiv(M, RP_ROWS);
   // row lanes in groups of 8 (the b / b + 8 pairing above). Default: 3/8 of the CU count (96 lanes = 192 workgroups
   // on 256 CUs): end to end 810.4-810.8 audio-s/s against 800.6-806.1 with one workgroup per CU, 804-805 with 80 lanes
@@ -278,11 +279,7 @@ int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, c
   constexpr int depth = 3;
   const void* fn = bf16 ? (const void*)res_proj_kernel<true, depth> : (const void*)res_proj_kernel<false, depth>;
   const int lds = depth * RP_SLOT;
-  static bool attr[2] = {};
-  if (!attr[bf16]) {
-    SVC_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-    attr[bf16] = true;
-  }
+  if (int st = ensure_dyn_lds(fn, lds)) return st;
   const int tok = prof_begin("res_proj<16x192>", 2.0 * M * RP_C * RP_C, (double)M * RP_C * 10.0, s);
   void* args[] = {&a};
   SVC_HIP_CHECK(hipLaunchKernel(fn, dim3(2 * lanes), dim3(RP_NT), args, lds, s));

@@ -297,6 +297,17 @@ def test_bigvgan(engine, cfg, states, golden, direct, tune):
     emu = OF.synthesis_fade(emu[0, 0], mel.shape[-1]).numpy()
     budget = 1.5 * rel_l2(emu, g["synth"]) + 1e-3
     assert rel_l2(wav[0].cpu().numpy(), g["synth"]) < budget
+    # The emulation above also rounds AMPBlock1's convs1 output to f16 (the HIP path's storage since round 3), so its
+    # budget could grow by what that storage gives up. Anchor it to fp32: the operand-rounding-only
+    # emulation (the pre-round-3 one) sets a budget of its own, the HIP result must meet it too, and the storage term
+    # must not move the emulation further from the f32 oracle (measured: 4.10e-2 with it, 4.18e-2 without; in this
+    # chaotic regime any rounding moves the waveform by ~3-4 %).
+    with OM.Fp16Operands(store16=False):
+        emu_ops = OM.bigvgan_forward(states["vocoder"], cfg.vocoder, torch.from_numpy(mel)[None])
+    emu_ops = OF.synthesis_fade(emu_ops[0, 0], mel.shape[-1]).numpy()
+    d_ops = rel_l2(emu_ops, g["synth"])
+    assert rel_l2(emu, g["synth"]) <= 1.1 * d_ops, (rel_l2(emu, g["synth"]), d_ops)
+    assert rel_l2(wav[0].cpu().numpy(), g["synth"]) < 1.5 * d_ops + 1e-3
 
 
 @pytest.mark.parametrize("variant", list(W.VOCODER_VARIANTS))

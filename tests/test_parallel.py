@@ -122,6 +122,9 @@ def _bench(tmp_path, gpus, name):
 def test_bench_spawn_dry_run_world2_matches_world1(tmp_path):
     line2, out2 = _bench(tmp_path, 2, "w2")
     assert line2["dist_world"] == 2 and line2["backend"] == "gloo" and len(line2["per_rank_s"]) == 2
+    # the process group's own size and each rank's gather time per step (bench.py reports both on the GPU line too)
+    assert line2["rccl_world"] == 2 and len(line2["gather_ms_per_step"]) == 2
+    assert all(v >= 0 for v in line2["gather_ms_per_step"])
     assert line2["gathered"][0] == 6
     # world 1 with the whole batch (6 utterances, ids 0..5) must gather identical waveforms
     import subprocess

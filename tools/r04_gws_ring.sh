@@ -2,9 +2,11 @@
 # round 4: gate_ws (ring form) parity and timing
 set -o pipefail
 O=gpurun_out/${TAG:-r04e}; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_gpu_stages.py -m gpu -x -q --timeout 300 --timeout-method thread -k "gate_ws_bit_identical" > $O/tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_stages.py -m gpu -x -q --timeout 300 --timeout-method thread -k "gate_ws_bit_identical or gate_gemm_ragged or eps_gemm_variants" > $O/tests.log 2>&1
 rc=$?; tail -3 $O/tests.log; [ $rc -ne 0 ] && { tail -60 $O/tests.log; exit $rc; }
 SH="29984,768,384,3,1;14992,768,384,3,1"
+timeout -k 10 300 python3 tools/r04_gws_dump.py > $O/dump.txt 2>&1 || exit $?
+cat $O/dump.txt
 for dbg in 0 2 6; do
   SVC_GWS_DBG=$dbg GEMM_BENCH_TORCH=0 GEMM_BENCH_CUSTOM="$SH" timeout -k 10 120 python3 tools/gemm_bench.py 40 > $O/d$dbg.txt 2>&1 || exit $?
   grep -v amdgpu $O/d$dbg.txt | sed "s/^/dbg $dbg: /"
