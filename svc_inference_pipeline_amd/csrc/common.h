@@ -156,6 +156,7 @@ struct ConvGemmArgs {
   const int* tv;
   int tv_mul;
   int bf16;      // operands (X, W) are bfloat16 (Op16<true>); the epilogue's 16-bit inputs / outputs too
+  const f16* Wfrag;  // W once more in a kernel's own fragment order (gate_ws; NULL: none)
 };
 
 __device__ __forceinline__ int valid_in_rows(const ConvGemmArgs& a, int b) {

@@ -109,7 +109,11 @@ int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
 bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e);
+extern unsigned long long* gate_ws_stamps;
+int gate_ws_nstamp();
 int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
+int gate_ws_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
+size_t gate_ws_pack_elems();
 int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, const float* add, float div, f16* hi,
              f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s);
 int res_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
@@ -242,7 +246,8 @@ struct PackedGemm {
   int N = 0, Npad = 0, K = 0, Kpad = 0, Cp = 0, Cin = 0, taps = 0;
   int tap_mul = 1, tap_add = 0, istride = 1;
   bool bf16 = false;  // W (and so the GEMM's operands) in bfloat16 (the bf16 operand variant, common.h Op16)
-  f16* Wfrag = nullptr;  // the DiffSVC residual projections: W in res_proj's fragment order (res_proj.hip)
+  f16* Wfrag = nullptr;  // W in a kernel's fragment order: the DiffSVC residual projections (res_proj.hip), the dilated
+                         // convs (gate_ws.hip)
 };
 
 // host-side rounding of a weight to the 16-bit operand format: binary16 (default) or bfloat16 (round to nearest even)
@@ -679,6 +684,7 @@ static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cv
   a.T_out = T_out;
   a.N = g.N;
   a.bf16 = g.bf16 ? 1 : 0;
+  a.Wfrag = g.Wfrag;
   if (e.T_ostore == 0) {
     e.T_ostore = T_out;
     e.ostride = 1;
@@ -1064,6 +1070,15 @@ int build_mapper(svc_ctx* c) {
     dpb[i] = pb;
     const int d = 1 << (i % c->dil_cycle);
     if ((st = pack_conv1d(c, c->dil[i], dw->host, db->host, 2 * C, C, 3, C, d, d, 1, &perm))) return st;
+    if (C == 384 && c->dil[i].Kpad == 3 * C) {  // gate_ws's shape: its weights once more, in its fragment order
+      void* wf = nullptr;
+      SVC_HIP_CHECK(hipMalloc(&wf, gate_ws_pack_elems() * sizeof(f16)));
+      c->allocs.push_back(wf);
+      c->weight_bytes += (int64_t)(gate_ws_pack_elems() * sizeof(f16));
+      c->dil[i].Wfrag = reinterpret_cast<f16*>(wf);
+      if ((st = gate_ws_pack(c->dil[i].W, c->dil[i].Kpad, c->dil[i].Wfrag, 0))) return st;
+      SVC_HIP_CHECK(hipStreamSynchronize(0));
+    }
     // rows 0..C-1 of output_projection are the residual, C..2C-1 the skip (modules/diffsvc.py:229-231)
     if ((st = pack_conv1d(c, c->outres[i], ow->host, ob->host, C, C, 1, C, 1, 0, 1))) return st;
     if (C == 384) {  // res_proj's shape: its weights once more, in MFMA fragment order
@@ -2819,11 +2834,15 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
       e.ld_acc = N; e.acc_div = 1.41421356237309515f; e.add16 = bias;
     }
   }
-  f16* Wf = nullptr;  // variant 30: res_proj's fragment-order weights
+  f16* Wf = nullptr;  // variant 30 / 40: res_proj's / gate_ws's fragment-order weights
   int st = SVC_OK;
   if (variant == 30) {
     SVC_HIP_CHECK(hipMalloc(&Wf, res_proj_pack_elems() * sizeof(f16)));
     st = res_proj_pack(W, Kpad, Wf, 0);  // (on failure: no launches below, the buffers are freed at the end)
+  } else if (variant == 40) {
+    SVC_HIP_CHECK(hipMalloc(&Wf, gate_ws_pack_elems() * sizeof(f16)));
+    st = gate_ws_pack(W, Kpad, Wf, 0);
+    a.Wfrag = Wf;
   }
   hipEvent_t e0, e1;
   SVC_HIP_CHECK(hipEventCreate(&e0));
@@ -2843,6 +2862,24 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
     return conv_gemm3(a, e, zero_page(), variant - 10, 0);
   };
   for (int w = 0; w < 2 && !st; ++w) st = run();
+  if (const char* sp = variant == 40 ? getenv("SVC_GWS_STAMPS") : nullptr) {  // (bench tool only) step timeline
+    unsigned long long* ds = nullptr;
+    const size_t n = (size_t)256 * gate_ws_nstamp();
+    SVC_HIP_CHECK(hipMalloc(&ds, n * 8));
+    SVC_HIP_CHECK(hipMemset(ds, 0, n * 8));
+    SVC_HIP_CHECK(hipDeviceSynchronize());
+    gate_ws_stamps = ds;
+    for (int w = 0; w < 3 && !st; ++w) st = run();  // the last launch's stamps remain
+    gate_ws_stamps = nullptr;
+    SVC_HIP_CHECK(hipDeviceSynchronize());
+    std::vector<unsigned long long> hs(n);
+    SVC_HIP_CHECK(hipMemcpy(hs.data(), ds, n * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(ds);
+    if (FILE* f = fopen(sp, "wb")) {
+      fwrite(hs.data(), 8, n, f);
+      fclose(f);
+    }
+  }
   if (const char* dump = getenv("SVC_BENCH_DUMP")) {  // (bench tool only) the gate output of the warm-up launches
     SVC_HIP_CHECK(hipDeviceSynchronize());
     std::vector<f16> hy((size_t)M * N / 2);

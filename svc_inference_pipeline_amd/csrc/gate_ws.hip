@@ -64,7 +64,7 @@ static_assert(GW_GBYTES % 1024 == 0 && GW_STRIDE % 16 == 0, "ring geometry");
 
 struct GateWsArgs {
   const f16* X;       // [M][384] layer input (the split residual stream's high half)
-  const f16* W;       // packed [768][1152]
+  const f16* W;       // W in fragment order (gate_ws_pack)
   const float* bias;  // [768] packed
   const f16* cp;      // [M][ld_cp] conditioner projection (packed order)
   int ld_cp;
@@ -76,7 +76,9 @@ struct GateWsArgs {
   int tv_mul, B;
   float invT;
   int dbg;            // diagnostics (SVC_GWS_DBG, timing only): 2 no MFMAs, 4 no gate arithmetic
+  unsigned long long* stamps;  // diagnostics (SVC_GWS_STAMPS, svc_gemm_bench only): s_memtime per workgroup and step
 };
+constexpr int GW_NSTAMP = 128;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 gw_desc(const void* base, int64_t bytes) {
@@ -106,6 +108,12 @@ __device__ __forceinline__ void gw_barrier() {
 
 union GwH4 { uint2 u; f16 h[4]; };
 
+// diagnostics: the first second wave's lane 0 records s_memtime at step boundaries into a buffer nothing else reads
+// (a second wave: its vector-memory operations are the compiler's to count; the first waves' waits are hand-counted)
+__device__ __forceinline__ void gw_stamp(const GateWsArgs& a, int i) {
+  if (a.stamps && threadIdx.x == 256 && i < GW_NSTAMP) a.stamps[blockIdx.x * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
+}
+
 // LDS byte offsets of a lane's three tap rows for row block j of the part (output row m = r_begin + 16 j + fr): ring
 // row (8 + 16 j + fr + (tap - 1) dil) mod 160, or the zero row when the tap's input frame lies outside the utterance's
 // valid rows
@@ -132,6 +140,55 @@ __device__ __forceinline__ void gw_tap_bases(const GateWsArgs& a, const int* tvt
     base[tap] = (ok ? rr * GW_STRIDE : GW_ZERO) + fk * 16;
   }
 }
+
+// W in fragment order (gate_ws_pack): for column group c, pair p, K half kh, K-step s, gate / filter g and lane l, the
+// 8 halves W[n][32 (18 kh + s) + 8 (l >> 4) ..], n = (g ? nf : ng) + (l & 15): each wave's 36 loads are contiguous KiB
+__device__ __forceinline__ size_t gw_frag_index(int c, int p, int kh, int s, int g) {
+  return (size_t)((((c * 4 + p) * 2 + kh) * GW_KH + s) * 2 + g) * 512;
+}
+
+// The lane's row of block j of the part: utterance bb and frame t, advanced block by block (no division per block)
+struct GwRow {
+  int m, bb, t, tvb;
+  __device__ __forceinline__ void init(const GateWsArgs& a, const int* tvt, int m0) {
+    m = m0;
+    bb = (int)((float)m * a.invT);
+    t = m - bb * a.T;
+    if (t < 0) {
+      --bb;
+      t += a.T;
+    } else if (t >= a.T) {
+      ++bb;
+      t -= a.T;
+    }
+    tvb = a.tv ? (m < a.M ? tvt[bb] : 0) : a.T;
+  }
+  __device__ __forceinline__ void next(const GateWsArgs& a, const int* tvt) {
+    m += 16;
+    t += 16;
+    bool moved = false;
+    while (t >= a.T) {
+      t -= a.T;
+      ++bb;
+      moved = true;
+    }
+    if (moved && a.tv) tvb = m < a.M ? tvt[bb] : 0;
+  }
+  // LDS byte offsets of the three tap rows for row block j: ring row (8 + 16 j + fr + (tap - 1) dil) mod 160, or the
+  // zero row when the tap's input frame lies outside the utterance's valid rows
+  __device__ __forceinline__ void bases(const GateWsArgs& a, int j, int fr, int fk, int base[3]) const {
+    const bool row_ok = m < a.M;
+    const int r0 = (16 * j) % GW_RROWS + GW_HALO + fr;  // < 160 + 23
+#pragma unroll
+    for (int tap = 0; tap < 3; ++tap) {
+      const int tp = t + (tap - 1) * a.dil;
+      const bool ok = row_ok && tp >= 0 && tp < tvb;
+      int rr = r0 + (tap - 1) * a.dil;  // in [0, 160 + 31)
+      rr = rr >= GW_RROWS ? rr - GW_RROWS : rr;
+      base[tap] = (ok ? rr * GW_STRIDE : GW_ZERO) + fk * 16;
+    }
+  }
+};
 
 template <bool BF>
 __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
@@ -174,15 +231,14 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
   const int* tvt = reinterpret_cast<const int*>(smw + GW_TVT);
   unsigned char* const part_buf = smw + GW_PART + pair * 2048;  // + (k & 1) * 8192
 
-  // W fragments of the swapped MFMA (its first operand): w[s] = W[n + fr][32 (18 kh + s) + 8 fk .. + 8]
+  // W fragments of the swapped MFMA (its first operand), this wave's K half: wg[s] / wf[s] = K-step 18 kh + s
   half8 wg[GW_KH], wf[GW_KH];
   auto load_w = [&]() {
-    const f16* pg = a.W + (size_t)(ng + fr) * GW_K + kh * GW_KH * 32 + fk * 8;
-    const f16* pf = a.W + (size_t)(nf + fr) * GW_K + kh * GW_KH * 32 + fk * 8;
+    const f16* wb = a.W + gw_frag_index(type, pair, kh, 0, 0) + lane * 8;
 #pragma unroll
     for (int s = 0; s < GW_KH; ++s) {
-      wg[s] = *reinterpret_cast<const half8*>(pg + s * 32);
-      wf[s] = *reinterpret_cast<const half8*>(pf + s * 32);
+      wg[s] = *reinterpret_cast<const half8*>(wb + (size_t)(2 * s) * 512);
+      wf[s] = *reinterpret_cast<const half8*>(wb + (size_t)(2 * s + 1) * 512);
     }
   };
 
@@ -217,6 +273,8 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     issue(2);
     issue(3);
     issue(4);
+    GwRow row;
+    row.init(a, tvt, r_begin + fr);
     gw_barrier();  // groups 0 and 1, the zero row and the length table
     // Block j reads groups j / 2 .. (j + 1) / 2, so group G's last reader is block 2 G + 1 (the second wave, step
     // 2 G + 2). Group g = (k + 7) / 2 >= 5 is issued at the start of odd steps k >= 3, into the slot of group g - 5,
@@ -227,7 +285,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       if (k < nsub) {
         if ((k & 1) && k >= 3) issue((k + 7) / 2);
         int base[3];
-        gw_tap_bases(a, tvt, r_begin + k * 16 + fr, k, fr, fk, base);
+        row.bases(a, k, fr, fk, base);
         floatx4 ag = {0.f, 0.f, 0.f, 0.f}, af = {0.f, 0.f, 0.f, 0.f};
         if (!(a.dbg & 2)) {
 #pragma unroll
@@ -240,6 +298,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
         unsigned char* pb = part_buf + (k & 1) * 8192 + lane * 16;
         *reinterpret_cast<floatx4*>(pb) = ag;
         *reinterpret_cast<floatx4*>(pb + 1024) = af;
+        row.next(a, tvt);
         if (k & 1) {
           if (seven) gw_vmwait<3 * PV>(); else gw_vmwait<3 * (PV - 1)>();
         } else {
@@ -251,47 +310,33 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     gw_vmwait<0>();  // (the groups issued past the part land before the workgroup's LDS is released)
   } else {
     // ------------------------------------------------------------------ second waves: K-steps 18..35 + gate epilogue
+    // Step k: the MFMAs of block k - 1 (its partial sums come from step k - 1), interleaved with the gate epilogue of
+    // block k - 2, whose accumulators this wave kept from step k - 1: the epilogue's VALU work runs in the MFMAs'
+    // issue shadow instead of after them. The last block's epilogue follows the loop.
     const __amdgpu_buffer_rsrc_t rcp =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.cp), (short)0, a.M * a.ld_cp * 2, GW_CFG);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y, (short)0, a.M * a.ldy * 2, GW_CFG);
+    gw_stamp(a, 0);
     load_w();
     const float4 bg = *reinterpret_cast<const float4*>(a.bias + ng + 4 * fk);
     const float4 bfv = *reinterpret_cast<const float4*>(a.bias + nf + 4 * fk);
-    // conditioner projection of blocks blk (in use), blk + 1 and blk + 2 (in flight) in three register sets with
-    // fixed roles (blocks = 0, 1, 2 mod 3; the step loop is unrolled by 3), so no register move waits on a load
+    // conditioner projection of block j, loaded in step j (two steps before its epilogue) into register set j % 3:
+    // fixed roles per set (the step loop is unrolled by 3), so no register move waits on a load
     auto load_cp = [&](int blk, GwH4* dst) {
       const uint32_t vo = (uint32_t)(r_begin + blk * 16 + fr) * (uint32_t)(a.ld_cp * 2);  // rows past M read 0
       dst[0].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (ng + 4 * fk) * 2, 0, 0));
       dst[1].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (nf + 4 * fk) * 2, 0, 0));
     };
     GwH4 c0[2], c1[2], c2[2];
-    load_cp(0, c0);
-    load_cp(1, c1);
+    floatx4 pg = {0.f, 0.f, 0.f, 0.f}, pf = {0.f, 0.f, 0.f, 0.f};  // accumulators of the block awaiting its epilogue
+    GwRow row;
+    row.init(a, tvt, r_begin + fr);
+    gw_stamp(a, 1);
     gw_barrier();  // (pairs with the first waves' prologue barrier)
-    // block blk: its partial sums and ring groups are in since the barrier ending step blk (the first waves' block)
-    auto step = [&](int blk, const GwH4* cur, GwH4* next2) {
-      load_cp(blk + 2, next2);
-      const int m = r_begin + blk * 16 + fr;
-      int base[3];
-      gw_tap_bases(a, tvt, m, blk, fr, fk, base);
-      const unsigned char* pb = part_buf + (blk & 1) * 8192 + lane * 16;
-      floatx4 ag = *reinterpret_cast<const floatx4*>(pb);
-      floatx4 af = *reinterpret_cast<const floatx4*>(pb + 1024);
-      // the second wave's MFMAs go first on the SIMD (priority 1), so its gate epilogue (VALU) runs beside the first
-      // wave's remaining MFMAs instead of after them (+6 % on the kernel in the round-4 super-block form, r04c)
-      __builtin_amdgcn_s_setprio(1);
-      if (!(a.dbg & 2)) {
-#pragma unroll
-        for (int s = 0; s < GW_KH; ++s) {  // K-steps 18..23: tap 1 channels 192..383; 24..35: tap 2
-          const int ks = GW_KH + s;
-          const half8 av = *reinterpret_cast<const half8*>(smw + base[ks / 12] + (ks % 12) * 64);
-          ag = O::mfma(wg[s], av, ag);
-          af = O::mfma(wf[s], av, af);
-        }
-      }
-      __builtin_amdgcn_s_setprio(0);
-      // gate in registers (conv_gemm4's DIRECT epilogue arithmetic, same order); rows past the part are dropped
-      const GwH4 cg = cur[0], cf = cur[1];
+    gw_stamp(a, 2);
+    // gate in registers (conv_gemm4's DIRECT epilogue arithmetic, same order); rows past the part are dropped
+    auto epilogue = [&](int blk, const GwH4* cp, floatx4 ag, floatx4 af) {
+      const GwH4 cg = cp[0], cf = cp[1];
       GwH4 pk;
       if (a.dbg & 4) {
         pk.h[0] = (f16)(ag[0] + af[1]);
@@ -304,24 +349,90 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
         pk.h[2] = O::enc_lo(gate_act(ag[2] + bg.z + O::dec(cg.h[2]), af[2] + bfv.z + O::dec(cf.h[2])));
         pk.h[3] = O::enc_lo(gate_act(ag[3] + bg.w + O::dec(cg.h[3]), af[3] + bfv.w + O::dec(cf.h[3])));
       }
+      const int m = r_begin + blk * 16 + fr;
       const uint32_t vo = m < r_end ? (uint32_t)m * (uint32_t)(a.ldy * 2) + (uint32_t)ch * 2 : GW_OOR;
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, pk.u), ry,
                                             vo, 0, 0);
-      gw_barrier();
     };
-    gw_barrier();  // step 0 (the first waves' block 0)
-    for (int blk = 0; blk < nsub; blk += 3) {
-      step(blk, c0, c2);
-      if (blk + 1 < nsub) step(blk + 1, c1, c0);
-      if (blk + 2 < nsub) step(blk + 2, c2, c1);
+    // step k: load cp(k) into `ld`, MFMAs of block k - 1, epilogue of block k - 2 from `ep`
+    auto step = [&](int k, GwH4* ld, const GwH4* ep) {
+      if (k < nsub) load_cp(k, ld);
+      floatx4 ag = {0.f, 0.f, 0.f, 0.f}, af = {0.f, 0.f, 0.f, 0.f};
+      if (k >= 1) {
+        const int blk = k - 1;
+        int base[3];
+        row.bases(a, blk, fr, fk, base);
+        const unsigned char* pb = part_buf + (blk & 1) * 8192 + lane * 16;
+        ag = *reinterpret_cast<const floatx4*>(pb);
+        af = *reinterpret_cast<const floatx4*>(pb + 1024);
+        // the second wave's MFMAs go first on the SIMD (priority 1), so the first wave's run beside this wave's VALU
+        __builtin_amdgcn_s_setprio(1);
+        if (!(a.dbg & 2)) {
+#pragma unroll
+          for (int s = 0; s < GW_KH; ++s) {  // K-steps 18..23: tap 1 channels 192..383; 24..35: tap 2
+            const int ks = GW_KH + s;
+            const half8 av = *reinterpret_cast<const half8*>(smw + base[ks / 12] + (ks % 12) * 64);
+            ag = O::mfma(wg[s], av, ag);
+            af = O::mfma(wf[s], av, af);
+          }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        row.next(a, tvt);
+      }
+      if (k >= 2) epilogue(k - 2, ep, pg, pf);
+      pg = ag;
+      pf = af;
+      gw_barrier();
+      gw_stamp(a, 3 + k);
+    };
+    for (int k = 0; k <= nsub; k += 3) {
+      step(k, c0, c1);
+      if (k + 1 <= nsub) step(k + 1, c1, c2);
+      if (k + 2 <= nsub) step(k + 2, c2, c0);
+    }
+    // the last block's epilogue (its cp went into set (nsub - 1) % 3)
+    const int last = nsub - 1;
+    switch (last % 3) {
+      case 0: epilogue(last, c0, pg, pf); break;
+      case 1: epilogue(last, c1, pg, pf); break;
+      default: epilogue(last, c2, pg, pf); break;
     }
   }
 }
 
-// Does gate_ws take this launch? (the DiffSVC dilated-conv shape: 384 channels, 3 centred taps of dilation 1/2/4/8)
+// W (packed [768][1152], W[n][k]) -> gate_ws fragment order (gw_frag_index): 16 B per thread
+__global__ void gate_ws_pack_kernel(const f16* __restrict__ W, f16* __restrict__ Wf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // 16-B unit
+  if (i >= GW_N * GW_K / 8) return;
+  const int lane = i & 63;
+  int r = i >> 6;
+  const int g = r & 1;
+  r >>= 1;
+  const int s = r % GW_KH;
+  r /= GW_KH;
+  const int kh = r & 1;
+  r >>= 1;
+  const int p = r & 3, c = r >> 2;
+  const int n = 64 * (2 * c + (p >> 1)) + 16 * (p & 1) + 32 * g + (lane & 15);
+  const int k = 32 * (GW_KH * kh + s) + 8 * (lane >> 4);
+  *reinterpret_cast<uint4*>(Wf + (size_t)i * 8) = *reinterpret_cast<const uint4*>(W + (size_t)n * GW_K + k);
+}
+
+int gate_ws_pack(const f16* W, int ldw, f16* Wf, hipStream_t s) {
+  SVC_REQUIRE(ldw == GW_K && ((uintptr_t)W & 15) == 0 && ((uintptr_t)Wf & 15) == 0, "gate_ws_pack: ldw %d", ldw);
+  hipLaunchKernelGGL(gate_ws_pack_kernel, dim3(cdiv(GW_N * GW_K / 8, 256)), dim3(256), 0, s, W, Wf);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+size_t gate_ws_pack_elems() { return (size_t)GW_N * GW_K; }
+
+// diagnostics (svc_gemm_bench with SVC_GWS_STAMPS): a [256][GW_NSTAMP] s_memtime buffer, else NULL
+unsigned long long* gate_ws_stamps = nullptr;
+int gate_ws_nstamp() { return GW_NSTAMP; }
+
 bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e) {
   const int d = a.tap_mul;
-  return e.kind == EPI_GATE && e.cp && e.y16 && e.bias && a.Cp == GW_C && a.Cvalid == GW_C && a.ldx == GW_C &&
+  return e.kind == EPI_GATE && e.cp && e.y16 && e.bias && a.Wfrag && a.Cp == GW_C && a.Cvalid == GW_C && a.ldx == GW_C &&
          a.K == GW_K && a.Kpad == GW_K && a.N == GW_N && (d == 1 || d == 2 || d == 4 || d == 8) && a.tap_add == -d &&
          a.istride == 1 && a.T_in == a.T_out && (!a.tv || a.B <= GW_MAXB) && e.ld_cp % 4 == 0 && e.ldy16 % 4 == 0 &&
          (int64_t)a.B * a.T_out * std::max(e.ld_cp, std::max(e.ldy16, GW_C)) * 2 < (1ll << 30);
@@ -329,14 +440,14 @@ bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e) {
 
 int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   SVC_REQUIRE(gate_ws_fits(a, e), "gate_ws: not the DiffSVC dilated-conv gate shape");
-  SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0 && ((uintptr_t)e.cp & 7) == 0 &&
+  SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.Wfrag & 15) == 0 && ((uintptr_t)e.cp & 7) == 0 &&
                   ((uintptr_t)e.y16 & 7) == 0 && ((uintptr_t)e.bias & 15) == 0,
               "gate_ws: alignment");
   const int M = a.B * a.T_out;
   if (M == 0) return SVC_OK;
   static const int dbg = getenv("SVC_GWS_DBG") ? atoi(getenv("SVC_GWS_DBG")) : 0;  // (diagnostics, read once)
-  GateWsArgs g{a.X, a.W, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
-               1.0f / (float)a.T_out, dbg};
+  GateWsArgs g{a.X, a.Wfrag, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
+               1.0f / (float)a.T_out, dbg, gate_ws_stamps};
   const int bf = a.bf16 ? 1 : 0;
   const void* fn = bf ? (const void*)gate_ws_kernel<true> : (const void*)gate_ws_kernel<false>;
   if (int st = ensure_dyn_lds(fn, GW_LDS)) return st;
