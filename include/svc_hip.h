@@ -91,6 +91,15 @@ svc_status svc_mel_energy(svc_ctx* ctx, const float* wav24k, int B, int64_t n_sa
 svc_status svc_f0_ac(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples, const int64_t* utt_samples, int T,
                      double* f0, void* stream);
 
+/* F4: pYIN F0, utils/f0.py:95-117 get_f0_features_using_pyin(audio, fs, win_length, hop_length,
+   f0_min, f0_max) = librosa.pyin with its defaults (frame_length 2048, centred frames, 100 beta(2, 18) thresholds,
+   0.1-semitone bins, Viterbi decoding) and the unvoiced frames set to 0. wav [B][n_samples] f32 -> f0 [B*T] float64,
+   utterance b's frames 1 + utt_samples[b] / hop_length, the rest of its T rows 0 (T >= 1 + n_samples / hop_length
+   when every utterance is full length). Uses the feature-stage workspace, like svc_f0_ac; the context need not be
+   finalized. Parity is unpinned (librosa is absent here): tests/test_f0.py holds it to oracle/pyin.py. */
+svc_status svc_f0_pyin(svc_ctx* ctx, const float* wav, int B, int64_t n_samples, const int64_t* utt_samples, double fs,
+                       int win_length, int hop_length, double f0_min, double f0_max, int T, double* f0, void* stream);
+
 /* A4: in place, f0 [B*T] float64 *= target_median / median(voiced f0 of that utterance)
    (utils/acoustic_feature_extraction.py:33-52; np.median semantics, NaN when no frame is voiced). */
 svc_status svc_pitch_shift(svc_ctx* ctx, double* f0, int B, int T, double target_median, void* stream);

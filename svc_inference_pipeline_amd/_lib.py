@@ -24,6 +24,8 @@ PROTOTYPES = {
     "svc_ctx_stream": (c_int, [c_void_p, c_int, ctypes.POINTER(c_void_p)]),
     "svc_mel_energy": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
     "svc_f0_ac": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_int, c_void_p, c_void_p]),
+    "svc_f0_pyin": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_double, c_int, c_int, c_double, c_double,
+                            c_int, c_void_p, c_void_p]),
     "svc_pitch_shift": (c_int, [c_void_p, c_void_p, c_int, c_int, c_double, c_void_p]),
     "svc_whisper_encode": (c_int, [c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p]),
     "svc_map_content": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),

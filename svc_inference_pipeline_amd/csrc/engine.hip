@@ -101,7 +101,7 @@ int conv_post(const f16* a, int lda, int B, int L, int C, const float* w, float 
               float* out, hipStream_t s, const int* tv = nullptr, int tv_mul = 1);
 int zero_tail_rows(float* x, int B, int T, int C, const int* Tb, hipStream_t s);
 int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s,
-                      int split_c, bool bf);
+                      int split_c, bool bf, int ldo);
 int layernorm_f16x3(const float* x, const float* g, const float* b, f16* y, int rows, int D, hipStream_t s, bool bf);
 int f32_to_f16x3_grouped(const float* x, f16* y, int rows, int C, int Cg, hipStream_t s, bool bf);
 int f16_to_f32(const f16* x, float* y, int64_t n, hipStream_t s);
@@ -134,6 +134,13 @@ int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double ti
                 double ceiling_hz, double voicing, int T, double* f0_out, void* workspace, size_t ws_bytes,
                 hipStream_t s, const int64_t* n_b = nullptr, const int* T_b = nullptr, StageRing* ring = nullptr);
 size_t f0_workspace_bytes(int B, int64_t n_samples, double fs, double time_step, double floor_hz);
+size_t pyin_table_doubles(double sr, double fmin, double fmax, int frame_length, int win_length, int hop);
+size_t pyin_workspace_bytes(int B, int F, double sr, double fmin, double fmax, int frame_length, int win_length,
+                            int hop);
+int pyin_tables(double sr, double fmin, double fmax, int frame_length, int win_length, int hop, double* out);
+int f0_pyin(const float* wav, int B, int64_t ld, const int64_t* nvalid_dev, const int64_t* nvalid_host, double sr,
+            double fmin, double fmax, int frame_length, int win_length, int hop, int F, double* f0, void* ws,
+            size_t ws_bytes, const double* tables_dev, hipStream_t s);
 
 // ---------------------------------------------------------------------------- host helpers
 static std::vector<float> slaney_mel(int sr, int n_fft, int n_mels, double f_lo, double f_hi) {
@@ -407,6 +414,7 @@ struct svc_ctx {
   bool has_whisper = false;
   int wD = 0, wH = 0, wL = 0, wctx = 0, wmels = 80;
   PackedGemm wconv1, wconv2;
+  int wstem_ld = 0;  // row stride (halves) of the conv stem's log-mel operand (split: 3 n_mels padded to 64)
   float *wpos = nullptr, *wlnp_g = nullptr, *wlnp_b = nullptr;
   std::vector<WBlock> wblocks;
   // hubert / contentvec (A8)
@@ -525,10 +533,12 @@ int pack_gemm(svc_ctx* c, PackedGemm& g, int N, int Cin, int Cp, int taps, WG wg
 
 // Split-fp16 packing of a 1-tap GEMM for the [x_hi | x_lo | x_hi] operand of f32_to_f16x3:
 // W'[n] = [f16(w) | f16(w) | f16(w - f16(w))] over K = 3 * Cin.
+// Cp > 3 * Cin: each tap's K segment padded to Cp (zero weights), e.g. to a multiple of 64 for the buffer-descriptor
+// K-loop (the Whisper conv stem: 3 x 80 -> 256 per tap, its operand rows padded to match).
 template <typename WG, typename BG>
-int pack_gemm_split3(svc_ctx* c, PackedGemm& g, int N, int Cin, WG wget, BG bget, int taps = 1) {
+int pack_gemm_split3(svc_ctx* c, PackedGemm& g, int N, int Cin, WG wget, BG bget, int taps = 1, int Cp = 0) {
   return pack_gemm(
-      c, g, N, 3 * Cin, 3 * Cin, taps,
+      c, g, N, 3 * Cin, Cp > 0 ? Cp : 3 * Cin, taps,
       [&](int n, int ci, int t) {
         const int seg = ci / Cin;
         const float w = wget(n, ci - seg * Cin, t);
@@ -766,7 +776,22 @@ int build_whisper(svc_ctx* c) {
   const int mode = c->content_mode;
   const bool sp = mode != 0;
   SVC_REQUIRE(!sp || nm % 8 == 0, "whisper split precision: n_mels %d", nm);
-  int st = pack_conv1d_opt(c, c->wconv1, c1w->host, c1b->host, D, nm, 3, (int)round_up(nm, 8), 1, 1, 1, sp);
+  // the split stem's operand rows [hi | lo | hi] (3 n_mels = 240 wide) are stored 256 wide with a zero pad, and each
+  // tap's K segment padded to match, so a K-tile of 64 lies in one tap (the K-loop's buffer-descriptor form):
+  // 768 instead of 720-deep K, but no per-lane tap arithmetic
+  int st;
+  if (sp) {
+    c->wstem_ld = (int)round_up(3 * nm, 64);
+    st = pack_gemm_split3(
+        c, c->wconv1, D, nm, [&](int n, int ci, int t) { return c1w->host[((int64_t)n * nm + ci) * 3 + t]; },
+        [&](int n) { return c1b->host[n]; }, 3, c->wstem_ld);
+    c->wconv1.tap_mul = 1;
+    c->wconv1.tap_add = -1;
+    c->wconv1.istride = 1;
+  } else {
+    c->wstem_ld = (int)round_up(nm, 8);
+    st = pack_conv1d(c, c->wconv1, c1w->host, c1b->host, D, nm, 3, c->wstem_ld, 1, 1, 1);
+  }
   if (st) return st;
   st = pack_conv1d_opt(c, c->wconv2, c2w->host, c2b->host, D, D, 3, D, 1, 1, 2, sp);
   if (st) return st;
@@ -1695,6 +1720,31 @@ svc_status svc_f0_ac(svc_ctx* c, const float* wav, int B, int64_t n, const int64
                      (hipStream_t)stream, n_samples, n_samples ? Tb.data() : nullptr, &c->lens_feat);
 }
 
+svc_status svc_f0_pyin(svc_ctx* c, const float* wav, int B, int64_t n, const int64_t* n_samples, double fs,
+                       int win_length, int hop_length, double f0_min, double f0_max, int T, double* f0, void* stream) {
+  SVC_REQUIRE(c, "null context");
+  TuningScope tuning_scope_(&c->tune);
+  SVC_HIP_CHECK(hipSetDevice(c->device));
+  const int FL = 2048;  // librosa.pyin frame_length default (utils/f0.py:107 leaves it unset)
+  const size_t nt = pyin_table_doubles(fs, f0_min, f0_max, FL, win_length, hop_length);
+  if (!nt) return SVC_ERR_INVALID;  // (pyin_plan set the error)
+  SVC_REQUIRE(B > 0 && n > 0 && T > 0, "pyin: B=%d n=%lld T=%d", B, (long long)n, T);
+  const size_t need = pyin_workspace_bytes(B, T, fs, f0_min, f0_max, FL, win_length, hop_length);
+  int st;
+  if ((st = c->auxws.reserve(std::max(need + 4096, c->auxws.cap)))) return st;
+  // one staged table per call (the ring retires its last slot): [lengths int64 B][pyin tables f64]
+  std::vector<double> buf(B + nt);
+  if (n_samples) memcpy(buf.data(), n_samples, (size_t)B * 8);
+  if ((st = pyin_tables(fs, f0_min, f0_max, FL, win_length, hop_length, buf.data() + B))) return st;
+  hipStream_t s = (hipStream_t)stream;
+  RingRetire retire_(c->lens_feat, s);
+  void* dev = nullptr;
+  if ((st = c->lens_feat.put(buf.data(), buf.size() * 8, s, &dev))) return st;
+  const int64_t* nb_dev = n_samples ? reinterpret_cast<const int64_t*>(dev) : nullptr;
+  return f0_pyin(wav, B, n, nb_dev, n_samples, fs, f0_min, f0_max, FL, win_length, hop_length, T, f0, c->auxws.base,
+                 c->auxws.cap, reinterpret_cast<const double*>(dev) + B, s);
+}
+
 svc_status svc_pitch_shift(svc_ctx* c, double* f0, int B, int T, double target_median, void* stream) {
   SVC_REQUIRE(c && f0 && B > 0 && T > 0, "pitch_shift: bad args");
   SVC_HIP_CHECK(hipSetDevice(c->device));
@@ -1714,13 +1764,14 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   const size_t rows1 = (size_t)B * F, rows2 = (size_t)B * L;
   const int X3 = c->content_split ? 3 : 1;  // split-fp16 block operands are [hi | lo | hi] rows
   const int XS = c->content_mode != 0 ? 3 : 1;  // the conv stem is split-fp16 in both split modes
-  size_t need = rows1 * c->wmels * 4 + rows1 * c->wmels * 2 * XS + rows1 * D * 2 * XS /*h1*/ +
+  const int LDM = XS == 3 ? c->wstem_ld : c->wmels;  // the stem operand's row stride
+  size_t need = rows1 * c->wmels * 4 + rows1 * LDM * 2 + rows1 * D * 2 * XS /*h1*/ +
                 rows2 * D * 4 + rows2 * D * 2 * X3 + rows2 * 3 * D * 2 + rows2 * D * 2 + rows2 * 4 * D * 2 * X3 + 64 * 4096;
   int st;
   if ((st = c->ws.reserve(std::max(need, c->ws.cap)))) return st;
   c->ws.reset();
   WS_GET(float, ls, rows1 * c->wmels);
-  WS_GET(f16, lm16, rows1 * c->wmels * XS);
+  WS_GET(f16, lm16, rows1 * LDM);
   WS_GET(float, mx, B);
   DftArgs a{};
   a.wav = wav16;
@@ -1741,7 +1792,8 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   a.n_mels = c->wmels;
   a.out = ls;
   if ((st = dft_mel(a, B, s))) return st;
-  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s, XS == 3 ? c->wmels : 0, c->bf16))) return st;
+  if ((st = whisper_normalize(ls, mx, lm16, B, (int64_t)F * c->wmels, s, XS == 3 ? c->wmels : 0, c->bf16, LDM)))
+    return st;
   // conv stem
   WS_GET(f16, h1, rows1 * D * XS);
   EpiArgs e = epi();
@@ -1749,7 +1801,7 @@ svc_status svc_whisper_encode(svc_ctx* c, const float* wav16, int B, int64_t n, 
   e.out16 = h1;
   e.ld16 = D * XS;
   e.split16 = XS == 3 ? D : 0;
-  if ((st = run_gemm(c->wconv1, lm16, c->wmels * XS, c->wmels * XS, B, F, F, e, s, "whisper.conv1"))) return st;
+  if ((st = run_gemm(c->wconv1, lm16, LDM, LDM, B, F, F, e, s, "whisper.conv1"))) return st;
   WS_GET(float, x, rows2 * D);
   e = epi();
   e.act = ACT_GELU;
@@ -2902,6 +2954,22 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
       ms += one;
     }
     (void)hipFree(flush);
+  } else if (getenv("SVC_BENCH_PERLAUNCH")) {  // (bench tool only) each launch between its own event pair, as
+    // bench.py's live profile brackets them: the event markers' own cost per launch
+    std::vector<hipEvent_t> ev(2 * (size_t)iters);
+    for (auto& x : ev) SVC_HIP_CHECK(hipEventCreate(&x));
+    for (int i = 0; i < iters && !st; ++i) {  // back to back, no host synchronisation in between
+      SVC_HIP_CHECK(hipEventRecord(ev[2 * i], 0));
+      st = run();
+      SVC_HIP_CHECK(hipEventRecord(ev[2 * i + 1], 0));
+    }
+    SVC_HIP_CHECK(hipEventSynchronize(ev.back()));
+    for (int i = 0; i < iters; ++i) {
+      float one = 0;
+      SVC_HIP_CHECK(hipEventElapsedTime(&one, ev[2 * i], ev[2 * i + 1]));
+      ms += one;
+    }
+    for (auto& x : ev) (void)hipEventDestroy(x);
   } else {
     SVC_HIP_CHECK(hipEventRecord(e0, 0));
     for (int i = 0; i < iters && !st; ++i)

@@ -304,7 +304,7 @@ __global__ void rowblock_max_kernel(const float* __restrict__ x, int64_t n_per_u
 }
 
 __global__ void whisper_norm_kernel(const float* __restrict__ x, const float* __restrict__ mx, f16* __restrict__ y,
-                                    int64_t n_per_utt, int B, int split_c, bool bf) {
+                                    int64_t n_per_utt, int B, int split_c, bool bf, int ldo) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_per_utt * B) return;
   int b = (int)(i / n_per_utt);
@@ -314,23 +314,26 @@ __global__ void whisper_norm_kernel(const float* __restrict__ x, const float* __
     y[i] = enc16_lo(o, bf);
     return;
   }
-  // split-fp16 operand rows [hi | lo | hi] of split_c (= n_mels) columns each
+  // split-fp16 operand rows [hi | lo | hi] of split_c (= n_mels) columns each, ldo apart; columns 3 split_c .. ldo - 1
+  // are zeros (the conv stem's K padding)
   const int64_t r = i / split_c;
   const int c = (int)(i - r * split_c);
   const f16 hi = enc16_lo(o, bf);
-  f16* yr = y + r * 3 * split_c;
+  f16* yr = y + r * ldo;
   yr[c] = hi;
   yr[split_c + c] = enc16_lo(o - dec16(hi, bf), bf);
   yr[2 * split_c + c] = hi;
+  if (c < ldo - 3 * split_c) yr[3 * split_c + c] = (f16)0.0f;
 }
 
 int whisper_normalize(const float* logspec, float* mx_scratch, f16* out, int B, int64_t n_per_utt, hipStream_t s,
-                      int split_c, bool bf) {
+                      int split_c, bool bf, int ldo) {
+  SVC_REQUIRE(split_c == 0 || (ldo >= 3 * split_c && ldo - 3 * split_c <= split_c), "whisper_normalize: ldo %d", ldo);
   hipLaunchKernelGGL(rowblock_max_kernel, dim3(B), dim3(1024), 0, s, logspec, n_per_utt, mx_scratch);
   SVC_LAUNCH_CHECK();
   int64_t n = n_per_utt * B;
   hipLaunchKernelGGL(whisper_norm_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, logspec, mx_scratch, out, n_per_utt, B,
-                     split_c, bf);
+                     split_c, bf, ldo);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

@@ -215,6 +215,21 @@ class SVCEngine:
                   _ptr(f0), _stream())
         return f0
 
+    def f0_pyin(self, wav24, n_samples=None, win_length=None, hop_length=None, f0_min=None, f0_max=None, T=None):
+        """pYIN F0 (utils/f0.py:95-117 get_f0_features_using_pyin: librosa.pyin defaults, unvoiced frames 0) ->
+        f64 [B, T], T = 1 + N // hop_length by default (librosa's centred frame count). Arguments default to the
+        config's fs / win_length / hop_length / f0_min / f0_max, as the reference's callers pass them."""
+        B, N = wav24.shape
+        hop = self.cfg.hop_length if hop_length is None else int(hop_length)
+        win = self.cfg.win_length if win_length is None else int(win_length)
+        lo = self.cfg.f0_min if f0_min is None else float(f0_min)
+        hi = self.cfg.f0_max if f0_max is None else float(f0_max)
+        T = 1 + N // hop if T is None else int(T)
+        f0 = torch.empty(B, T, device=wav24.device, dtype=torch.float64)
+        _lib.call("svc_f0_pyin", self._ctx, _ptr(wav24), B, N, _host_lengths(n_samples, B, ctypes.c_int64),
+                  float(self.cfg.fs), win, hop, float(lo), float(hi), T, _ptr(f0), _stream())
+        return f0
+
     def pitch_shift(self, f0, target_median=None):
         """In place: f0 *= target_median / median(voiced f0) per utterance
         (utils/acoustic_feature_extraction.py:33-52). f0 f64 [B, T]."""
