@@ -43,7 +43,8 @@ def build_engine(cfg, device=0, mapper_ckpt=None, vocoder_ckpt=None, whisper_ckp
     return SVCEngine(cfg, device, whisper_state=st["whisper"], mapper_state=st["mapper"], vocoder_state=st["vocoder"])
 
 
-def convert_file(engine, cfg, wav_path, singer_name, fast_inference=False, speedup=10, seed=0, device="cuda"):
+def convert_file(engine, cfg, wav_path, singer_name, fast_inference=False, speedup=10, seed=0, device="cuda",
+                 f0_method="parselmouth"):
     """One file through the GPU path -> (f32 waveform [T*hop] before save_audio's normalisation, T)."""
     wav24 = A.load_audio(wav_path, cfg.fs, device=device)          # utils/audio.py:10-55
     if wav24 is None:
@@ -54,12 +55,13 @@ def convert_file(engine, cfg, wav_path, singer_name, fast_inference=False, speed
         raise KeyError(f"unknown singer {singer_name!r}; known: {sorted(singers)}")
     singer = torch.tensor([int(singers[singer_name])], dtype=torch.int32, device=device)  # utils/util.py:49-54
     utt = torch.zeros(1, dtype=torch.int32, device=device)
-    res = SVCPipeline(engine).convert(wav24[None].contiguous(), wav16[None].contiguous(), singer,
+    res = SVCPipeline(engine, f0_method=f0_method).convert(wav24[None].contiguous(), wav16[None].contiguous(), singer,
                                       fast_inference=fast_inference, speedup=speedup, seed=seed, utt_ids=utt)
     return res.wav[0].cpu().numpy(), res.mel.shape[1]
 
 
-def convert_files(engine, cfg, wav_paths, singer_name, fast_inference=False, speedup=10, seed=0, device="cuda"):
+def convert_files(engine, cfg, wav_paths, singer_name, fast_inference=False, speedup=10, seed=0, device="cuda",
+                  f0_method="parselmouth"):
     """Several files as ONE ragged batch (SVCPipeline.convert_many, per-utterance lengths through the C-ABI) ->
     list of (f32 waveform [T_i*hop], T_i); file i uses utterance id i, so file 0 equals convert_file's result."""
     singers = C.load_singers(cfg)
@@ -73,7 +75,7 @@ def convert_files(engine, cfg, wav_paths, singer_name, fast_inference=False, spe
         w24.append(w)
         w16.append(A.load_whisper_audio(p, device=device))
     sid = int(singers[singer_name])
-    wavs = SVCPipeline(engine).convert_many(w24, w16, [sid] * len(w24), fast_inference=fast_inference,
+    wavs = SVCPipeline(engine, f0_method=f0_method).convert_many(w24, w16, [sid] * len(w24), fast_inference=fast_inference,
                                             speedup=speedup, seed=seed)
     hop = cfg.hop_length
     return [(w.cpu().numpy(), int(w.shape[0]) // hop) for w in wavs]
@@ -94,6 +96,8 @@ def main(argv=None):
     ap.add_argument("--whisper-ckpt", default=None)
     ap.add_argument("--random-weights", default=None, choices=sorted(W.WHISPER_DIMS))
     ap.add_argument("--device", type=int, default=0)
+    ap.add_argument("--f0-method", default="parselmouth", choices=("parselmouth", "pyin"),
+                    help="F0 extractor: Praat AC (the reference's infer.py) or pYIN (utils/f0.py:95-117)")
     args = ap.parse_args(argv)
 
     cfg = C.load_config(args.config) if args.config else C.load_config()
@@ -107,9 +111,11 @@ def main(argv=None):
     print("Converting...", flush=True)
     dev = f"cuda:{args.device}"
     if len(args.wav) == 1:
-        results = [convert_file(engine, cfg, args.wav[0], args.singer, args.fast, args.speedup, args.seed, device=dev)]
+        results = [convert_file(engine, cfg, args.wav[0], args.singer, args.fast, args.speedup, args.seed, device=dev,
+                                f0_method=args.f0_method)]
     else:
-        results = convert_files(engine, cfg, args.wav, args.singer, args.fast, args.speedup, args.seed, device=dev)
+        results = convert_files(engine, cfg, args.wav, args.singer, args.fast, args.speedup, args.seed, device=dev,
+                                f0_method=args.f0_method)
     print(f"Using time: {time.time() - t0:.3f}s ({sum(T for _, T in results)} frames, {len(results)} file(s))",
           flush=True)
     for path, (wav, _) in zip(args.wav, results):

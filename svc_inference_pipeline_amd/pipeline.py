@@ -42,11 +42,28 @@ class ConvertResult:
 
 
 class SVCPipeline:
-    def __init__(self, engine: SVCEngine, f0_side=True):
+    def __init__(self, engine: SVCEngine, f0_side=True, f0_method="parselmouth"):
         """f0_side: run the 24 kHz features (mel / energy, F0, pitch shift) on the context's sub-stream 2 beside the
-        content encoder (default; measured +0.4 %) instead of on the caller's stream."""
+        content encoder (default; measured +0.4 %) instead of on the caller's stream.
+        f0_method: "parselmouth" (utils/f0.py:120-161, what utils/acoustic_feature_extraction.py:53 uses) or "pyin"
+        (utils/f0.py:95-117 get_f0_features_using_pyin, svc_f0_pyin; its 1 + N // hop frames cut to the mel frames)."""
+        if f0_method not in ("parselmouth", "pyin"):
+            raise ValueError(f"f0_method {f0_method!r}: 'parselmouth' or 'pyin'")
         self.engine = engine
         self.f0_side = f0_side
+        self.f0_method = f0_method
+
+    def extract_f0(self, wav24, T, n_samples=None, T_b=None):
+        """F0 by the configured method -> f64 [B, T] (rows past an utterance's T_b frames 0)."""
+        e = self.engine
+        if self.f0_method == "parselmouth":
+            return e.f0(wav24, T, n_samples=n_samples)
+        N = wav24.shape[1]
+        f0 = e.f0_pyin(wav24, n_samples=n_samples, T=max(T, 1 + N // e.cfg.hop_length))[:, :T].contiguous()
+        if T_b is not None:
+            for b, tb in enumerate(T_b):
+                f0[b, tb:] = 0
+        return f0
 
     def content(self, wav16, T, wav16_float=None):
         """Content features of every type in cfg.mapper.content_feature mapped to T mel frames -> [B, T, sum of
@@ -119,7 +136,7 @@ class SVCPipeline:
         with torch.cuda.stream(side):
             mel, energy = e.mel_energy(wav24)
             # a caller-supplied f0 is shifted on a copy (svc_pitch_shift works in place)
-            f0 = e.f0(wav24, T) if f0 is None else f0.to(torch.float64).contiguous().clone()
+            f0 = self.extract_f0(wav24, T) if f0 is None else f0.to(torch.float64).contiguous().clone()
             e.pitch_shift(f0)
         assert mel.shape[1] == T
         content = self.content(wav16, T, wav16_float)
@@ -240,7 +257,7 @@ class SVCPipeline:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             mel, energy = e.mel_energy(w24, n_samples=n24)
-            f0 = e.f0(w24, T, n_samples=n24)
+            f0 = self.extract_f0(w24, T, n_samples=n24, T_b=T_b)
             e.pitch_shift(f0)
         content = self.ragged_content(list(wavs16), T_b, T, wavs16_float)
         main.wait_stream(side)

@@ -69,6 +69,10 @@ class _FakeEngine:
         self.calls.append(("f0", T, list(n_samples)))
         return torch.zeros(w24.shape[0], T, dtype=torch.float64)
 
+    def f0_pyin(self, w24, n_samples=None, T=None):
+        self.calls.append(("f0_pyin", T, list(n_samples)))
+        return torch.ones(w24.shape[0], T, dtype=torch.float64)  # every frame voiced at 1 Hz
+
     def pitch_shift(self, f0):
         return f0
 
@@ -139,3 +143,27 @@ def test_ragged_content_whisper_groups_and_hubert_buckets(monkeypatch):
     assert [c for c in eng.calls if c[0] == "whisper"] == [("whisper", (3, 32000))]  # one zero-padded batch
     for i in range(3):
         assert bool((out[i, :T_b[i]] == float(i + 1)).all()) and not out[i, T_b[i]:].any()
+
+
+def test_pyin_f0_method_cuts_to_mel_frames(monkeypatch):
+    """f0_method="pyin" (utils/f0.py:95-117): librosa's 1 + N // hop frames are cut to the mel frames, and the rows
+    past each utterance's own frames are zero, as the Praat path leaves them."""
+    import contextlib
+    monkeypatch.setattr(torch.cuda, "current_stream", lambda *a: types.SimpleNamespace(wait_stream=lambda s: None))
+    monkeypatch.setattr(torch.cuda, "stream", lambda s: contextlib.nullcontext())
+    eng = _FakeEngine()
+    seen = {}
+    cond = eng.condition
+    eng.condition = lambda content, f0, energy, singer: (seen.setdefault("f0", f0), cond(content, f0, energy, singer))[1]
+    pipe = SVCPipeline(eng, f0_side=False, f0_method="pyin")
+    lens = [2400, 4800, 1000]
+    pipe.convert_many([torch.zeros(n) for n in lens], [torch.zeros(n * 2 // 3) for n in lens], [0, 1, 2])
+    T_b = [(n + 768 - 1024) // 256 + 1 for n in lens]
+    call = next(c for c in eng.calls if c[0] == "f0_pyin")
+    assert call == ("f0_pyin", 1 + max(lens) // 256, lens)  # librosa's frame count for the batch length
+    f0 = seen["f0"]
+    assert f0.shape == (3, max(T_b))
+    for b, tb in enumerate(T_b):
+        assert bool((f0[b, :tb] == 1).all()) and not f0[b, tb:].any()
+    with pytest.raises(ValueError, match="f0_method"):
+        SVCPipeline(eng, f0_method="crepe")
