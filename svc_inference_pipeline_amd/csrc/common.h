@@ -285,13 +285,14 @@ struct Tuning {
                             // conv_gemm4 with the LDS-staged / register epilogue where N > 64
   int gemm3_direct = 3;     // conv_gemm3 register-epilogue forms in use (mask, gemm3.hip direct_form3)
   int whisper_streams = 1;  // Whisper encoder sub-batch streams
-  int sampler_streams = 2;  // DiffSVC sampler sub-batch streams
+  int sampler_streams = 1;  // DiffSVC sampler sub-batch streams (round 4: 1 with gate_ws; 2 was the conv_gemm4 default)
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
   int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip)
   int amp_maxc = 48;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none)
   int res_proj = 1;         // DiffSVC residual projection on the weight-stationary stream (res_proj.hip; 0: conv_gemm3;
-                            // > 1: that many row lanes of 2 workgroups instead of 3/8 of the CU count)
-  int gate_ws = 0;          // DiffSVC dilated conv + gate on the weight-stationary row stream (gate_ws.hip; 0: conv_gemm4)
+                            // > 1: that many row lanes of 2 workgroups instead of 1/2 (one sampler stream) or 3/8
+                            // (several) of the CU count)
+  int gate_ws = 1;          // DiffSVC dilated conv + gate on the weight-stationary row stream (gate_ws.hip; 0: conv_gemm4)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only, A/B runs)
   void from_env();
   bool set(const char* name, double v);  // false: unknown name ("reset" restores the creation-time values)

@@ -2135,7 +2135,8 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
       prof_site("diffsvc.outproj");
       if ((st = res_proj(bb.g16 + (size_t)i * bb.g_ls, c->outres[i].Wfrag, c->outres[i].bias,
                          dp + (size_t)i * C, dp + (size_t)(i + 1) * C, 1.41421356237309515f, bb.y16, bb.lo16, rows,
-                         c->outres[i].bf16, tuning().res_proj > 1 ? tuning().res_proj : 0, s)))
+                         c->outres[i].bf16,
+                         tuning().res_proj > 1 ? tuning().res_proj : (tuning().sampler_streams == 1 ? -2 : 0), s)))
         return st;
       continue;
     }

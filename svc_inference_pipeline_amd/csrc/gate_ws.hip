@@ -54,7 +54,9 @@ constexpr int GW_PART = GW_NG * GW_GBYTES;    // partial accumulators: [2 buffer
 constexpr int GW_ZERO = GW_PART + 2 * 4 * 2048;  // 768 B of zeros
 constexpr int GW_TVT = GW_ZERO + 768;  // ragged batches: valid input rows per utterance
 constexpr int GW_MAXB = 1024;
-constexpr int GW_LDS = GW_TVT + GW_MAXB * 4;  // 149,248 B
+constexpr int GW_STL = GW_TVT + GW_MAXB * 4;   // diagnostics: in-LDS step stamps [3 kinds][GW_NSTAMP] u64
+constexpr int GW_NSTAMP = 128;
+constexpr int GW_LDS = GW_STL + 3 * GW_NSTAMP * 8;  // 152,320 B
 constexpr int GW_PARTS = 42;          // row parts (x 6 column groups)
 constexpr int GW_GRID = 256;
 constexpr int GW_NT = 512;
@@ -78,7 +80,6 @@ struct GateWsArgs {
   int dbg;            // diagnostics (SVC_GWS_DBG, timing only): 2 no MFMAs, 4 no gate arithmetic
   unsigned long long* stamps;  // diagnostics (SVC_GWS_STAMPS, svc_gemm_bench only): s_memtime per workgroup and step
 };
-constexpr int GW_NSTAMP = 128;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ u32x4 gw_desc(const void* base, int64_t bytes) {
@@ -108,10 +109,23 @@ __device__ __forceinline__ void gw_barrier() {
 
 union GwH4 { uint2 u; f16 h[4]; };
 
-// diagnostics: the first second wave's lane 0 records s_memtime at step boundaries into a buffer nothing else reads
-// (a second wave: its vector-memory operations are the compiler's to count; the first waves' waits are hand-counted)
+// diagnostics: s_memtime at step boundaries, [workgroup][kind][GW_NSTAMP] in a buffer nothing else reads. Kind 0: the
+// first second wave after each barrier (stored directly: its vector-memory operations are the compiler's to count);
+// kinds 1 / 2: the first first wave before / after its ring wait, kind 3: the first second wave before its barrier,
+// kept in LDS and copied out after the loop (a first wave's vmcnt waits are hand-counted, so it stores nothing inside)
 __device__ __forceinline__ void gw_stamp(const GateWsArgs& a, int i) {
-  if (a.stamps && threadIdx.x == 256 && i < GW_NSTAMP) a.stamps[blockIdx.x * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
+  if (a.stamps && threadIdx.x == 256 && i < GW_NSTAMP)
+    a.stamps[(size_t)blockIdx.x * 4 * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ void gw_stamp_lds(const GateWsArgs& a, unsigned char* smw, int kind, int i, int thread) {
+  if (a.stamps && threadIdx.x == thread && i < GW_NSTAMP)
+    reinterpret_cast<unsigned long long*>(smw + GW_STL)[(kind - 1) * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ void gw_stamp_flush(const GateWsArgs& a, const unsigned char* smw, int kind, int n) {
+  if (!a.stamps) return;
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(smw + GW_STL) + (kind - 1) * GW_NSTAMP;
+  for (int i = threadIdx.x & 63; i < n && i < GW_NSTAMP; i += 64)
+    a.stamps[((size_t)blockIdx.x * 4 + kind) * GW_NSTAMP + i] = src[i];
 }
 
 // LDS byte offsets of a lane's three tap rows for row block j of the part (output row m = r_begin + 16 j + fr): ring
@@ -299,15 +313,21 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
         *reinterpret_cast<floatx4*>(pb) = ag;
         *reinterpret_cast<floatx4*>(pb + 1024) = af;
         row.next(a, tvt);
+        gw_stamp_lds(a, smw, 1, k, 0);
         if (k & 1) {
           if (seven) gw_vmwait<3 * PV>(); else gw_vmwait<3 * (PV - 1)>();
         } else {
           if (seven) gw_vmwait<2 * PV>(); else gw_vmwait<2 * (PV - 1)>();
         }
+        gw_stamp_lds(a, smw, 2, k, 0);
       }
       gw_barrier();  // the partial sums of block k; every first wave's pieces of block k + 1's groups
     }
     gw_vmwait<0>();  // (the groups issued past the part land before the workgroup's LDS is released)
+    if (wave == 0) {
+      gw_stamp_flush(a, smw, 1, nsub);
+      gw_stamp_flush(a, smw, 2, nsub);
+    }
   } else {
     // ------------------------------------------------------------------ second waves: K-steps 18..35 + gate epilogue
     // Step k: the MFMAs of block k - 1 (its partial sums come from step k - 1), interleaved with the gate epilogue of
@@ -382,6 +402,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       if (k >= 2) epilogue(k - 2, ep, pg, pf);
       pg = ag;
       pf = af;
+      gw_stamp_lds(a, smw, 3, k, 256);
       gw_barrier();
       gw_stamp(a, 3 + k);
     };
@@ -397,6 +418,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       case 1: epilogue(last, c1, pg, pf); break;
       default: epilogue(last, c2, pg, pf); break;
     }
+    if (wave == 4) gw_stamp_flush(a, smw, 3, nsub + 1);
   }
 }
 
@@ -428,7 +450,7 @@ size_t gate_ws_pack_elems() { return (size_t)GW_N * GW_K; }
 
 // diagnostics (svc_gemm_bench with SVC_GWS_STAMPS): a [256][GW_NSTAMP] s_memtime buffer, else NULL
 unsigned long long* gate_ws_stamps = nullptr;
-int gate_ws_nstamp() { return GW_NSTAMP; }
+int gate_ws_nstamp() { return 4 * GW_NSTAMP; }  // per workgroup
 
 bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e) {
   const int d = a.tap_mul;

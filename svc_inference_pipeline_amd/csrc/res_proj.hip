@@ -248,7 +248,8 @@ int res_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s) {
 size_t res_proj_pack_elems() { return (size_t)RP_C * RP_C; }
 
 // M rows of the split residual update for one layer; Wf: W_res in fragment order (res_proj_pack).
-// lanes_cap > 0: that many row lanes (2 workgroups each) instead of one workgroup per CU
+// lanes_cap > 0: that many row lanes (2 workgroups each); 0: 3/8 of the CU count (beside another sampler stream);
+// -2: half the CU count (the projection alone on the chip: one workgroup per CU)
 int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, const float* add, float div, f16* hi,
              f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s) {
   SVC_REQUIRE(M >= 0 && Wf, "res_proj: M %d, packed weights %p", M, (const void*)Wf);
@@ -270,7 +271,10 @@ int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, c
   // on 256 CUs): end to end 810.4-810.8 audio-s/s against 800.6-806.1 with one workgroup per CU, 804-805 with 80 lanes
   // and 807-808 with 112 (r03p, three alternating rounds): the CUs it leaves free run the other sampler stream's gate
   // GEMM, and fewer workgroups load W fewer times
-  int lanes = lanes_cap > 0 ? lanes_cap : ncu * 3 / 8;
+  // One sampler stream (the round-4 default): half the CU count, 128 lanes = 256 workgroups, one per CU. Alone on the
+  // chip 850.7 / 850.0 / 849.9 audio-s/s against 843.3 / 843.5 / 841.0 with 112 lanes (r04j, alternating); 160 lanes
+  // (320 workgroups: a second round) 816 (r04i)
+  int lanes = lanes_cap > 0 ? lanes_cap : (lanes_cap == -2 ? ncu / 2 : ncu * 3 / 8);
   lanes = std::max(8, std::min(lanes, (int)round_up(tiles, 8)));
   lanes = (int)round_up(lanes, 8);
   ResProjArgs a{g, Wf, bias, sub, add, div, hi, lo, M, lanes, cdiv(tiles, lanes)};

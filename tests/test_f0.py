@@ -125,7 +125,10 @@ def _pyin_clips():
 def test_gpu_pyin_matches_oracle():
     """HIP pYIN vs the oracle: the decoded path agrees on >= 99 % of frames (voicing and bin) per clip. The kernels sum
     the lag products directly in f64 where librosa (and the oracle) use an FFT, so a CMND value that sits on a trough /
-    threshold decision boundary may flip; everything downstream is the same f64 arithmetic."""
+    threshold decision boundary may flip; everything downstream is the same f64 arithmetic. A bin's frequency
+    fmin * 2^(k / 120) is compared to 1e-14 relative, not bit for bit: the library's table comes from C pow, numpy's
+    from its own vectorised power, and the two differ by 1 ulp on 24 of the 435 bins (first GPU run, r04i: every
+    mismatching frame was such a bin; bins are 0.58 % apart, so the tolerance cannot confuse two)."""
     import torch
     from svc_inference_pipeline_amd import config as C
     from svc_inference_pipeline_amd.runtime import SVCEngine
@@ -136,7 +139,7 @@ def test_gpu_pyin_matches_oracle():
     assert f0.shape == (len(clips), 1 + wav.shape[1] // 256)
     for b, x in enumerate(clips):
         ref = PY.f0_pyin(x, **PY_ARGS)
-        same = (f0[b] == ref)
+        same = np.isclose(f0[b], ref, rtol=1e-14, atol=0)
         assert np.mean(same) >= 0.99, (b, np.mean(same), np.nonzero(~same)[0][:10])
         assert np.array_equal(f0[b] > 0, ref > 0) or np.mean((f0[b] > 0) != (ref > 0)) <= 0.01, b
     # ragged batch: each utterance as a clip of its own length, rows past its frames 0

@@ -7,7 +7,8 @@ Infinity-Cache hits are counted as fetches, so the figure is an upper bound on D
 One kernel can serve launches of different sizes (conv_gemm4<128,128,pair> runs both the sampler's sub-batch
 launches and the full-batch launches of bench.py's single-stream roofline pass), so traffic and the rocprof trace
 durations are also split by grid size; a kernel's headline `hbm_bytes_per_launch` is that of its LARGEST grid, which
-is the roofline pass's full-batch launch.
+is the roofline pass's full-batch launch. (gate_ws<16x128> runs a fixed 256-workgroup grid at every size: with one
+sampler stream every launch of it is a full batch.)
 Usage: python tools/pmc_summary.py gpurun_out/<tag> profiles/<round-prefix>
 """
 import csv
@@ -43,6 +44,8 @@ def short(name):
         return "activation1d"
     if "res_proj_kernel" in name:
         return "res_proj<16x192>"
+    if "gate_ws_kernel" in name:
+        return "gate_ws<16x128>"
     for k, v in NAME_MAP.items():
         if k in name:
             return v

@@ -1,6 +1,7 @@
 """(diagnostics) gate_ws step timeline: s_memtime stamps per workgroup (svc_gemm_bench variant 40, SVC_GWS_STAMPS).
-Stamp 0: kernel start (second wave), 1: after its W / cp prologue loads were issued, 2: prologue barrier, 3: end of
-step 0, 4 + j: end of the step that finished block j."""
+Kind 0 (second wave): 0 kernel start, 1 after its W / cp prologue loads were issued, 2 prologue barrier, 3 + k after the
+barrier of step k. Kind 1 / 2 (first wave): step k before / after its ring vmcnt wait; kind 3 (second wave): step k
+before its barrier."""
 import os, subprocess, sys
 import numpy as np
 R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -9,9 +10,10 @@ for M in [int(v) for v in (sys.argv[1:] or ["29984", "14992"])]:
     env = dict(os.environ, SVC_GWS_STAMPS=path, GEMM_BENCH_TORCH="0", GEMM_BENCH_CUSTOM=f"{M},768,384,3,1")
     subprocess.run([sys.executable, os.path.join(R, "tools", "gemm_bench.py"), "40"], env=env, check=True,
                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-    st = np.fromfile(path, dtype=np.uint64).reshape(256, 128).astype(np.int64)
-    live = st[:, 0] > 0
-    st = st[live]
+    full = np.fromfile(path, dtype=np.uint64).reshape(256, 4, 128).astype(np.int64)
+    live = full[:, 0, 0] > 0
+    full = full[live]
+    st = full[:, 0]
     t0 = st[:, 0].min()
     rel = np.where(st > 0, st - t0, -1)
     n = (rel >= 0).sum(1)
@@ -29,3 +31,16 @@ for M in [int(v) for v in (sys.argv[1:] or ["29984", "14992"])]:
     print("  per step (ticks) pctl 10/50/90/max:", np.percentile(alls, [10, 50, 90, 100]))
     print("  first 12 steps median:", [int(np.median([s[i] for s in steps if len(s) > i])) for i in range(12)])
     print("  end (last stamp) spread:", np.percentile([rel[w, n[w] - 1] for w in range(len(rel))], [0, 50, 100]))
+    # per step roles: D_{k-1} = end of the previous barrier (kind 0 index 2 + k)
+    fw, wt, sw, bw = [], [], [], []
+    for w in range(len(full)):
+        nsub = n[w] - 4  # stamps 3..3+nsub
+        for k in range(1, nsub):
+            d0 = full[w, 0, 2 + k]
+            a1, b2, c3, d1 = full[w, 1, k], full[w, 2, k], full[w, 3, k], full[w, 0, 3 + k]
+            if min(a1, b2, c3, d1, d0) <= 0:
+                continue
+            fw.append(a1 - d0); wt.append(b2 - a1); sw.append(c3 - d0); bw.append(d1 - max(b2, c3))
+    for name, v in (("first wave: MFMAs + partial write", fw), ("first wave: ring vmcnt wait", wt),
+                    ("second wave: cp load + MFMAs + epilogue", sw), ("barrier release after the later arrival", bw)):
+        print(f"  {name}: pctl 10/50/90", np.percentile(v, [10, 50, 90]).astype(int))
