@@ -77,7 +77,6 @@ struct GateWsArgs {
   const int* tv;      // ragged: utterance b has min(T, tv[b] * tv_mul) valid input rows (NULL = T)
   int tv_mul, B;
   float invT;
-  int dbg;            // diagnostics (SVC_GWS_DBG, timing only): 2 no MFMAs, 4 no gate arithmetic
   unsigned long long* stamps;  // diagnostics (SVC_GWS_STAMPS, svc_gemm_bench only): s_memtime per workgroup and step
 };
 
@@ -109,49 +108,30 @@ __device__ __forceinline__ void gw_barrier() {
 
 union GwH4 { uint2 u; f16 h[4]; };
 
-// diagnostics: s_memtime at step boundaries, [workgroup][kind][GW_NSTAMP] in a buffer nothing else reads. Kind 0: the
-// first second wave after each barrier (stored directly: its vector-memory operations are the compiler's to count);
-// kinds 1 / 2: the first first wave before / after its ring wait, kind 3: the first second wave before its barrier,
-// kept in LDS and copied out after the loop (a first wave's vmcnt waits are hand-counted, so it stores nothing inside)
+// Diagnostics (compile-time DBG, svc_gemm_bench / SVC_GWS_DBG / SVC_GWS_STAMPS only): 2 no MFMAs, 4 no gate arithmetic,
+// 8 step stamps. Stamps: s_memtime at step boundaries, [workgroup][kind][GW_NSTAMP] in a buffer nothing else reads.
+// Kind 0: the first second wave after each barrier (stored directly: its vector-memory operations are the compiler's
+// to count); kinds 1 / 2: the first first wave before / after its ring wait, kind 3: the first second wave before its
+// barrier, kept in LDS and copied out after the loop (a first wave's vmcnt waits are hand-counted, so it stores
+// nothing inside)
+template <int DBG>
 __device__ __forceinline__ void gw_stamp(const GateWsArgs& a, int i) {
-  if (a.stamps && threadIdx.x == 256 && i < GW_NSTAMP)
-    a.stamps[(size_t)blockIdx.x * 4 * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
+  if constexpr ((DBG & 8) != 0)
+    if (threadIdx.x == 256 && i < GW_NSTAMP)
+      a.stamps[(size_t)blockIdx.x * 4 * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
 }
-__device__ __forceinline__ void gw_stamp_lds(const GateWsArgs& a, unsigned char* smw, int kind, int i, int thread) {
-  if (a.stamps && threadIdx.x == thread && i < GW_NSTAMP)
-    reinterpret_cast<unsigned long long*>(smw + GW_STL)[(kind - 1) * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
+template <int DBG>
+__device__ __forceinline__ void gw_stamp_lds(unsigned char* smw, int kind, int i, int thread) {
+  if constexpr ((DBG & 8) != 0)
+    if (threadIdx.x == thread && i < GW_NSTAMP)
+      reinterpret_cast<unsigned long long*>(smw + GW_STL)[(kind - 1) * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
 }
+template <int DBG>
 __device__ __forceinline__ void gw_stamp_flush(const GateWsArgs& a, const unsigned char* smw, int kind, int n) {
-  if (!a.stamps) return;
-  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(smw + GW_STL) + (kind - 1) * GW_NSTAMP;
-  for (int i = threadIdx.x & 63; i < n && i < GW_NSTAMP; i += 64)
-    a.stamps[((size_t)blockIdx.x * 4 + kind) * GW_NSTAMP + i] = src[i];
-}
-
-// LDS byte offsets of a lane's three tap rows for row block j of the part (output row m = r_begin + 16 j + fr): ring
-// row (8 + 16 j + fr + (tap - 1) dil) mod 160, or the zero row when the tap's input frame lies outside the utterance's
-// valid rows
-__device__ __forceinline__ void gw_tap_bases(const GateWsArgs& a, const int* tvt, int m, int j, int fr, int fk,
-                                             int base[3]) {
-  int bb = (int)((float)m * a.invT);
-  int t = m - bb * a.T;
-  if (t < 0) {
-    --bb;
-    t += a.T;
-  } else if (t >= a.T) {
-    ++bb;
-    t -= a.T;
-  }
-  const bool row_ok = m < a.M;
-  const int tvb = a.tv ? (row_ok ? tvt[bb] : 0) : a.T;
-  const int r0 = (16 * j) % GW_RROWS + GW_HALO + fr;  // < 160 + 23
-#pragma unroll
-  for (int tap = 0; tap < 3; ++tap) {
-    const int tp = t + (tap - 1) * a.dil;
-    const bool ok = row_ok && tp >= 0 && tp < tvb;
-    int rr = r0 + (tap - 1) * a.dil;  // in [0, 160 + 31)
-    rr = rr >= GW_RROWS ? rr - GW_RROWS : rr;
-    base[tap] = (ok ? rr * GW_STRIDE : GW_ZERO) + fk * 16;
+  if constexpr ((DBG & 8) != 0) {
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(smw + GW_STL) + (kind - 1) * GW_NSTAMP;
+    for (int i = threadIdx.x & 63; i < n && i < GW_NSTAMP; i += 64)
+      a.stamps[((size_t)blockIdx.x * 4 + kind) * GW_NSTAMP + i] = src[i];
   }
 }
 
@@ -161,7 +141,8 @@ __device__ __forceinline__ size_t gw_frag_index(int c, int p, int kh, int s, int
   return (size_t)((((c * 4 + p) * 2 + kh) * GW_KH + s) * 2 + g) * 512;
 }
 
-// The lane's row of block j of the part: utterance bb and frame t, advanced block by block (no division per block)
+// The lane's row of block j of the part: utterance bb and frame t, advanced block by block without a branch (T >= 16,
+// gate_ws_fits: at most one utterance boundary per block); tvt holds every utterance's valid rows (T without a table)
 struct GwRow {
   int m, bb, t, tvb;
   __device__ __forceinline__ void init(const GateWsArgs& a, const int* tvt, int m0) {
@@ -175,21 +156,18 @@ struct GwRow {
       ++bb;
       t -= a.T;
     }
-    tvb = a.tv ? (m < a.M ? tvt[bb] : 0) : a.T;
+    tvb = tvt[min(bb, a.B - 1)];
   }
   __device__ __forceinline__ void next(const GateWsArgs& a, const int* tvt) {
     m += 16;
     t += 16;
-    bool moved = false;
-    while (t >= a.T) {
-      t -= a.T;
-      ++bb;
-      moved = true;
-    }
-    if (moved && a.tv) tvb = m < a.M ? tvt[bb] : 0;
+    const bool wrap = t >= a.T;
+    t = wrap ? t - a.T : t;
+    bb += wrap ? 1 : 0;
+    tvb = tvt[min(bb, a.B - 1)];
   }
   // LDS byte offsets of the three tap rows for row block j: ring row (8 + 16 j + fr + (tap - 1) dil) mod 160, or the
-  // zero row when the tap's input frame lies outside the utterance's valid rows
+  // zero row when the tap's input frame lies outside the utterance's valid rows (or the row is past M)
   __device__ __forceinline__ void bases(const GateWsArgs& a, int j, int fr, int fk, int base[3]) const {
     const bool row_ok = m < a.M;
     const int r0 = (16 * j) % GW_RROWS + GW_HALO + fr;  // < 160 + 23
@@ -204,7 +182,10 @@ struct GwRow {
   }
 };
 
-template <bool BF>
+// sched_group_barrier masks (LLVM AMDGPU): VALU, MFMA, DS read
+constexpr int GW_SG_VALU = 0x002, GW_SG_MFMA = 0x008, GW_SG_DSR = 0x100;
+
+template <bool BF, int DBG>
 __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
   using O = Op16<BF>;
   extern __shared__ __align__(16) unsigned char smw[];
@@ -237,9 +218,9 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
   const int ng = 64 * q + 16 * h, nf = ng + 32;
   const int ch = 32 * q + 16 * h + 4 * fk;  // the lane's 4 output channels (second waves)
 
-  if (a.tv) {
+  {
     int* tvt = reinterpret_cast<int*>(smw + GW_TVT);
-    for (int i = tid; i < a.B; i += GW_NT) tvt[i] = min(a.T, a.tv[i] * a.tv_mul);
+    for (int i = tid; i < a.B; i += GW_NT) tvt[i] = a.tv ? min(a.T, a.tv[i] * a.tv_mul) : a.T;
   }
   for (int i = tid; i < 768 / 16; i += GW_NT) *reinterpret_cast<uint4*>(smw + GW_ZERO + i * 16) = make_uint4(0, 0, 0, 0);
   const int* tvt = reinterpret_cast<const int*>(smw + GW_TVT);
@@ -247,12 +228,32 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
 
   // W fragments of the swapped MFMA (its first operand), this wave's K half: wg[s] / wf[s] = K-step 18 kh + s
   half8 wg[GW_KH], wf[GW_KH];
-  auto load_w = [&]() {
+  auto load_w = [&]() __attribute__((always_inline)) {
     const f16* wb = a.W + gw_frag_index(type, pair, kh, 0, 0) + lane * 8;
 #pragma unroll
     for (int s = 0; s < GW_KH; ++s) {
       wg[s] = *reinterpret_cast<const half8*>(wb + (size_t)(2 * s) * 512);
       wf[s] = *reinterpret_cast<const half8*>(wb + (size_t)(2 * s + 1) * 512);
+    }
+  };
+  // this wave's 18 K-steps of one block onto (ag, af): A fragments read three K-steps ahead of their MFMAs (one
+  // ds_read_b128 in flight per MFMA pair would leave each pair waiting on LDS latency), pinned to that order
+  auto kloop = [&](const int base[3], int s_off, floatx4& ag, floatx4& af) __attribute__((always_inline)) {
+    half8 av[4];
+    auto rd = [&](int s) __attribute__((always_inline)) {
+      const int ks = s_off + s;
+      return *reinterpret_cast<const half8*>(smw + base[ks / 12] + (ks % 12) * 64);
+    };
+    av[0] = rd(0);
+    av[1] = rd(1);
+    av[2] = rd(2);
+#pragma unroll
+    for (int s = 0; s < GW_KH; ++s) {
+      if (s + 3 < GW_KH) av[(s + 3) & 3] = rd(s + 3);
+      if constexpr (!(DBG & 2)) {
+        ag = O::mfma(wg[s], av[s & 3], ag);
+        af = O::mfma(wf[s], av[s & 3], af);
+      }
     }
   };
 
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     const bool seven = pair + 4 * (PV - 1) < GW_GPIECES;  // this wave issues PV pieces per group (else PV - 1)
     // every group index is issued, past the part's rows too (harmless rows or zeros), so each wave's count of DMAs
     // younger than a given group is the same at every step: the waits below are compile-time vmcnt values
-    auto issue = [&](int g) {
+    auto issue = [&](int g) __attribute__((always_inline)) {
       const uint32_t base = (uint32_t)((r_begin - GW_HALO + g * GW_GR) * (GW_C * 2));  // (negative: wraps, out of range)
       unsigned char* dst = smw + (g % GW_NG) * GW_GBYTES + pair * 1024;
 #pragma unroll
@@ -295,54 +296,54 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     // whose last reader finished in step k - 1; its first reader is block 2 g - 1, 5 steps later. At the end of step k,
     // block k + 1's groups (up to (k + 2) / 2) must have landed: the groups issued after them are the 3 newest on odd
     // steps and the 2 newest on even ones (3 on step 0: waiting for 2 there is merely early)
-    for (int k = 0; k <= nsub; ++k) {
-      if (k < nsub) {
-        if ((k & 1) && k >= 3) issue((k + 7) / 2);
-        int base[3];
-        row.bases(a, k, fr, fk, base);
-        floatx4 ag = {0.f, 0.f, 0.f, 0.f}, af = {0.f, 0.f, 0.f, 0.f};
-        if (!(a.dbg & 2)) {
+    auto step = [&](int k) __attribute__((always_inline)) {  // k < nsub; ends with the step's barrier
+      if ((k & 1) && k >= 3) issue((k + 7) / 2);
+      int base[3];
+      row.bases(a, k, fr, fk, base);
+      floatx4 ag = {0.f, 0.f, 0.f, 0.f}, af = {0.f, 0.f, 0.f, 0.f};
+      kloop(base, 0, ag, af);
+      unsigned char* pb = part_buf + (k & 1) * 8192 + lane * 16;
+      *reinterpret_cast<floatx4*>(pb) = ag;
+      *reinterpret_cast<floatx4*>(pb + 1024) = af;
+      row.next(a, tvt);
 #pragma unroll
-          for (int s = 0; s < GW_KH; ++s) {  // K-steps 0..11: tap 0; 12..17: tap 1 channels 0..191
-            const half8 av = *reinterpret_cast<const half8*>(smw + base[s / 12] + (s % 12) * 64);
-            ag = O::mfma(wg[s], av, ag);
-            af = O::mfma(wf[s], av, af);
-          }
-        }
-        unsigned char* pb = part_buf + (k & 1) * 8192 + lane * 16;
-        *reinterpret_cast<floatx4*>(pb) = ag;
-        *reinterpret_cast<floatx4*>(pb + 1024) = af;
-        row.next(a, tvt);
-        gw_stamp_lds(a, smw, 1, k, 0);
-        if (k & 1) {
-          if (seven) gw_vmwait<3 * PV>(); else gw_vmwait<3 * (PV - 1)>();
-        } else {
-          if (seven) gw_vmwait<2 * PV>(); else gw_vmwait<2 * (PV - 1)>();
-        }
-        gw_stamp_lds(a, smw, 2, k, 0);
+      for (int s = 0; s < GW_KH; ++s) {  // one A-fragment read per MFMA pair, three K-steps ahead
+        __builtin_amdgcn_sched_group_barrier(GW_SG_DSR, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(GW_SG_MFMA, 2, 0);
       }
+      gw_stamp_lds<DBG>(smw, 1, k, 0);
+      if (k & 1) {
+        if (seven) gw_vmwait<3 * PV>(); else gw_vmwait<3 * (PV - 1)>();
+      } else {
+        if (seven) gw_vmwait<2 * PV>(); else gw_vmwait<2 * (PV - 1)>();
+      }
+      gw_stamp_lds<DBG>(smw, 2, k, 0);
       gw_barrier();  // the partial sums of block k; every first wave's pieces of block k + 1's groups
-    }
+    };
+    for (int k = 0; k < nsub; ++k) step(k);
+    gw_barrier();  // step nsub: the second waves finish block nsub - 1
     gw_vmwait<0>();  // (the groups issued past the part land before the workgroup's LDS is released)
     if (wave == 0) {
-      gw_stamp_flush(a, smw, 1, nsub);
-      gw_stamp_flush(a, smw, 2, nsub);
+      gw_stamp_flush<DBG>(a, smw, 1, nsub);
+      gw_stamp_flush<DBG>(a, smw, 2, nsub);
     }
   } else {
     // ------------------------------------------------------------------ second waves: K-steps 18..35 + gate epilogue
     // Step k: the MFMAs of block k - 1 (its partial sums come from step k - 1), interleaved with the gate epilogue of
-    // block k - 2, whose accumulators this wave kept from step k - 1: the epilogue's VALU work runs in the MFMAs'
-    // issue shadow instead of after them. The last block's epilogue follows the loop.
+    // block k - 2, whose accumulators this wave kept from step k - 1. In the steady state (2 <= k < nsub) a step is one
+    // basic block, so the scheduler can (and the group barriers below make it) spread the epilogue's VALU work and the
+    // A-fragment reads among the MFMAs. These waves are the second-dispatched half: static priority 1 for the whole
+    // loop (MI355X_MICROARCH.md, two waves per SIMD, item 4).
     const __amdgpu_buffer_rsrc_t rcp =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.cp), (short)0, a.M * a.ld_cp * 2, GW_CFG);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y, (short)0, a.M * a.ldy * 2, GW_CFG);
-    gw_stamp(a, 0);
+    gw_stamp<DBG>(a, 0);
     load_w();
     const float4 bg = *reinterpret_cast<const float4*>(a.bias + ng + 4 * fk);
     const float4 bfv = *reinterpret_cast<const float4*>(a.bias + nf + 4 * fk);
     // conditioner projection of block j, loaded in step j (two steps before its epilogue) into register set j % 3:
-    // fixed roles per set (the step loop is unrolled by 3), so no register move waits on a load
-    auto load_cp = [&](int blk, GwH4* dst) {
+    // fixed roles per set (the steady loop is unrolled by 3), so no register move waits on a load
+    auto load_cp = [&](int blk, GwH4* dst) __attribute__((always_inline)) {
       const uint32_t vo = (uint32_t)(r_begin + blk * 16 + fr) * (uint32_t)(a.ld_cp * 2);  // rows past M read 0
       dst[0].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (ng + 4 * fk) * 2, 0, 0));
       dst[1].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (nf + 4 * fk) * 2, 0, 0));
@@ -351,14 +352,15 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     floatx4 pg = {0.f, 0.f, 0.f, 0.f}, pf = {0.f, 0.f, 0.f, 0.f};  // accumulators of the block awaiting its epilogue
     GwRow row;
     row.init(a, tvt, r_begin + fr);
-    gw_stamp(a, 1);
+    gw_stamp<DBG>(a, 1);
     gw_barrier();  // (pairs with the first waves' prologue barrier)
-    gw_stamp(a, 2);
+    __builtin_amdgcn_s_setprio(1);
+    gw_stamp<DBG>(a, 2);
     // gate in registers (conv_gemm4's DIRECT epilogue arithmetic, same order); rows past the part are dropped
-    auto epilogue = [&](int blk, const GwH4* cp, floatx4 ag, floatx4 af) {
+    auto epilogue = [&](int blk, const GwH4* cp, floatx4 ag, floatx4 af) __attribute__((always_inline)) {
       const GwH4 cg = cp[0], cf = cp[1];
       GwH4 pk;
-      if (a.dbg & 4) {
+      if constexpr ((DBG & 4) != 0) {
         pk.h[0] = (f16)(ag[0] + af[1]);
         pk.h[1] = (f16)(ag[1] + af[2]);
         pk.h[2] = (f16)(ag[2] + af[3]);
@@ -374,51 +376,70 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, pk.u), ry,
                                             vo, 0, 0);
     };
-    // step k: load cp(k) into `ld`, MFMAs of block k - 1, epilogue of block k - 2 from `ep`
-    auto step = [&](int k, GwH4* ld, const GwH4* ep) {
-      if (k < nsub) load_cp(k, ld);
-      floatx4 ag = {0.f, 0.f, 0.f, 0.f}, af = {0.f, 0.f, 0.f, 0.f};
-      if (k >= 1) {
-        const int blk = k - 1;
-        int base[3];
-        row.bases(a, blk, fr, fk, base);
-        const unsigned char* pb = part_buf + (blk & 1) * 8192 + lane * 16;
-        ag = *reinterpret_cast<const floatx4*>(pb);
-        af = *reinterpret_cast<const floatx4*>(pb + 1024);
-        // the second wave's MFMAs go first on the SIMD (priority 1), so the first wave's run beside this wave's VALU
-        __builtin_amdgcn_s_setprio(1);
-        if (!(a.dbg & 2)) {
-#pragma unroll
-          for (int s = 0; s < GW_KH; ++s) {  // K-steps 18..23: tap 1 channels 192..383; 24..35: tap 2
-            const int ks = GW_KH + s;
-            const half8 av = *reinterpret_cast<const half8*>(smw + base[ks / 12] + (ks % 12) * 64);
-            ag = O::mfma(wg[s], av, ag);
-            af = O::mfma(wf[s], av, af);
-          }
-        }
-        __builtin_amdgcn_s_setprio(0);
-        row.next(a, tvt);
-      }
-      if (k >= 2) epilogue(k - 2, ep, pg, pf);
+    // the MFMAs of block blk on its partial sums (K-steps 18..23: tap 1 channels 192..383; 24..35: tap 2)
+    auto mfma_blk = [&](int blk, floatx4& ag, floatx4& af) __attribute__((always_inline)) {
+      int base[3];
+      row.bases(a, blk, fr, fk, base);
+      const unsigned char* pb = part_buf + (blk & 1) * 8192 + lane * 16;
+      ag = *reinterpret_cast<const floatx4*>(pb);
+      af = *reinterpret_cast<const floatx4*>(pb + 1024);
+      kloop(base, GW_KH, ag, af);
+      row.next(a, tvt);
+    };
+    auto end_step = [&](int k) __attribute__((always_inline)) {
+      gw_stamp_lds<DBG>(smw, 3, k, 256);
+      gw_barrier();
+      gw_stamp<DBG>(a, 3 + k);
+    };
+    // steady step k (2 <= k < nsub): cp(k) into LS, MFMAs of block k - 1, epilogue of block k - 2 from ES
+    auto steady = [&](int k, GwH4* ls, const GwH4* es) __attribute__((always_inline)) {
+      load_cp(k, ls);
+      floatx4 ag, af;
+      mfma_blk(k - 1, ag, af);
+      epilogue(k - 2, es, pg, pf);
       pg = ag;
       pf = af;
-      gw_stamp_lds(a, smw, 3, k, 256);
-      gw_barrier();
-      gw_stamp(a, 3 + k);
+      // one A-fragment read, two MFMAs and 8 of the epilogue's ~150 VALU instructions per K-step
+#pragma unroll
+      for (int s = 0; s < GW_KH; ++s) {
+        __builtin_amdgcn_sched_group_barrier(GW_SG_DSR, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(GW_SG_MFMA, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(GW_SG_VALU, 8, 0);
+      }
+      end_step(k);
     };
-    for (int k = 0; k <= nsub; k += 3) {
-      step(k, c0, c1);
-      if (k + 1 <= nsub) step(k + 1, c1, c2);
-      if (k + 2 <= nsub) step(k + 2, c2, c0);
+    // step 0: cp(0); step 1: cp(1), MFMAs of block 0
+    load_cp(0, c0);
+    end_step(0);
+    if (nsub >= 2) load_cp(1, c1);
+    mfma_blk(0, pg, pf);
+    end_step(1);
+    int k = 2;
+    for (; k + 3 <= nsub; k += 3) {  // k = 2 mod 3: loads into c2, c0, c1; epilogues from c0, c1, c2
+      steady(k, c2, c0);
+      steady(k + 1, c0, c1);
+      steady(k + 2, c1, c2);
     }
-    // the last block's epilogue (its cp went into set (nsub - 1) % 3)
-    const int last = nsub - 1;
-    switch (last % 3) {
-      case 0: epilogue(last, c0, pg, pf); break;
-      case 1: epilogue(last, c1, pg, pf); break;
-      default: epilogue(last, c2, pg, pf); break;
+    if (k < nsub) steady(k++, c2, c0);
+    if (k < nsub) steady(k++, c0, c1);
+    // step nsub (>= 2): MFMAs of block nsub - 1, epilogue of block nsub - 2 (cp set (nsub - 2) % 3)
+    auto epi_set = [&](int blk) __attribute__((always_inline)) {  // epilogue of blk from its set blk % 3
+      switch (blk % 3) {
+        case 0: epilogue(blk, c0, pg, pf); break;
+        case 1: epilogue(blk, c1, pg, pf); break;
+        default: epilogue(blk, c2, pg, pf); break;
+      }
+    };
+    if (nsub >= 2) {
+      floatx4 ag, af;
+      mfma_blk(nsub - 1, ag, af);
+      epi_set(nsub - 2);
+      pg = ag;
+      pf = af;
+      end_step(nsub);
     }
-    if (wave == 4) gw_stamp_flush(a, smw, 3, nsub + 1);
+    epi_set(nsub - 1);  // the last block's epilogue
+    if (wave == 4) gw_stamp_flush<DBG>(a, smw, 3, nsub + 1);
   }
 }
 
@@ -456,7 +477,7 @@ bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e) {
   const int d = a.tap_mul;
   return e.kind == EPI_GATE && e.cp && e.y16 && e.bias && a.Wfrag && a.Cp == GW_C && a.Cvalid == GW_C && a.ldx == GW_C &&
          a.K == GW_K && a.Kpad == GW_K && a.N == GW_N && (d == 1 || d == 2 || d == 4 || d == 8) && a.tap_add == -d &&
-         a.istride == 1 && a.T_in == a.T_out && (!a.tv || a.B <= GW_MAXB) && e.ld_cp % 4 == 0 && e.ldy16 % 4 == 0 &&
+         a.istride == 1 && a.T_in == a.T_out && a.T_out >= 16 && a.B <= GW_MAXB && e.ld_cp % 4 == 0 && e.ldy16 % 4 == 0 &&
          (int64_t)a.B * a.T_out * std::max(e.ld_cp, std::max(e.ldy16, GW_C)) * 2 < (1ll << 30);
 }
 
@@ -469,9 +490,12 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   if (M == 0) return SVC_OK;
   static const int dbg = getenv("SVC_GWS_DBG") ? atoi(getenv("SVC_GWS_DBG")) : 0;  // (diagnostics, read once)
   GateWsArgs g{a.X, a.Wfrag, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
-               1.0f / (float)a.T_out, dbg, gate_ws_stamps};
-  const int bf = a.bf16 ? 1 : 0;
-  const void* fn = bf ? (const void*)gate_ws_kernel<true> : (const void*)gate_ws_kernel<false>;
+               1.0f / (float)a.T_out, gate_ws_stamps};
+  // diagnostics instances (fp16 only): 2 no MFMAs, 4 no gate arithmetic, 8 step stamps (SVC_GWS_STAMPS)
+  const void* fn = a.bf16 ? (const void*)gate_ws_kernel<true, 0> : (const void*)gate_ws_kernel<false, 0>;
+  if (!a.bf16 && gate_ws_stamps) fn = (const void*)gate_ws_kernel<false, 8>;
+  else if (!a.bf16 && dbg == 2) fn = (const void*)gate_ws_kernel<false, 2>;
+  else if (!a.bf16 && dbg == 4) fn = (const void*)gate_ws_kernel<false, 4>;
   if (int st = ensure_dyn_lds(fn, GW_LDS)) return st;
   const int tok = prof_begin("gate_ws<16x128>", 2.0 * M * (double)GW_N * GW_K, 0.0, s);
   void* args[] = {&g};
