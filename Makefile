@@ -24,7 +24,7 @@ build/attention.o: CXXFLAGS += -fno-honor-nans
 build/res_proj.o build/gate_ws.o: build/%.o: $(SRC_DIR)/%.hip $(wildcard $(SRC_DIR)/*.h) include/svc_hip.h
 	@mkdir -p build
 	$(HIPCC) $(CXXFLAGS) -c $< -o $@ -Rpass-analysis=kernel-resource-usage 2> build/$*.res || { cat build/$*.res; rm -f $@; exit 1; }
-	@python3 tools/check_kernel_resources.py build/$*.res $(if $(filter res_proj,$*),res_proj_kernel 104,gate_ws_kernel 256) || { rm -f $@; exit 1; }
+	@python3 tools/check_kernel_resources.py build/$*.res $(if $(filter res_proj,$*),res_proj_kernel 104,gate_ws 256) || { rm -f $@; exit 1; }
 
 $(LIB): $(OBJS)
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $(OBJS) -o $@

@@ -13,6 +13,7 @@
 typedef _Float16 f16;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 #define SVC_OK 0
 #define SVC_ERR_INVALID 1
@@ -114,6 +115,9 @@ struct Op16<false> {
   static __device__ __forceinline__ floatx4 mfma(half8 a, half8 b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
+  static __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  }
 };
 template <>
 struct Op16<true> {
@@ -124,6 +128,10 @@ struct Op16<true> {
   static __device__ __forceinline__ f16 enc_lo(float v) { return __builtin_bit_cast(f16, (__bf16)v); }
   static __device__ __forceinline__ floatx4 mfma(half8 a, half8 b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
+                                                   0, 0, 0);
+  }
+  static __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
   }
 };
@@ -156,7 +164,8 @@ struct ConvGemmArgs {
   const int* tv;
   int tv_mul;
   int bf16;      // operands (X, W) are bfloat16 (Op16<true>); the epilogue's 16-bit inputs / outputs too
-  const f16* Wfrag;  // W once more in a kernel's own fragment order (gate_ws; NULL: none)
+  const f16* Wfrag;    // W once more in a kernel's own fragment order (gate_ws; NULL: none)
+  const f16* Wfrag32;  // and in gate_ws32's (NULL: none)
 };
 
 __device__ __forceinline__ int valid_in_rows(const ConvGemmArgs& a, int b) {

@@ -8,7 +8,7 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for M in [int(v) for v in (sys.argv[1:] or ["29984", "14992"])]:
     path = "/tmp/gws_stamps.bin"
     env = dict(os.environ, SVC_GWS_STAMPS=path, GEMM_BENCH_TORCH="0", GEMM_BENCH_CUSTOM=f"{M},768,384,3,1")
-    subprocess.run([sys.executable, os.path.join(R, "tools", "gemm_bench.py"), "40"], env=env, check=True,
+    subprocess.run([sys.executable, os.path.join(R, "tools", "gemm_bench.py"), os.environ.get("GWS_V", "40")], env=env, check=True,
                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     full = np.fromfile(path, dtype=np.uint64).reshape(256, 4, 128).astype(np.int64)
     live = full[:, 0, 0] > 0
