@@ -8,12 +8,12 @@
 // whole L2 -> LDS bandwidth of a CU (64 B per clock), so its K-loop runs at ~0.4 of the MFMA peak.
 // Here the weights stay put instead:
 //   * a workgroup owns 128 packed columns = 64 output channels, as 4 column sets of 16 gate + 16 filter columns; each set
-//     belongs to a PAIR of waves on one SIMD (waves w and w + 4): wave w holds the set's weights for K-steps 0..17 (tap
-//     0 and the first half of tap 1), wave w + 4 for K-steps 18..35, as MFMA fragments in VGPRs (36 x half8 = 144
+//     belongs to a PAIR of waves on one SIMD (waves w and w + 4): wave w holds the set's weights for K-steps 0..19 (tap
+//     0 and the first 256 channels of tap 1), wave w + 4 for K-steps 20..35, as MFMA fragments in VGPRs (2 x 20 / 16 x half8 = 160 / 128
 //     registers each: two waves per SIMD), loaded once per launch;
-//   * the workgroup walks its share of the rows in 16-row blocks: in step k the first wave of a pair runs K-steps 0..17
+//   * the workgroup walks its share of the rows in 16-row blocks: in step k the first wave of a pair runs K-steps 0..19
 //     of block k and hands its two f32 accumulators to its partner through LDS, which continues them over K-steps
-//     18..35 for block k - 1 (the partial sums are the partner's MFMA C operand, so the K order is one sequential chain,
+//     20..35 for block k - 1 (the partial sums are the partner's MFMA C operand, so the K order is one sequential chain,
 //     exactly conv_gemm4's) and applies the gate in registers; one workgroup barrier per step;
 //   * the input rows come through a ring of 160 rows in LDS, DMA'd in 32-row groups (25 KiB) once each: the three taps
 //     of a block read its rows at offsets -dil, 0, +dil, so no row is fetched twice, and a group is issued 5 steps
@@ -31,6 +31,8 @@
 // ConvGemmArgs::tv) reads its A fragments from a 768-B zero row in LDS, so every ring row serves all three taps and no
 // fragment needs a select.
 // Bit-identical to conv_gemm4<128,128,gate> (tests/test_gpu_stages.py test_gate_ws_bit_identical).
+#include <type_traits>
+
 #include "common.h"
 
 // gw_dma clobbers m0 (reserved for the compiler's own LDS-DMA and indexing uses, which all set it right before use)
@@ -41,7 +43,10 @@ namespace svc {
 constexpr int GW_C = 384;             // channels per tap
 constexpr int GW_N = 768;             // packed output columns (gate | filter per 64-column block)
 constexpr int GW_K = 3 * GW_C;        // 1152 = 36 K-steps of 32
-constexpr int GW_KH = 18;             // K-steps per wave of a pair
+constexpr int GW_KS = 36;             // K-steps of 32
+constexpr int GW_KA_DEF = 20;         // K-steps of a pair's first wave (0..19); its partner takes 20..35. Unequal on
+                                      // purpose: the partner also runs the gate epilogue (18 / 18: partner 2248 vs
+                                      // 1672 cycles per step, r04m stamps). SVC_GWS_KA (18 / 20 / 22) for A/B runs
 constexpr int GW_HALO = 8;            // largest tap shift (dilation 8): ring row 0 = input row r_begin - 8
 constexpr int GW_GR = 32;             // rows per DMA group
 constexpr int GW_NG = 5;              // ring slots (groups): 160 rows
@@ -136,9 +141,9 @@ __device__ __forceinline__ void gw_stamp_flush(const GateWsArgs& a, const unsign
 }
 
 // W in fragment order (gate_ws_pack): for column group c, pair p, K half kh, K-step s, gate / filter g and lane l, the
-// 8 halves W[n][32 (18 kh + s) + 8 (l >> 4) ..], n = (g ? nf : ng) + (l & 15): each wave's 36 loads are contiguous KiB
-__device__ __forceinline__ size_t gw_frag_index(int c, int p, int kh, int s, int g) {
-  return (size_t)((((c * 4 + p) * 2 + kh) * GW_KH + s) * 2 + g) * 512;
+// 8 halves W[n][32 ks + 8 (l >> 4) ..], n = (g ? nf : ng) + (l & 15), K-step ks: each wave's loads are contiguous KiB
+__device__ __forceinline__ size_t gw_frag_index(int c, int p, int ks, int g) {
+  return (size_t)(((c * 4 + p) * GW_KS + ks) * 2 + g) * 512;
 }
 
 // The lane's row of block j of the part: utterance bb and frame t, advanced block by block without a branch (T >= 16,
@@ -185,9 +190,11 @@ struct GwRow {
 // sched_group_barrier masks (LLVM AMDGPU): VALU, MFMA, DS read
 constexpr int GW_SG_VALU = 0x002, GW_SG_MFMA = 0x008, GW_SG_DSR = 0x100;
 
-template <bool BF, int DBG>
+template <bool BF, int DBG, int GW_KA = GW_KA_DEF>
 __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
   using O = Op16<BF>;
+  constexpr int GW_KB = GW_KS - GW_KA;
+  static_assert(GW_KA >= GW_KB && GW_KB >= 4, "K split: the weight arrays are sized for the first wave");
   extern __shared__ __align__(16) unsigned char smw[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -226,39 +233,48 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
   const int* tvt = reinterpret_cast<const int*>(smw + GW_TVT);
   unsigned char* const part_buf = smw + GW_PART + pair * 2048;  // + (k & 1) * 8192
 
-  // W fragments of the swapped MFMA (its first operand), this wave's K half: wg[s] / wf[s] = K-step 18 kh + s
-  half8 wg[GW_KH], wf[GW_KH];
-  auto load_w = [&]() __attribute__((always_inline)) {
-    const f16* wb = a.W + gw_frag_index(type, pair, kh, 0, 0) + lane * 8;
+  // W fragments of the swapped MFMA (its first operand), this wave's K-steps: wg[s] / wf[s] = K-step ks0 + s
+  half8 wg[GW_KA], wf[GW_KA];
+  auto load_w = [&](int ks0, auto n_) __attribute__((always_inline)) {
+    constexpr int N = decltype(n_)::value;
+    const f16* wb = a.W + gw_frag_index(type, pair, ks0, 0) + lane * 8;
 #pragma unroll
-    for (int s = 0; s < GW_KH; ++s) {
+    for (int s = 0; s < N; ++s) {
       wg[s] = *reinterpret_cast<const half8*>(wb + (size_t)(2 * s) * 512);
       wf[s] = *reinterpret_cast<const half8*>(wb + (size_t)(2 * s + 1) * 512);
     }
   };
-  // this wave's 18 K-steps of one block onto (ag, af): A fragments read three K-steps ahead of their MFMAs (one
-  // ds_read_b128 in flight per MFMA pair would leave each pair waiting on LDS latency), pinned to that order
-  auto kloop = [&](const int base[3], int s_off, floatx4& ag, floatx4& af) __attribute__((always_inline)) {
-    half8 av[4];
+  // this wave's 18 K-steps of one block onto (ag, af). The A fragments are read four K-steps ahead of their MFMAs into
+  // five registers sets, and every K-step is its own scheduling segment (sched_barrier): the read of K-step s + 4, the
+  // two MFMAs of K-step s and hook(s), the caller's work for that segment (the second waves' gate epilogue, spread over
+  // the segments so its VALU work sits between MFMAs). Left to itself the scheduler sank each read to just before its
+  // MFMA pair (one read in flight, each pair waiting out the LDS latency: r04k / r04l assembly and step stamps).
+  auto kloop = [&](const int base[3], int s_off, auto n_, floatx4& ag, floatx4& af, auto&& hook)
+                   __attribute__((always_inline)) {
+    constexpr int N = decltype(n_)::value;
+    half8 av[5];
     auto rd = [&](int s) __attribute__((always_inline)) {
       const int ks = s_off + s;
       return *reinterpret_cast<const half8*>(smw + base[ks / 12] + (ks % 12) * 64);
     };
-    av[0] = rd(0);
-    av[1] = rd(1);
-    av[2] = rd(2);
 #pragma unroll
-    for (int s = 0; s < GW_KH; ++s) {
-      if (s + 3 < GW_KH) av[(s + 3) & 3] = rd(s + 3);
+    for (int s = 0; s < 4; ++s) av[s] = rd(s);
+#pragma unroll
+    for (int s = 0; s < N; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 4 < N) av[(s + 4) % 5] = rd(s + 4);
       if constexpr (!(DBG & 2)) {
-        ag = O::mfma(wg[s], av[s & 3], ag);
-        af = O::mfma(wf[s], av[s & 3], af);
+        ag = O::mfma(wg[s], av[s % 5], ag);
+        af = O::mfma(wf[s], av[s % 5], af);
       }
+      hook(s);
     }
+    __builtin_amdgcn_sched_barrier(0);
   };
+  auto no_hook = [](int) __attribute__((always_inline)) {};
 
   if (kh == 0) {
-    // ------------------------------------------------------------------ first waves: K-steps 0..17 + ring DMAs
+    // ------------------------------------------------------------------ first waves: K-steps 0..19 + ring DMAs
     const u32x4 dx = gw_desc(a.X, (int64_t)a.M * GW_C * 2);
     // group g = input rows r_begin - 8 + 32 g .. + 31 into ring slot g % 5; its 25 pieces go to the four first waves
     // round robin (piece p = pair + 4 v): pair 0 issues 7 per group, the others 6. A lane's unit u of piece p -> row
@@ -283,7 +299,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     };
     issue(0);
     issue(1);
-    load_w();
+    load_w(0, std::integral_constant<int, GW_KA>());
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0) through the builtin, so the compiler knows W has landed too
     issue(2);
     issue(3);
@@ -301,16 +317,11 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       int base[3];
       row.bases(a, k, fr, fk, base);
       floatx4 ag = {0.f, 0.f, 0.f, 0.f}, af = {0.f, 0.f, 0.f, 0.f};
-      kloop(base, 0, ag, af);
+      kloop(base, 0, std::integral_constant<int, GW_KA>(), ag, af, no_hook);
       unsigned char* pb = part_buf + (k & 1) * 8192 + lane * 16;
       *reinterpret_cast<floatx4*>(pb) = ag;
       *reinterpret_cast<floatx4*>(pb + 1024) = af;
       row.next(a, tvt);
-#pragma unroll
-      for (int s = 0; s < GW_KH; ++s) {  // one A-fragment read per MFMA pair, three K-steps ahead
-        __builtin_amdgcn_sched_group_barrier(GW_SG_DSR, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(GW_SG_MFMA, 2, 0);
-      }
       gw_stamp_lds<DBG>(smw, 1, k, 0);
       if (k & 1) {
         if (seven) gw_vmwait<3 * PV>(); else gw_vmwait<3 * (PV - 1)>();
@@ -328,7 +339,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       gw_stamp_flush<DBG>(a, smw, 2, nsub);
     }
   } else {
-    // ------------------------------------------------------------------ second waves: K-steps 18..35 + gate epilogue
+    // ------------------------------------------------------------------ second waves: K-steps 20..35 + gate epilogue
     // Step k: the MFMAs of block k - 1 (its partial sums come from step k - 1), interleaved with the gate epilogue of
     // block k - 2, whose accumulators this wave kept from step k - 1. In the steady state (2 <= k < nsub) a step is one
     // basic block, so the scheduler can (and the group barriers below make it) spread the epilogue's VALU work and the
@@ -338,7 +349,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
         __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.cp), (short)0, a.M * a.ld_cp * 2, GW_CFG);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y, (short)0, a.M * a.ldy * 2, GW_CFG);
     gw_stamp<DBG>(a, 0);
-    load_w();
+    load_w(GW_KA, std::integral_constant<int, GW_KB>());
     const float4 bg = *reinterpret_cast<const float4*>(a.bias + ng + 4 * fk);
     const float4 bfv = *reinterpret_cast<const float4*>(a.bias + nf + 4 * fk);
     // conditioner projection of block j, loaded in step j (two steps before its epilogue) into register set j % 3:
@@ -356,34 +367,37 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     gw_barrier();  // (pairs with the first waves' prologue barrier)
     __builtin_amdgcn_s_setprio(1);
     gw_stamp<DBG>(a, 2);
-    // gate in registers (conv_gemm4's DIRECT epilogue arithmetic, same order); rows past the part are dropped
-    auto epilogue = [&](int blk, const GwH4* cp, floatx4 ag, floatx4 af) __attribute__((always_inline)) {
-      const GwH4 cg = cp[0], cf = cp[1];
-      GwH4 pk;
+    // gate of the lane's element i (conv_gemm4's DIRECT epilogue arithmetic, same order), and the block's store (rows
+    // past the part are dropped)
+    auto gate_el = [&](int i, const GwH4* cp, const floatx4& ag, const floatx4& af) __attribute__((always_inline)) {
       if constexpr ((DBG & 4) != 0) {
-        pk.h[0] = (f16)(ag[0] + af[1]);
-        pk.h[1] = (f16)(ag[1] + af[2]);
-        pk.h[2] = (f16)(ag[2] + af[3]);
-        pk.h[3] = (f16)(ag[3] + af[0]);
+        return (f16)(ag[i] + af[(i + 1) & 3]);
       } else {
-        pk.h[0] = O::enc_lo(gate_act(ag[0] + bg.x + O::dec(cg.h[0]), af[0] + bfv.x + O::dec(cf.h[0])));
-        pk.h[1] = O::enc_lo(gate_act(ag[1] + bg.y + O::dec(cg.h[1]), af[1] + bfv.y + O::dec(cf.h[1])));
-        pk.h[2] = O::enc_lo(gate_act(ag[2] + bg.z + O::dec(cg.h[2]), af[2] + bfv.z + O::dec(cf.h[2])));
-        pk.h[3] = O::enc_lo(gate_act(ag[3] + bg.w + O::dec(cg.h[3]), af[3] + bfv.w + O::dec(cf.h[3])));
+        const float b_g = i == 0 ? bg.x : (i == 1 ? bg.y : (i == 2 ? bg.z : bg.w));
+        const float b_f = i == 0 ? bfv.x : (i == 1 ? bfv.y : (i == 2 ? bfv.z : bfv.w));
+        return O::enc_lo(gate_act(ag[i] + b_g + O::dec(cp[0].h[i]), af[i] + b_f + O::dec(cp[1].h[i])));
       }
+    };
+    auto store_blk = [&](int blk, const GwH4& pk) __attribute__((always_inline)) {
       const int m = r_begin + blk * 16 + fr;
       const uint32_t vo = m < r_end ? (uint32_t)m * (uint32_t)(a.ldy * 2) + (uint32_t)ch * 2 : GW_OOR;
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, pk.u), ry,
                                             vo, 0, 0);
     };
-    // the MFMAs of block blk on its partial sums (K-steps 18..23: tap 1 channels 192..383; 24..35: tap 2)
-    auto mfma_blk = [&](int blk, floatx4& ag, floatx4& af) __attribute__((always_inline)) {
+    auto epilogue = [&](int blk, const GwH4* cp, const floatx4& ag, const floatx4& af) __attribute__((always_inline)) {
+      GwH4 pk;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pk.h[i] = gate_el(i, cp, ag, af);
+      store_blk(blk, pk);
+    };
+    // the MFMAs of block blk on its partial sums (K-steps 20..23: tap 1 channels 256..383; 24..35: tap 2)
+    auto mfma_blk = [&](int blk, floatx4& ag, floatx4& af, auto&& hook) __attribute__((always_inline)) {
       int base[3];
       row.bases(a, blk, fr, fk, base);
       const unsigned char* pb = part_buf + (blk & 1) * 8192 + lane * 16;
       ag = *reinterpret_cast<const floatx4*>(pb);
       af = *reinterpret_cast<const floatx4*>(pb + 1024);
-      kloop(base, GW_KH, ag, af);
+      kloop(base, GW_KA, std::integral_constant<int, GW_KB>(), ag, af, hook);
       row.next(a, tvt);
     };
     auto end_step = [&](int k) __attribute__((always_inline)) {
@@ -391,28 +405,27 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       gw_barrier();
       gw_stamp<DBG>(a, 3 + k);
     };
-    // steady step k (2 <= k < nsub): cp(k) into LS, MFMAs of block k - 1, epilogue of block k - 2 from ES
+    // steady step k (2 <= k < nsub): cp(k) into LS, MFMAs of block k - 1 with the epilogue of block k - 2 (cp from ES)
+    // in their K-step segments: element i in segment 4 i + 3, the store in the last
     auto steady = [&](int k, GwH4* ls, const GwH4* es) __attribute__((always_inline)) {
       load_cp(k, ls);
       floatx4 ag, af;
-      mfma_blk(k - 1, ag, af);
-      epilogue(k - 2, es, pg, pf);
+      const floatx4 eg = pg, ef = pf;
+      GwH4 pk;
+      auto hook = [&](int s) __attribute__((always_inline)) {
+        if (s % 4 == 3) pk.h[s / 4] = gate_el(s / 4, es, eg, ef);
+        if (s == GW_KB - 1) store_blk(k - 2, pk);
+      };
+      mfma_blk(k - 1, ag, af, hook);
       pg = ag;
       pf = af;
-      // one A-fragment read, two MFMAs and 8 of the epilogue's ~150 VALU instructions per K-step
-#pragma unroll
-      for (int s = 0; s < GW_KH; ++s) {
-        __builtin_amdgcn_sched_group_barrier(GW_SG_DSR, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(GW_SG_MFMA, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(GW_SG_VALU, 8, 0);
-      }
       end_step(k);
     };
     // step 0: cp(0); step 1: cp(1), MFMAs of block 0
     load_cp(0, c0);
     end_step(0);
     if (nsub >= 2) load_cp(1, c1);
-    mfma_blk(0, pg, pf);
+    mfma_blk(0, pg, pf, no_hook);
     end_step(1);
     int k = 2;
     for (; k + 3 <= nsub; k += 3) {  // k = 2 mod 3: loads into c2, c0, c1; epilogues from c0, c1, c2
@@ -432,7 +445,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     };
     if (nsub >= 2) {
       floatx4 ag, af;
-      mfma_blk(nsub - 1, ag, af);
+      mfma_blk(nsub - 1, ag, af, no_hook);
       epi_set(nsub - 2);
       pg = ag;
       pf = af;
@@ -451,13 +464,11 @@ __global__ void gate_ws_pack_kernel(const f16* __restrict__ W, f16* __restrict__
   int r = i >> 6;
   const int g = r & 1;
   r >>= 1;
-  const int s = r % GW_KH;
-  r /= GW_KH;
-  const int kh = r & 1;
-  r >>= 1;
+  const int ks = r % GW_KS;
+  r /= GW_KS;
   const int p = r & 3, c = r >> 2;
   const int n = 64 * (2 * c + (p >> 1)) + 16 * (p & 1) + 32 * g + (lane & 15);
-  const int k = 32 * (GW_KH * kh + s) + 8 * (lane >> 4);
+  const int k = 32 * ks + 8 * (lane >> 4);
   *reinterpret_cast<uint4*>(Wf + (size_t)i * 8) = *reinterpret_cast<const uint4*>(W + (size_t)n * GW_K + k);
 }
 
@@ -494,10 +505,13 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   GateWsArgs g{a.X, a.Wfrag, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
                1.0f / (float)a.T_out, gate_ws_stamps};
   // diagnostics instances (fp16 only): 2 no MFMAs, 4 no gate arithmetic, 8 step stamps (SVC_GWS_STAMPS)
+  static const int ka = getenv("SVC_GWS_KA") ? atoi(getenv("SVC_GWS_KA")) : GW_KA_DEF;  // (A/B runs, read once)
   const void* fn = a.bf16 ? (const void*)gate_ws_kernel<true, 0> : (const void*)gate_ws_kernel<false, 0>;
   if (!a.bf16 && gate_ws_stamps) fn = (const void*)gate_ws_kernel<false, 8>;
   else if (!a.bf16 && dbg == 2) fn = (const void*)gate_ws_kernel<false, 2>;
   else if (!a.bf16 && dbg == 4) fn = (const void*)gate_ws_kernel<false, 4>;
+  else if (!a.bf16 && ka == 18) fn = (const void*)gate_ws_kernel<false, 0, 18>;
+  else if (!a.bf16 && ka == 22) fn = (const void*)gate_ws_kernel<false, 0, 22>;
   if (int st = ensure_dyn_lds(fn, GW_LDS)) return st;
   const int tok = prof_begin("gate_ws<16x128>", 2.0 * M * (double)GW_N * GW_K, 0.0, s);
   void* args[] = {&g};
@@ -534,7 +548,8 @@ constexpr int G5_GBYTES = 32 * G5_STRIDE;        // 25,088 B
 constexpr int G5_PART = G5_NG * G5_GBYTES;       // 125,440: partials [2 buffers][4 pairs][4 KiB]
 constexpr int G5_ZERO = G5_PART + 2 * 4 * 4096;  // 158,208: 784 B of zeros
 constexpr int G5_TVT = G5_ZERO + G5_STRIDE;      // 158,992: valid input rows per utterance
-constexpr int G5_LDS = G5_TVT + GW_MAXB * 4;     // 163,088 B
+constexpr int G5_BIAS = G5_TVT + GW_MAXB * 4;    // 163,088: the workgroup's 128 packed biases (f32)
+constexpr int G5_LDS = G5_BIAS + 128 * 4;         // 163,600 B
 constexpr int G5_STL = G5_TVT + 256 * 4;         // stamps variant (B <= 256): 3 x GW_NSTAMP u64 after a 256-entry table
 static_assert(G5_LDS <= 163840 && G5_STL + 3 * GW_NSTAMP * 8 <= G5_LDS, "gate_ws32 LDS");
 
@@ -644,22 +659,23 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws32_kernel(GateWsArgs a) {
 #pragma unroll
     for (int s = 0; s < G5_KH; ++s) w[s] = *reinterpret_cast<const half8*>(wb + (size_t)s * 512);
   };
-  // this wave's 36 K-steps of one block onto acc, B fragments read three K-steps ahead (K-step ks: tap ks / 24,
-  // channels 16 (ks % 24) ..)
+  // this wave's 36 K-steps of one block onto acc (K-step ks: tap ks / 24, channels 16 (ks % 24) ..): the B fragments
+  // read four K-steps ahead into five register sets, one scheduling segment per K-step (as gate_ws's kloop)
   auto kloop = [&](const int base[3], int s_off, floatx16& acc) __attribute__((always_inline)) {
-    half8 av[4];
+    half8 av[5];
     auto rd = [&](int s) __attribute__((always_inline)) {
       const int ks = s_off + s;
       return *reinterpret_cast<const half8*>(smw + base[ks / 24] + (ks % 24) * 32);
     };
-    av[0] = rd(0);
-    av[1] = rd(1);
-    av[2] = rd(2);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) av[s] = rd(s);
 #pragma unroll
     for (int s = 0; s < G5_KH; ++s) {
-      if (s + 3 < G5_KH) av[(s + 3) & 3] = rd(s + 3);
-      if constexpr (!(DBG & 2)) acc = O::mfma32(w[s], av[s & 3], acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 4 < G5_KH) av[(s + 4) % 5] = rd(s + 4);
+      if constexpr (!(DBG & 2)) acc = O::mfma32(w[s], av[s % 5], acc);
     }
+    __builtin_amdgcn_sched_barrier(0);
   };
 
   if (kh == 0) {
@@ -736,10 +752,13 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws32_kernel(GateWsArgs a) {
     load_w();
     // the lane's channels: group A ch0 + 4 fk .. + 3 (accumulators 0..3 gate, 8..11 filter), group B ch0 + 8 + 4 fk
     // (4..7, 12..15)
-    const float4 bgA = *reinterpret_cast<const float4*>(a.bias + ng + 4 * fk);
-    const float4 bgB = *reinterpret_cast<const float4*>(a.bias + ng + 8 + 4 * fk);
-    const float4 bfA = *reinterpret_cast<const float4*>(a.bias + nf + 4 * fk);
-    const float4 bfB = *reinterpret_cast<const float4*>(a.bias + nf + 8 + 4 * fk);
+    // (their biases are read from LDS in the epilogue: 16 VGPRs held for the whole loop left too few for the K-loop's
+    // read-ahead). Bias of packed column 128 type + i at G5_BIAS + 4 i
+    {
+      float* bl = reinterpret_cast<float*>(smw + G5_BIAS);
+      for (int i = tid - 256; i < 128; i += 256) bl[i] = a.bias[128 * type + i];
+    }
+    const float* bl = reinterpret_cast<const float*>(smw + G5_BIAS) - 128 * type;
     auto load_cp = [&](int blk, GwH4* dst) __attribute__((always_inline)) {
       const uint32_t vo = (uint32_t)(r_begin + blk * G5_BR + fr) * (uint32_t)(a.ld_cp * 2);  // rows past M read 0
       dst[0].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (ng + 4 * fk) * 2, 0, 0));
@@ -756,6 +775,10 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws32_kernel(GateWsArgs a) {
     gw_stamp<DBG>(a, 2);
     auto epilogue = [&](int blk, const GwH4* cp, const floatx16& acc) __attribute__((always_inline)) {
       GwH4 pa, pb;
+      const float4 bgA = *reinterpret_cast<const float4*>(bl + ng + 4 * fk);
+      const float4 bgB = *reinterpret_cast<const float4*>(bl + ng + 8 + 4 * fk);
+      const float4 bfA = *reinterpret_cast<const float4*>(bl + nf + 4 * fk);
+      const float4 bfB = *reinterpret_cast<const float4*>(bl + nf + 8 + 4 * fk);
       const float bga[4] = {bgA.x, bgA.y, bgA.z, bgA.w}, bgb[4] = {bgB.x, bgB.y, bgB.z, bgB.w};
       const float bfa[4] = {bfA.x, bfA.y, bfA.z, bfA.w}, bfb[4] = {bfB.x, bfB.y, bfB.z, bfB.w};
 #pragma unroll

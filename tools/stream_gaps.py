@@ -12,7 +12,7 @@ def main():
     f = glob.glob(os.path.join(sys.argv[1], "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
     ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], r["Kernel_Name"]) for r in rows)
-    g4 = [e for e in ev if "conv_gemm4" in e[3]]
+    g4 = [e for e in ev if "conv_gemm4" in e[3] or "gate_ws" in e[3]]
     t0, t1 = g4[0][0], g4[-1][1]
     by = collections.defaultdict(list)
     for s, e, q, _ in ev:
