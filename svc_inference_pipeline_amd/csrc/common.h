@@ -100,6 +100,16 @@ __device__ __forceinline__ float gate_act(float a, float b) {
   return copysignf(r, b);
 }
 
+// 8-byte buffer store, optionally write-through (cache policy sc1): the line leaves L2 clean, so the release at the end of
+// the kernel has none of it to write back (MI355X_MICROARCH.md, price list row "boundary": + dirty bytes / 6 TB/s)
+__device__ __forceinline__ void buffer_store_b64(uint2 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, bool wt) {
+  typedef unsigned int u32x2v __attribute__((vector_size(8)));
+  if (wt) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, v), r, vo, 0, 16);
+  else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, v), r, vo, 0, 0);
+}
+// SVC_STORE_WT=1: the DiffSVC row-stream kernels (gate_ws, res_proj) store write-through (A/B runs; read once)
+int store_write_through();
+
 // ------------------------------------------------------------------ 16-bit MFMA operand formats
 // GEMM operands (activations and packed weights) are 16-bit values in f16-typed buffers: IEEE binary16 by default, or
 // bfloat16 bit patterns when a context runs its DiffSVC / content-encoder GEMMs in the bf16 operand variant (config

@@ -367,6 +367,10 @@ const Tuning& tuning() {
 }
 TuningScope::TuningScope(const Tuning* t) : prev(t_tuning) { t_tuning = t; }
 TuningScope::~TuningScope() { t_tuning = prev; }
+int store_write_through() {
+  static const int wt = getenv("SVC_STORE_WT") ? atoi(getenv("SVC_STORE_WT")) : 0;
+  return wt;
+}
 int ensure_dyn_lds(const void* fn, int bytes) {
   static std::mutex mu;
   static std::set<std::tuple<const void*, int, int>> done;

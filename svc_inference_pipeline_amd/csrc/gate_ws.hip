@@ -83,6 +83,7 @@ struct GateWsArgs {
   int tv_mul, B;
   float invT;
   unsigned long long* stamps;  // diagnostics (SVC_GWS_STAMPS, svc_gemm_bench only): s_memtime per workgroup and step
+  int wt;             // write-through output stores (store_write_through)
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -381,8 +382,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     auto store_blk = [&](int blk, const GwH4& pk) __attribute__((always_inline)) {
       const int m = r_begin + blk * 16 + fr;
       const uint32_t vo = m < r_end ? (uint32_t)m * (uint32_t)(a.ldy * 2) + (uint32_t)ch * 2 : GW_OOR;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, pk.u), ry,
-                                            vo, 0, 0);
+      buffer_store_b64(pk.u, ry, vo, a.wt);
     };
     auto epilogue = [&](int blk, const GwH4* cp, const floatx4& ag, const floatx4& af) __attribute__((always_inline)) {
       GwH4 pk;
@@ -503,7 +503,7 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   if (M == 0) return SVC_OK;
   static const int dbg = getenv("SVC_GWS_DBG") ? atoi(getenv("SVC_GWS_DBG")) : 0;  // (diagnostics, read once)
   GateWsArgs g{a.X, a.Wfrag, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
-               1.0f / (float)a.T_out, gate_ws_stamps};
+               1.0f / (float)a.T_out, gate_ws_stamps, store_write_through()};
   // diagnostics instances (fp16 only): 2 no MFMAs, 4 no gate arithmetic, 8 step stamps (SVC_GWS_STAMPS)
   static const int ka = getenv("SVC_GWS_KA") ? atoi(getenv("SVC_GWS_KA")) : GW_KA_DEF;  // (A/B runs, read once)
   const void* fn = a.bf16 ? (const void*)gate_ws_kernel<true, 0> : (const void*)gate_ws_kernel<false, 0>;
@@ -793,10 +793,8 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws32_kernel(GateWsArgs a) {
       }
       const int m = r_begin + blk * G5_BR + fr;
       const uint32_t vo = m < r_end ? (uint32_t)m * (uint32_t)(a.ldy * 2) + (uint32_t)(ch0 + 4 * fk) * 2 : GW_OOR;
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, pa.u), ry,
-                                            vo, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((vector_size(8))) unsigned int, pb.u), ry,
-                                            vo == GW_OOR ? GW_OOR : vo + 16, 0, 0);
+      buffer_store_b64(pa.u, ry, vo, a.wt);
+      buffer_store_b64(pb.u, ry, vo == GW_OOR ? GW_OOR : vo + 16, a.wt);
     };
     auto mfma_blk = [&](int blk, floatx16& acc) __attribute__((always_inline)) {
       int base[3];
@@ -882,7 +880,7 @@ int gate_ws32(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   if (M == 0) return SVC_OK;
   static const int dbg = getenv("SVC_GWS_DBG") ? atoi(getenv("SVC_GWS_DBG")) : 0;  // (diagnostics, read once)
   GateWsArgs g{a.X, a.Wfrag32, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
-               1.0f / (float)a.T_out, gate_ws_stamps};
+               1.0f / (float)a.T_out, gate_ws_stamps, store_write_through()};
   const void* fn = a.bf16 ? (const void*)gate_ws32_kernel<true, 0> : (const void*)gate_ws32_kernel<false, 0>;
   if (!a.bf16 && gate_ws_stamps) {
     SVC_REQUIRE(a.B <= 256, "gate_ws32 stamps: B <= 256");
