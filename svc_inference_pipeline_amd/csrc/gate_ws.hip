@@ -8,12 +8,13 @@
 // whole L2 -> LDS bandwidth of a CU (64 B per clock), so its K-loop runs at ~0.4 of the MFMA peak.
 // Here the weights stay put instead:
 //   * a workgroup owns 128 packed columns = 64 output channels, as 4 column sets of 16 gate + 16 filter columns; each set
-//     belongs to a PAIR of waves on one SIMD (waves w and w + 4): wave w holds the set's weights for K-steps 0..19 (tap
-//     0 and the first 256 channels of tap 1), wave w + 4 for K-steps 20..35, as MFMA fragments in VGPRs (2 x 20 / 16 x half8 = 160 / 128
+//     belongs to a PAIR of waves on one SIMD (waves w and w + 4): wave w holds the set's weights for K-steps 0..21 (tap
+//     0 and the first 320 channels of tap 1), wave w + 4 for K-steps 22..35, as MFMA fragments in VGPRs (2 x 22 / 14 x
+//     half8 = 176 / 112
 //     registers each: two waves per SIMD), loaded once per launch;
-//   * the workgroup walks its share of the rows in 16-row blocks: in step k the first wave of a pair runs K-steps 0..19
+//   * the workgroup walks its share of the rows in 16-row blocks: in step k the first wave of a pair runs K-steps 0..21
 //     of block k and hands its two f32 accumulators to its partner through LDS, which continues them over K-steps
-//     20..35 for block k - 1 (the partial sums are the partner's MFMA C operand, so the K order is one sequential chain,
+//     22..35 for block k - 1 (the partial sums are the partner's MFMA C operand, so the K order is one sequential chain,
 //     exactly conv_gemm4's) and applies the gate in registers; one workgroup barrier per step;
 //   * the input rows come through a ring of 160 rows in LDS, DMA'd in 32-row groups (25 KiB) once each: the three taps
 //     of a block read its rows at offsets -dil, 0, +dil, so no row is fetched twice, and a group is issued 5 steps
@@ -44,9 +45,11 @@ constexpr int GW_C = 384;             // channels per tap
 constexpr int GW_N = 768;             // packed output columns (gate | filter per 64-column block)
 constexpr int GW_K = 3 * GW_C;        // 1152 = 36 K-steps of 32
 constexpr int GW_KS = 36;             // K-steps of 32
-constexpr int GW_KA_DEF = 20;         // K-steps of a pair's first wave (0..19); its partner takes 20..35. Unequal on
+constexpr int GW_KA_DEF = 22;         // K-steps of a pair's first wave (0..21); its partner takes 22..35. Unequal on
                                       // purpose: the partner also runs the gate epilogue (18 / 18: partner 2248 vs
-                                      // 1672 cycles per step, r04m stamps). SVC_GWS_KA (18 / 20 / 22) for A/B runs
+                                      // 1672 cycles per step, r04m stamps). 18 / 20 / 22: 880.7 / 880.5 / 890.2 and
+                                      // 878.1 / 879.7 / 891.0 audio-s/s (r04n, alternating). SVC_GWS_KA (20 / 23 / 24)
+                                      // for A/B runs
 constexpr int GW_HALO = 8;            // largest tap shift (dilation 8): ring row 0 = input row r_begin - 8
 constexpr int GW_GR = 32;             // rows per DMA group
 constexpr int GW_NG = 5;              // ring slots (groups): 160 rows
@@ -275,7 +278,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
   auto no_hook = [](int) __attribute__((always_inline)) {};
 
   if (kh == 0) {
-    // ------------------------------------------------------------------ first waves: K-steps 0..19 + ring DMAs
+    // ------------------------------------------------------------------ first waves: K-steps 0..GW_KA - 1 + ring DMAs
     const u32x4 dx = gw_desc(a.X, (int64_t)a.M * GW_C * 2);
     // group g = input rows r_begin - 8 + 32 g .. + 31 into ring slot g % 5; its 25 pieces go to the four first waves
     // round robin (piece p = pair + 4 v): pair 0 issues 7 per group, the others 6. A lane's unit u of piece p -> row
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       gw_stamp_flush<DBG>(a, smw, 2, nsub);
     }
   } else {
-    // ------------------------------------------------------------------ second waves: K-steps 20..35 + gate epilogue
+    // ------------------------------------------------------------------ second waves: K-steps GW_KA..35 + gate epilogue
     // Step k: the MFMAs of block k - 1 (its partial sums come from step k - 1), interleaved with the gate epilogue of
     // block k - 2, whose accumulators this wave kept from step k - 1. In the steady state (2 <= k < nsub) a step is one
     // basic block, so the scheduler can (and the group barriers below make it) spread the epilogue's VALU work and the
@@ -390,7 +393,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       for (int i = 0; i < 4; ++i) pk.h[i] = gate_el(i, cp, ag, af);
       store_blk(blk, pk);
     };
-    // the MFMAs of block blk on its partial sums (K-steps 20..23: tap 1 channels 256..383; 24..35: tap 2)
+    // the MFMAs of block blk on its partial sums (K-steps GW_KA..23: the rest of tap 1; 24..35: tap 2)
     auto mfma_blk = [&](int blk, floatx4& ag, floatx4& af, auto&& hook) __attribute__((always_inline)) {
       int base[3];
       row.bases(a, blk, fr, fk, base);
@@ -510,8 +513,9 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   if (!a.bf16 && gate_ws_stamps) fn = (const void*)gate_ws_kernel<false, 8>;
   else if (!a.bf16 && dbg == 2) fn = (const void*)gate_ws_kernel<false, 2>;
   else if (!a.bf16 && dbg == 4) fn = (const void*)gate_ws_kernel<false, 4>;
-  else if (!a.bf16 && ka == 18) fn = (const void*)gate_ws_kernel<false, 0, 18>;
-  else if (!a.bf16 && ka == 22) fn = (const void*)gate_ws_kernel<false, 0, 22>;
+  else if (!a.bf16 && ka == 20) fn = (const void*)gate_ws_kernel<false, 0, 20>;
+  else if (!a.bf16 && ka == 23) fn = (const void*)gate_ws_kernel<false, 0, 23>;
+  else if (!a.bf16 && ka == 24) fn = (const void*)gate_ws_kernel<false, 0, 24>;
   if (int st = ensure_dyn_lds(fn, GW_LDS)) return st;
   const int tok = prof_begin("gate_ws<16x128>", 2.0 * M * (double)GW_N * GW_K, 0.0, s);
   void* args[] = {&g};
