@@ -13,7 +13,6 @@
 typedef _Float16 f16;
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx4 __attribute__((ext_vector_type(4)));
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 #define SVC_OK 0
 #define SVC_ERR_INVALID 1
@@ -100,15 +99,13 @@ __device__ __forceinline__ float gate_act(float a, float b) {
   return copysignf(r, b);
 }
 
-// 8-byte buffer store, optionally write-through (cache policy sc1): the line leaves L2 clean, so the release at the end of
-// the kernel has none of it to write back (MI355X_MICROARCH.md, price list row "boundary": + dirty bytes / 6 TB/s)
-__device__ __forceinline__ void buffer_store_b64(uint2 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, bool wt) {
+// 8-byte buffer store (range-checked: a voffset past the descriptor's range is dropped). Write-through (cache policy
+// sc1), so that the kernel-end release would find the outputs clean, measured slower for the row-stream kernels
+// (r04n: 855.8 / 857.1 against 879.6 / 881.3 audio-s/s): plain write-back
+__device__ __forceinline__ void buffer_store_b64(uint2 v, __amdgpu_buffer_rsrc_t r, uint32_t vo) {
   typedef unsigned int u32x2v __attribute__((vector_size(8)));
-  if (wt) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, v), r, vo, 0, 16);
-  else __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, v), r, vo, 0, 0);
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, v), r, vo, 0, 0);
 }
-// SVC_STORE_WT=1: the DiffSVC row-stream kernels (gate_ws, res_proj) store write-through (A/B runs; read once)
-int store_write_through();
 
 // ------------------------------------------------------------------ 16-bit MFMA operand formats
 // GEMM operands (activations and packed weights) are 16-bit values in f16-typed buffers: IEEE binary16 by default, or
@@ -125,9 +122,6 @@ struct Op16<false> {
   static __device__ __forceinline__ floatx4 mfma(half8 a, half8 b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
   }
-  static __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-  }
 };
 template <>
 struct Op16<true> {
@@ -138,10 +132,6 @@ struct Op16<true> {
   static __device__ __forceinline__ f16 enc_lo(float v) { return __builtin_bit_cast(f16, (__bf16)v); }
   static __device__ __forceinline__ floatx4 mfma(half8 a, half8 b, floatx4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
-                                                   0, 0, 0);
-  }
-  static __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c,
                                                    0, 0, 0);
   }
 };
@@ -174,8 +164,7 @@ struct ConvGemmArgs {
   const int* tv;
   int tv_mul;
   int bf16;      // operands (X, W) are bfloat16 (Op16<true>); the epilogue's 16-bit inputs / outputs too
-  const f16* Wfrag;    // W once more in a kernel's own fragment order (gate_ws; NULL: none)
-  const f16* Wfrag32;  // and in gate_ws32's (NULL: none)
+  const f16* Wfrag;  // W once more in a kernel's own fragment order (gate_ws; NULL: none)
 };
 
 __device__ __forceinline__ int valid_in_rows(const ConvGemmArgs& a, int b) {

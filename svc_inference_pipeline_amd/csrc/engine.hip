@@ -112,9 +112,6 @@ bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e);
 extern unsigned long long* gate_ws_stamps;
 int gate_ws_nstamp();
 int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
-int gate_ws32(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
-bool gate_ws32_fits(const ConvGemmArgs& a, const EpiArgs& e);
-int gate_ws32_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
 int gate_ws_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
 size_t gate_ws_pack_elems();
 int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, const float* add, float div, f16* hi,
@@ -256,7 +253,6 @@ struct PackedGemm {
   int N = 0, Npad = 0, K = 0, Kpad = 0, Cp = 0, Cin = 0, taps = 0;
   int tap_mul = 1, tap_add = 0, istride = 1;
   bool bf16 = false;  // W (and so the GEMM's operands) in bfloat16 (the bf16 operand variant, common.h Op16)
-  f16* Wfrag32 = nullptr;  // the dilated convs' W in gate_ws32's fragment order
   f16* Wfrag = nullptr;  // W in a kernel's fragment order: the DiffSVC residual projections (res_proj.hip), the dilated
                          // convs (gate_ws.hip)
 };
@@ -367,10 +363,6 @@ const Tuning& tuning() {
 }
 TuningScope::TuningScope(const Tuning* t) : prev(t_tuning) { t_tuning = t; }
 TuningScope::~TuningScope() { t_tuning = prev; }
-int store_write_through() {
-  static const int wt = getenv("SVC_STORE_WT") ? atoi(getenv("SVC_STORE_WT")) : 0;
-  return wt;
-}
 int ensure_dyn_lds(const void* fn, int bytes) {
   static std::mutex mu;
   static std::set<std::tuple<const void*, int, int>> done;
@@ -703,7 +695,6 @@ static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cv
   a.N = g.N;
   a.bf16 = g.bf16 ? 1 : 0;
   a.Wfrag = g.Wfrag;
-  a.Wfrag32 = g.Wfrag32;
   if (e.T_ostore == 0) {
     e.T_ostore = T_out;
     e.ostride = 1;
@@ -741,7 +732,6 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
       }
   }
   // the DiffSVC dilated conv + gate: the weight-stationary row stream (gate_ws.hip) where it fits, else conv_gemm4
-  if (variant == 15 && pair && tu.gate_ws == 2 && gate_ws32_fits(a, e)) return gate_ws32(a, e, s);
   if (variant == 15 && pair && tu.gate_ws && gate_ws_fits(a, e)) return gate_ws(a, e, s);
   if (variant == 15 && pair) variant = 24;
   // The skip-sum GEMM of a sampler sub-batch (K = 20 x 384, M <= 20 k rows) takes conv_gemm3's 256 x 128 tile although
@@ -1112,12 +1102,6 @@ int build_mapper(svc_ctx* c) {
       c->weight_bytes += (int64_t)(gate_ws_pack_elems() * sizeof(f16));
       c->dil[i].Wfrag = reinterpret_cast<f16*>(wf);
       if ((st = gate_ws_pack(c->dil[i].W, c->dil[i].Kpad, c->dil[i].Wfrag, 0))) return st;
-      void* wf32 = nullptr;
-      SVC_HIP_CHECK(hipMalloc(&wf32, gate_ws_pack_elems() * sizeof(f16)));
-      c->allocs.push_back(wf32);
-      c->weight_bytes += (int64_t)(gate_ws_pack_elems() * sizeof(f16));
-      c->dil[i].Wfrag32 = reinterpret_cast<f16*>(wf32);
-      if ((st = gate_ws32_pack(c->dil[i].W, c->dil[i].Kpad, c->dil[i].Wfrag32, 0))) return st;
       SVC_HIP_CHECK(hipStreamSynchronize(0));
     }
     // rows 0..C-1 of output_projection are the residual, C..2C-1 the skip (modules/diffsvc.py:229-231)
@@ -2860,9 +2844,9 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
   SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24 ||
                   (variant == 30 && epi_kind == 6 && N == 384 && Cin == 384 && taps == 1) ||
-                  ((variant == 40 || variant == 41) && epi_kind == 1 && N == 768 && Cin == 384 && taps == 3),
-              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap; 40 / 41: gate_ws / "
-              "gate_ws32, gate epilogue, N = 768, Cin = 384, 3 taps)", variant);
+                  (variant == 40 && epi_kind == 1 && N == 768 && Cin == 384 && taps == 3),
+              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap; 40: gate_ws, gate "
+              "epilogue, N = 768, Cin = 384, 3 taps)", variant);
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float *bias, *R = nullptr;
@@ -2912,10 +2896,6 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
     SVC_HIP_CHECK(hipMalloc(&Wf, gate_ws_pack_elems() * sizeof(f16)));
     st = gate_ws_pack(W, Kpad, Wf, 0);
     a.Wfrag = Wf;
-  } else if (variant == 41) {
-    SVC_HIP_CHECK(hipMalloc(&Wf, gate_ws_pack_elems() * sizeof(f16)));
-    st = gate_ws32_pack(W, Kpad, Wf, 0);
-    a.Wfrag32 = Wf;
   }
   hipEvent_t e0, e1;
   SVC_HIP_CHECK(hipEventCreate(&e0));
@@ -2932,11 +2912,10 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
     if (variant == 30) return res_proj(X, Wf, bias, bias, bias, e.acc_div, Y, reinterpret_cast<f16*>(R), M, false, 0, 0);
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
     if (variant == 40) return gate_ws(a, e, 0);
-    if (variant == 41) return gate_ws32(a, e, 0);
     return conv_gemm3(a, e, zero_page(), variant - 10, 0);
   };
   for (int w = 0; w < 2 && !st; ++w) st = run();
-  if (const char* sp = (variant == 40 || variant == 41) ? getenv("SVC_GWS_STAMPS") : nullptr) {  // (bench tool only) step timeline
+  if (const char* sp = variant == 40 ? getenv("SVC_GWS_STAMPS") : nullptr) {  // (bench tool only) step timeline
     unsigned long long* ds = nullptr;
     const size_t n = (size_t)256 * gate_ws_nstamp();
     SVC_HIP_CHECK(hipMalloc(&ds, n * 8));

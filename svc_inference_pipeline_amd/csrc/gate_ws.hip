@@ -86,7 +86,6 @@ struct GateWsArgs {
   int tv_mul, B;
   float invT;
   unsigned long long* stamps;  // diagnostics (SVC_GWS_STAMPS, svc_gemm_bench only): s_memtime per workgroup and step
-  int wt;             // write-through output stores (store_write_through)
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -385,7 +384,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     auto store_blk = [&](int blk, const GwH4& pk) __attribute__((always_inline)) {
       const int m = r_begin + blk * 16 + fr;
       const uint32_t vo = m < r_end ? (uint32_t)m * (uint32_t)(a.ldy * 2) + (uint32_t)ch * 2 : GW_OOR;
-      buffer_store_b64(pk.u, ry, vo, a.wt);
+      buffer_store_b64(pk.u, ry, vo);
     };
     auto epilogue = [&](int blk, const GwH4* cp, const floatx4& ag, const floatx4& af) __attribute__((always_inline)) {
       GwH4 pk;
@@ -506,7 +505,7 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   if (M == 0) return SVC_OK;
   static const int dbg = getenv("SVC_GWS_DBG") ? atoi(getenv("SVC_GWS_DBG")) : 0;  // (diagnostics, read once)
   GateWsArgs g{a.X, a.Wfrag, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
-               1.0f / (float)a.T_out, gate_ws_stamps, store_write_through()};
+               1.0f / (float)a.T_out, gate_ws_stamps};
   // diagnostics instances (fp16 only): 2 no MFMAs, 4 no gate arithmetic, 8 step stamps (SVC_GWS_STAMPS)
   static const int ka = getenv("SVC_GWS_KA") ? atoi(getenv("SVC_GWS_KA")) : GW_KA_DEF;  // (A/B runs, read once)
   const void* fn = a.bf16 ? (const void*)gate_ws_kernel<true, 0> : (const void*)gate_ws_kernel<false, 0>;
@@ -526,381 +525,5 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
 }
 
 
-// ------------------------------------------------------------------------------------------------------------------
-// gate_ws32 (tune.gate_ws = 2): the same weight-stationary row stream on v_mfma_f32_32x32x16. A 16x16x32 MFMA holds its
-// SIMD's vector issue for 8 of its 16 cycles, a 32x32x16 for 8 of its 32 (MI355X_MICROARCH.md, issue costs), so per
-// FLOP the 32-row form leaves three quarters of the issue slots, not half, to the ring DMAs, the A-fragment reads and
-// the gate epilogue, which in gate_ws share the SIMD with the MFMAs (its step runs at about twice the MFMA time).
-//   * blocks of 32 rows; a wave pair holds 32 W rows = 16 gate + 16 filter columns of 16 channels (K-steps of 16:
-//     wave w 0..35, wave w + 4 36..71, 36 x half8 = 144 VGPRs each). With W as the MFMA's first operand, lane l's 16
-//     accumulators are column l % 32 (the block's row) and W rows 8 (v / 4) + 4 (l / 32) + v % 4: gate channel c and
-//     filter channel c land in the same lane (v and v + 8), so the gate needs no lane exchange;
-//   * the partner wave takes the first wave's 16 accumulators through LDS as its C operand (one chain per output);
-//   * the second wave runs the block's MFMAs and then its own epilogue in the same step: its MFMAs go first at
-//     priority 1, and the epilogue's VALU work fills the issue slots beside the first wave's MFMAs;
-//   * the ring: 160 rows of 784 B (768 + one 16-B bank slot: the 32-row B-fragment reads, 16 rows per lane group, are
-//     conflict-free at any row offset), 32-row groups of 24.5 DMA pieces (the last on lanes 0..31), 5 slots; group g
-//     is read by blocks g - 1 and g and issued at step g - 3 (two steps before its first reader).
-// The K order differs from conv_gemm4 (16-deep MFMA steps instead of 32), so the result is not bit-identical to it:
-// tests/test_gpu_stages.py::test_gate_ws32_close holds it to conv_gemm4 within one f16 unit.
-constexpr int G5_BR = 32;
-constexpr int G5_KH = 36;
-constexpr int G5_STRIDE = 784;
-constexpr int G5_NG = 5;
-constexpr int G5_RROWS = G5_NG * 32;
-constexpr int G5_GBYTES = 32 * G5_STRIDE;        // 25,088 B
-constexpr int G5_PART = G5_NG * G5_GBYTES;       // 125,440: partials [2 buffers][4 pairs][4 KiB]
-constexpr int G5_ZERO = G5_PART + 2 * 4 * 4096;  // 158,208: 784 B of zeros
-constexpr int G5_TVT = G5_ZERO + G5_STRIDE;      // 158,992: valid input rows per utterance
-constexpr int G5_BIAS = G5_TVT + GW_MAXB * 4;    // 163,088: the workgroup's 128 packed biases (f32)
-constexpr int G5_LDS = G5_BIAS + 128 * 4;         // 163,600 B
-constexpr int G5_STL = G5_TVT + 256 * 4;         // stamps variant (B <= 256): 3 x GW_NSTAMP u64 after a 256-entry table
-static_assert(G5_LDS <= 163840 && G5_STL + 3 * GW_NSTAMP * 8 <= G5_LDS, "gate_ws32 LDS");
-
-__device__ __forceinline__ size_t g5_frag_index(int c, int p, int kh, int s) {
-  return (size_t)(((c * 4 + p) * 2 + kh) * G5_KH + s) * 512;
-}
-
-template <int DBG>
-__device__ __forceinline__ void g5_stamp_lds(unsigned char* smw, int kind, int i, int thread) {
-  if constexpr ((DBG & 8) != 0)
-    if (threadIdx.x == thread && i < GW_NSTAMP)
-      reinterpret_cast<unsigned long long*>(smw + G5_STL)[(kind - 1) * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
-}
-template <int DBG>
-__device__ __forceinline__ void g5_stamp_flush(const GateWsArgs& a, const unsigned char* smw, int kind, int n) {
-  if constexpr ((DBG & 8) != 0) {
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(smw + G5_STL) + (kind - 1) * GW_NSTAMP;
-    for (int i = threadIdx.x & 63; i < n && i < GW_NSTAMP; i += 64)
-      a.stamps[((size_t)blockIdx.x * 4 + kind) * GW_NSTAMP + i] = src[i];
-  }
-}
-
-// The lane's row of 32-row block j (T >= 32: at most one utterance boundary per block)
-struct G5Row {
-  int m, bb, t, tvb;
-  __device__ __forceinline__ void init(const GateWsArgs& a, const int* tvt, int m0) {
-    m = m0;
-    bb = (int)((float)m * a.invT);
-    t = m - bb * a.T;
-    if (t < 0) {
-      --bb;
-      t += a.T;
-    } else if (t >= a.T) {
-      ++bb;
-      t -= a.T;
-    }
-    tvb = tvt[min(bb, a.B - 1)];
-  }
-  __device__ __forceinline__ void next(const GateWsArgs& a, const int* tvt) {
-    m += G5_BR;
-    t += G5_BR;
-    const bool wrap = t >= a.T;
-    t = wrap ? t - a.T : t;
-    bb += wrap ? 1 : 0;
-    tvb = tvt[min(bb, a.B - 1)];
-  }
-  // LDS byte offsets of the three tap rows of block j: ring row (8 + 32 j + fr + (tap - 1) dil) mod 160, or the zero
-  // row; plus this lane's 16-B K half
-  __device__ __forceinline__ void bases(const GateWsArgs& a, int j, int fr, int fk, int base[3]) const {
-    const bool row_ok = m < a.M;
-    const int r0 = (G5_BR * j) % G5_RROWS + GW_HALO + fr;  // < 160 + 39
-#pragma unroll
-    for (int tap = 0; tap < 3; ++tap) {
-      const int tp = t + (tap - 1) * a.dil;
-      const bool ok = row_ok && tp >= 0 && tp < tvb;
-      int rr = r0 + (tap - 1) * a.dil;  // in [0, 160 + 47)
-      rr = rr >= G5_RROWS ? rr - G5_RROWS : rr;
-      base[tap] = (ok ? rr * G5_STRIDE : G5_ZERO) + fk * 16;
-    }
-  }
-};
-
-template <bool BF, int DBG>
-__global__ __launch_bounds__(GW_NT, 1) void gate_ws32_kernel(GateWsArgs a) {
-  using O = Op16<BF>;
-  extern __shared__ __align__(16) unsigned char smw[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int pair = wave & 3, kh = wave >> 2;
-  const int fr = lane & 31, fk = lane >> 5;  // the lane's row of the block (B operand and output), its K half
-
-  const int b = blockIdx.x, x = b & 7, j = b >> 3;
-  int type, part;
-  if (j < 30) {
-    type = j % 6;
-    part = x * 5 + j / 6;
-  } else {
-    const int s = (j - 30) * 8 + x;
-    if (s >= 12) return;
-    type = s % 6;
-    part = 40 + s / 6;
-  }
-  const int nblk = (a.M + G5_BR - 1) / G5_BR;
-  const int blk0 = (int)((int64_t)part * nblk / GW_PARTS);
-  const int nsub = (int)((int64_t)(part + 1) * nblk / GW_PARTS) - blk0;
-  if (nsub <= 0) return;
-  const int r_begin = blk0 * G5_BR;
-  const int r_end = min(a.M, r_begin + nsub * G5_BR);
-
-  // the pair's 16 channels ch0 .. ch0 + 15: packed gate columns ng .., filter columns nf ..
-  const int q = 2 * type + (pair >> 1), h = pair & 1;
-  const int ng = 64 * q + 16 * h, nf = ng + 32;
-  const int ch0 = 32 * q + 16 * h;
-
-  {
-    int* tvt = reinterpret_cast<int*>(smw + G5_TVT);
-    for (int i = tid; i < a.B; i += GW_NT) tvt[i] = a.tv ? min(a.T, a.tv[i] * a.tv_mul) : a.T;
-  }
-  for (int i = tid; i < G5_STRIDE / 16; i += GW_NT)
-    *reinterpret_cast<uint4*>(smw + G5_ZERO + i * 16) = make_uint4(0, 0, 0, 0);
-  const int* tvt = reinterpret_cast<const int*>(smw + G5_TVT);
-  unsigned char* const part_buf = smw + G5_PART + pair * 4096 + lane * 16;  // + (k & 1) * 16384 + i * 1024
-
-  half8 w[G5_KH];
-  auto load_w = [&]() __attribute__((always_inline)) {
-    const f16* wb = a.W + g5_frag_index(type, pair, kh, 0) + lane * 8;
-#pragma unroll
-    for (int s = 0; s < G5_KH; ++s) w[s] = *reinterpret_cast<const half8*>(wb + (size_t)s * 512);
-  };
-  // this wave's 36 K-steps of one block onto acc (K-step ks: tap ks / 24, channels 16 (ks % 24) ..): the B fragments
-  // read four K-steps ahead into five register sets, one scheduling segment per K-step (as gate_ws's kloop)
-  auto kloop = [&](const int base[3], int s_off, floatx16& acc) __attribute__((always_inline)) {
-    half8 av[5];
-    auto rd = [&](int s) __attribute__((always_inline)) {
-      const int ks = s_off + s;
-      return *reinterpret_cast<const half8*>(smw + base[ks / 24] + (ks % 24) * 32);
-    };
-#pragma unroll
-    for (int s = 0; s < 4; ++s) av[s] = rd(s);
-#pragma unroll
-    for (int s = 0; s < G5_KH; ++s) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (s + 4 < G5_KH) av[(s + 4) % 5] = rd(s + 4);
-      if constexpr (!(DBG & 2)) acc = O::mfma32(w[s], av[s % 5], acc);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  if (kh == 0) {
-    // ------------------------------------------------------------------ first waves: K-steps 0..35 + ring DMAs
-    const u32x4 dx = gw_desc(a.X, (int64_t)a.M * GW_C * 2);
-    // group g = input rows r_begin - 8 + 32 g .. + 31 into slot g % 5: 24.5 pieces round robin over the four first
-    // waves (piece p = pair + 4 v; pair 0 issues 7, the last of them the half piece on lanes 0..31). A lane's unit u of
-    // piece p -> row u / 49 of the group, 16-B chunk u % 49 (48: the row's padding slot, read as nothing)
-    constexpr int PV = 7;
-    uint32_t pc[PV];
-#pragma unroll
-    for (int v = 0; v < PV; ++v) {
-      const int u = (pair + 4 * v) * 64 + lane;
-      const int r = u / 49, c = u - r * 49;
-      pc[v] = c < 48 ? (uint32_t)(r * GW_C * 2 + c * 16) : GW_OOR;
-    }
-    const bool seven = pair == 0;
-    auto issue = [&](int g) __attribute__((always_inline)) {
-      const uint32_t base = (uint32_t)((r_begin - GW_HALO + g * 32) * (GW_C * 2));  // (negative: out of range)
-      unsigned char* dst = smw + (g % G5_NG) * G5_GBYTES + pair * 1024;
-#pragma unroll
-      for (int v = 0; v < PV - 1; ++v) gw_dma(dx, base + pc[v], dst + v * 4096);
-      if (seven && lane < 32) gw_dma(dx, base + pc[PV - 1], dst + (PV - 1) * 4096);
-    };
-    issue(0);
-    issue(1);
-    load_w();
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0) through the builtin, so the compiler knows W has landed too
-    issue(2);
-    issue(3);
-    issue(4);
-    G5Row row;
-    row.init(a, tvt, r_begin + fr);
-    gw_barrier();
-    // Block k reads groups k and k + 1. Group g's slot held group g - 5, whose last reader (block g - 5, the second
-    // wave) finished in step g - 4: group g is issued at the start of step g - 3 (k >= 2: group k + 3), two steps
-    // before its first reader (block g - 1, this wave). At the end of step k block k + 1's groups (up to k + 2) must
-    // have landed: younger than them are groups 3 and 4 after step 0, group 4 after step 1, group k + 3 after step k
-    auto step = [&](int k) __attribute__((always_inline)) {
-      if (k >= 2) issue(k + 3);
-      int base[3];
-      row.bases(a, k, fr, fk, base);
-      floatx16 acc = {};
-      kloop(base, 0, acc);
-      unsigned char* pb = part_buf + (k & 1) * 16384;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        *reinterpret_cast<floatx4*>(pb + i * 1024) = floatx4{acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]};
-      row.next(a, tvt);
-      g5_stamp_lds<DBG>(smw, 1, k, 0);
-      if (k == 0) {
-        if (seven) gw_vmwait<2 * PV>(); else gw_vmwait<2 * (PV - 1)>();
-      } else {
-        if (seven) gw_vmwait<PV>(); else gw_vmwait<PV - 1>();
-      }
-      g5_stamp_lds<DBG>(smw, 2, k, 0);
-      gw_barrier();
-    };
-    for (int k = 0; k < nsub; ++k) step(k);
-    gw_barrier();  // step nsub: the second waves finish block nsub - 1
-    gw_vmwait<0>();
-    if (wave == 0) {
-      g5_stamp_flush<DBG>(a, smw, 1, nsub);
-      g5_stamp_flush<DBG>(a, smw, 2, nsub);
-    }
-  } else {
-    // ------------------------------------------------------------------ second waves: K-steps 36..71 + gate epilogue
-    // Step k (1 <= k <= nsub): the MFMAs of block k - 1 on its partial sums, then its gate epilogue (conditioner
-    // projection loaded in step k - 1) and store; step k < nsub also loads block k's conditioner projection.
-    const __amdgpu_buffer_rsrc_t rcp =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.cp), (short)0, a.M * a.ld_cp * 2, GW_CFG);
-    const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y, (short)0, a.M * a.ldy * 2, GW_CFG);
-    gw_stamp<DBG>(a, 0);
-    load_w();
-    // the lane's channels: group A ch0 + 4 fk .. + 3 (accumulators 0..3 gate, 8..11 filter), group B ch0 + 8 + 4 fk
-    // (4..7, 12..15)
-    // (their biases are read from LDS in the epilogue: 16 VGPRs held for the whole loop left too few for the K-loop's
-    // read-ahead). Bias of packed column 128 type + i at G5_BIAS + 4 i
-    {
-      float* bl = reinterpret_cast<float*>(smw + G5_BIAS);
-      for (int i = tid - 256; i < 128; i += 256) bl[i] = a.bias[128 * type + i];
-    }
-    const float* bl = reinterpret_cast<const float*>(smw + G5_BIAS) - 128 * type;
-    auto load_cp = [&](int blk, GwH4* dst) __attribute__((always_inline)) {
-      const uint32_t vo = (uint32_t)(r_begin + blk * G5_BR + fr) * (uint32_t)(a.ld_cp * 2);  // rows past M read 0
-      dst[0].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (ng + 4 * fk) * 2, 0, 0));
-      dst[1].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (ng + 8 + 4 * fk) * 2, 0, 0));
-      dst[2].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (nf + 4 * fk) * 2, 0, 0));
-      dst[3].u = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rcp, vo + (nf + 8 + 4 * fk) * 2, 0, 0));
-    };
-    GwH4 c0[4], c1[4];
-    G5Row row;
-    row.init(a, tvt, r_begin + fr);
-    gw_stamp<DBG>(a, 1);
-    gw_barrier();
-    __builtin_amdgcn_s_setprio(1);
-    gw_stamp<DBG>(a, 2);
-    auto epilogue = [&](int blk, const GwH4* cp, const floatx16& acc) __attribute__((always_inline)) {
-      GwH4 pa, pb;
-      const float4 bgA = *reinterpret_cast<const float4*>(bl + ng + 4 * fk);
-      const float4 bgB = *reinterpret_cast<const float4*>(bl + ng + 8 + 4 * fk);
-      const float4 bfA = *reinterpret_cast<const float4*>(bl + nf + 4 * fk);
-      const float4 bfB = *reinterpret_cast<const float4*>(bl + nf + 8 + 4 * fk);
-      const float bga[4] = {bgA.x, bgA.y, bgA.z, bgA.w}, bgb[4] = {bgB.x, bgB.y, bgB.z, bgB.w};
-      const float bfa[4] = {bfA.x, bfA.y, bfA.z, bfA.w}, bfb[4] = {bfB.x, bfB.y, bfB.z, bfB.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr ((DBG & 4) != 0) {
-          pa.h[i] = (f16)(acc[i] + acc[8 + i]);
-          pb.h[i] = (f16)(acc[4 + i] + acc[12 + i]);
-        } else {
-          pa.h[i] = O::enc_lo(gate_act(acc[i] + bga[i] + O::dec(cp[0].h[i]), acc[8 + i] + bfa[i] + O::dec(cp[2].h[i])));
-          pb.h[i] = O::enc_lo(gate_act(acc[4 + i] + bgb[i] + O::dec(cp[1].h[i]), acc[12 + i] + bfb[i] + O::dec(cp[3].h[i])));
-        }
-      }
-      const int m = r_begin + blk * G5_BR + fr;
-      const uint32_t vo = m < r_end ? (uint32_t)m * (uint32_t)(a.ldy * 2) + (uint32_t)(ch0 + 4 * fk) * 2 : GW_OOR;
-      buffer_store_b64(pa.u, ry, vo, a.wt);
-      buffer_store_b64(pb.u, ry, vo == GW_OOR ? GW_OOR : vo + 16, a.wt);
-    };
-    auto mfma_blk = [&](int blk, floatx16& acc) __attribute__((always_inline)) {
-      int base[3];
-      row.bases(a, blk, fr, fk, base);
-      const unsigned char* pb = part_buf + (blk & 1) * 16384;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(pb + i * 1024);
-        acc[4 * i] = v[0];
-        acc[4 * i + 1] = v[1];
-        acc[4 * i + 2] = v[2];
-        acc[4 * i + 3] = v[3];
-      }
-      kloop(base, G5_KH, acc);
-      row.next(a, tvt);
-    };
-    auto end_step = [&](int k) __attribute__((always_inline)) {
-      g5_stamp_lds<DBG>(smw, 3, k, 256);
-      gw_barrier();
-      gw_stamp<DBG>(a, 3 + k);
-    };
-    // step k (1 <= k < nsub): cp(k) into ls, MFMAs + epilogue of block k - 1 from es
-    auto steady = [&](int k, GwH4* ls, const GwH4* es) __attribute__((always_inline)) {
-      load_cp(k, ls);
-      floatx16 acc;
-      mfma_blk(k - 1, acc);
-      epilogue(k - 1, es, acc);
-      end_step(k);
-    };
-    load_cp(0, c0);
-    end_step(0);
-    int k = 1;
-    for (; k + 1 < nsub; k += 2) {  // k odd: loads into c1, epilogue from c0; then the even step
-      steady(k, c1, c0);
-      steady(k + 1, c0, c1);
-    }
-    if (k < nsub) steady(k++, c1, c0);
-    {  // step nsub: block nsub - 1 from set (nsub - 1) % 2
-      floatx16 acc;
-      mfma_blk(nsub - 1, acc);
-      if ((nsub - 1) & 1) epilogue(nsub - 1, c1, acc); else epilogue(nsub - 1, c0, acc);
-      end_step(nsub);
-    }
-    if (wave == 4) g5_stamp_flush<DBG>(a, smw, 3, nsub + 1);
-  }
-}
-
-// W (packed [768][1152]) -> gate_ws32 fragment order (g5_frag_index): lane l of fragment (c, p, kh, s) holds
-// W[n][16 (36 kh + s) + 8 (l / 32) ..], n = ng + l % 32 for l % 32 < 16, else nf + l % 32 - 16
-__global__ void gate_ws32_pack_kernel(const f16* __restrict__ W, f16* __restrict__ Wf) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= GW_N * GW_K / 8) return;
-  const int lane = i & 63;
-  int r = i >> 6;
-  const int s = r % G5_KH;
-  r /= G5_KH;
-  const int kh = r & 1;
-  r >>= 1;
-  const int p = r & 3, c = r >> 2;
-  const int ng = 64 * (2 * c + (p >> 1)) + 16 * (p & 1), l32 = lane & 31;
-  const int n = l32 < 16 ? ng + l32 : ng + 32 + (l32 - 16);
-  const int k = 16 * (G5_KH * kh + s) + 8 * (lane >> 5);
-  *reinterpret_cast<uint4*>(Wf + (size_t)i * 8) = *reinterpret_cast<const uint4*>(W + (size_t)n * GW_K + k);
-}
-
-int gate_ws32_pack(const f16* W, int ldw, f16* Wf, hipStream_t s) {
-  SVC_REQUIRE(ldw == GW_K && ((uintptr_t)W & 15) == 0 && ((uintptr_t)Wf & 15) == 0, "gate_ws32_pack: ldw %d", ldw);
-  hipLaunchKernelGGL(gate_ws32_pack_kernel, dim3(cdiv(GW_N * GW_K / 8, 256)), dim3(256), 0, s, W, Wf);
-  SVC_LAUNCH_CHECK();
-  return SVC_OK;
-}
-
-bool gate_ws32_fits(const ConvGemmArgs& a, const EpiArgs& e) {
-  return a.Wfrag32 && a.T_out >= G5_BR && gate_ws_fits_shape(a, e);
-}
-
-int gate_ws32(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
-  SVC_REQUIRE(gate_ws32_fits(a, e), "gate_ws32: not the DiffSVC dilated-conv gate shape");
-  SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.Wfrag32 & 15) == 0 && ((uintptr_t)e.cp & 7) == 0 &&
-                  ((uintptr_t)e.y16 & 7) == 0 && ((uintptr_t)e.bias & 15) == 0,
-              "gate_ws32: alignment");
-  const int M = a.B * a.T_out;
-  if (M == 0) return SVC_OK;
-  static const int dbg = getenv("SVC_GWS_DBG") ? atoi(getenv("SVC_GWS_DBG")) : 0;  // (diagnostics, read once)
-  GateWsArgs g{a.X, a.Wfrag32, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
-               1.0f / (float)a.T_out, gate_ws_stamps, store_write_through()};
-  const void* fn = a.bf16 ? (const void*)gate_ws32_kernel<true, 0> : (const void*)gate_ws32_kernel<false, 0>;
-  if (!a.bf16 && gate_ws_stamps) {
-    SVC_REQUIRE(a.B <= 256, "gate_ws32 stamps: B <= 256");
-    fn = (const void*)gate_ws32_kernel<false, 8>;
-  } else if (!a.bf16 && dbg == 2) {
-    fn = (const void*)gate_ws32_kernel<false, 2>;
-  } else if (!a.bf16 && dbg == 4) {
-    fn = (const void*)gate_ws32_kernel<false, 4>;
-  }
-  if (int st = ensure_dyn_lds(fn, G5_LDS)) return st;
-  const int tok = prof_begin("gate_ws32<32x128>", 2.0 * M * (double)GW_N * GW_K, 0.0, s);
-  void* args[] = {&g};
-  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3(GW_GRID), dim3(GW_NT), args, G5_LDS, s));
-  prof_end(tok, s);
-  SVC_LAUNCH_CHECK();
-  return SVC_OK;
-}
 
 }  // namespace svc

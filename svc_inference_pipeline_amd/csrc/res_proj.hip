@@ -52,7 +52,6 @@ struct ResProjArgs {
   int M;
   int lanes;          // row lanes = gridDim.x / 2 (each lane's two workgroups take the two halves of N)
   int iters;          // tiles per workgroup: ceil(ceil(M / 16) / lanes)
-  int wt;             // write-through hi / lo stores (store_write_through)
 };
 
 // LDS images, 16-B chunks: g row r (< 16) chunk q (< 48) at r * 48 + (q ^ r); hi / lo row r chunk q (< 24) at
@@ -221,8 +220,8 @@ __global__ __launch_bounds__(RP_NT, 1) void res_proj_kernel(ResProjArgs p) {
     }
     const int row = (rlane + t * p.lanes) * RP_ROWS + fr;
     const uint32_t vo = (uint32_t)row * (RP_C * 2) + (uint32_t)(n0 + 4 * fk) * 2;
-    buffer_store_b64(ph.u, sh, vo, p.wt);
-    buffer_store_b64(pl.u, sl, vo, p.wt);
+    buffer_store_b64(ph.u, sh, vo);
+    buffer_store_b64(pl.u, sl, vo);
     __builtin_amdgcn_sched_barrier(0);
   }
   rp_vmwait<0>();  // (the remaining DMAs of tiles past the end land before the workgroup's LDS is released)
@@ -276,15 +275,13 @@ int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, c
   int lanes = lanes_cap > 0 ? lanes_cap : (lanes_cap == -2 ? ncu / 2 : ncu * 3 / 8);
   lanes = std::max(8, std::min(lanes, (int)round_up(tiles, 8)));
   lanes = (int)round_up(lanes, 8);
-  ResProjArgs a{g, Wf, bias, sub, add, div, hi, lo, M, lanes, cdiv(tiles, lanes), store_write_through()};
+  ResProjArgs a{g, Wf, bias, sub, add, div, hi, lo, M, lanes, cdiv(tiles, lanes)};
   // ring depth 3 (two tiles in flight): 4 / 5 slots measured no faster alone or in the sampler (r03k, two sampler
-  // streams, where the projection had to leave LDS for the other stream's gate GEMM), 2 slots 4 % slower end to end
-  // (r03o). SVC_RP_DEPTH (4 / 5) for A/B runs with one stream
-  static const int depth = getenv("SVC_RP_DEPTH") ? atoi(getenv("SVC_RP_DEPTH")) : 3;  // (read once)
-  const void* fn = bf16 ? (const void*)res_proj_kernel<true, 3> : (const void*)res_proj_kernel<false, 3>;
-  if (!bf16 && depth == 4) fn = (const void*)res_proj_kernel<false, 4>;
-  if (!bf16 && depth == 5) fn = (const void*)res_proj_kernel<false, 5>;
-  const int lds = (bf16 || (depth != 4 && depth != 5) ? 3 : depth) * RP_SLOT;
+  // streams; r04n, one stream: 882.3 / 880.9 and 876.8 / 878.3 against 879.6 / 881.3 audio-s/s), 2 slots 4 % slower end
+  // to end (r03o)
+  constexpr int depth = 3;
+  const void* fn = bf16 ? (const void*)res_proj_kernel<true, depth> : (const void*)res_proj_kernel<false, depth>;
+  const int lds = depth * RP_SLOT;
   if (int st = ensure_dyn_lds(fn, lds)) return st;
   const int tok = prof_begin("res_proj<16x192>", 2.0 * M * RP_C * RP_C, (double)M * RP_C * 10.0, s);
   void* args[] = {&a};

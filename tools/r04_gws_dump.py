@@ -1,4 +1,4 @@
-"""(debug) gate outputs of conv_gemm4 (24) and a gate_ws form (argv[1]: 40 gate_ws, 41 gate_ws32; default 40) on the
+"""(debug) gate outputs of conv_gemm4 (24) and gate_ws (argv[1], default 40) on the
 same synthetic operands, compared element by element (differing elements, max |d|, max difference in f16 units)."""
 import os, subprocess, sys
 import numpy as np
