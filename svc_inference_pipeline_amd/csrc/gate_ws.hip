@@ -197,7 +197,8 @@ template <bool BF, int DBG, int GW_KA = GW_KA_DEF>
 __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
   using O = Op16<BF>;
   constexpr int GW_KB = GW_KS - GW_KA;
-  static_assert(GW_KA >= GW_KB && GW_KB >= 4, "K split: the weight arrays are sized for the first wave");
+  static_assert(GW_KA >= GW_KB && GW_KB >= 4, "K split: the weight arrays are sized for the first wave; the epilogue's 4 "
+                                             "elements need 4 segments");
   extern __shared__ __align__(16) unsigned char smw[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -408,14 +409,17 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       gw_stamp<DBG>(a, 3 + k);
     };
     // steady step k (2 <= k < nsub): cp(k) into LS, MFMAs of block k - 1 with the epilogue of block k - 2 (cp from ES)
-    // in their K-step segments: element i in segment 4 i + 3, the store in the last
+    // in their K-step segments: element i at the end of segment (i + 1) GW_KB / 4 - 1 (every element, for any split),
+    // the store after the last
     auto steady = [&](int k, GwH4* ls, const GwH4* es) __attribute__((always_inline)) {
       load_cp(k, ls);
       floatx4 ag, af;
       const floatx4 eg = pg, ef = pf;
       GwH4 pk;
       auto hook = [&](int s) __attribute__((always_inline)) {
-        if (s % 4 == 3) pk.h[s / 4] = gate_el(s / 4, es, eg, ef);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (s == (i + 1) * GW_KB / 4 - 1) pk.h[i] = gate_el(i, es, eg, ef);
         if (s == GW_KB - 1) store_blk(k - 2, pk);
       };
       mfma_blk(k - 1, ag, af, hook);
