@@ -234,6 +234,9 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     for (int i = tid; i < a.B; i += GW_NT) tvt[i] = a.tv ? min(a.T, a.tv[i] * a.tv_mul) : a.T;
   }
   for (int i = tid; i < 768 / 16; i += GW_NT) *reinterpret_cast<uint4*>(smw + GW_ZERO + i * 16) = make_uint4(0, 0, 0, 0);
+  // the length table is read by every wave's GwRow::init before the prologue barrier (a 24 / 12 K split, whose second
+  // waves reach it sooner, read it before it was written: a ragged batch differed from conv_gemm4, r04p)
+  __syncthreads();
   const int* tvt = reinterpret_cast<const int*>(smw + GW_TVT);
   unsigned char* const part_buf = smw + GW_PART + pair * 2048;  // + (k & 1) * 8192
 
