@@ -87,7 +87,8 @@ def test_plms100_headline_shape_vs_golden(cfg, B):
     svc_model_inference on the same seeded weights (eps head x 3, so the denoiser's eps carries 80 % of the output's
     norm), conditioning and x_T, one utterance per run (tools/make_goldens_headline.py). The batch holds the golden's
     two utterances (B = 32: repeated, one copy per sampler sub-stream and utterance position) and each is compared:
-    rel-L2 <= 1e-3 on x_0 and on its eps-induced part x_0 - x_0|eps=0 (measured: see the printed line)."""
+    rel-L2 <= 1e-3 on x_0 and on its eps-induced part x_0 - x_0|eps=0 (measured on MI355X, r04p: worst 3.37e-4 at
+    B = 2 and at B = 32)."""
     import headline_golden as HG
     g = np.load(os.path.join(os.path.dirname(__file__), "golden", "plms100_headline.npz"))
     ms = HG.headline_mapper_state(cfg.mapper)
