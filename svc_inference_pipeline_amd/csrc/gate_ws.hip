@@ -8,13 +8,12 @@
 // whole L2 -> LDS bandwidth of a CU (64 B per clock), so its K-loop runs at ~0.4 of the MFMA peak.
 // Here the weights stay put instead:
 //   * a workgroup owns 128 packed columns = 64 output channels, as 4 column sets of 16 gate + 16 filter columns; each set
-//     belongs to a PAIR of waves on one SIMD (waves w and w + 4): wave w holds the set's weights for K-steps 0..21 (tap
-//     0 and the first 320 channels of tap 1), wave w + 4 for K-steps 22..35, as MFMA fragments in VGPRs (2 x 22 / 14 x
-//     half8 = 176 / 112
+//     belongs to a PAIR of waves on one SIMD (waves w and w + 4): wave w holds the set's weights for K-steps 0..23 (taps
+//     0 and 1), wave w + 4 for K-steps 24..35 (tap 2), as MFMA fragments in VGPRs (2 x 24 / 12 x half8 = 192 / 96
 //     registers each: two waves per SIMD), loaded once per launch;
-//   * the workgroup walks its share of the rows in 16-row blocks: in step k the first wave of a pair runs K-steps 0..21
+//   * the workgroup walks its share of the rows in 16-row blocks: in step k the first wave of a pair runs K-steps 0..23
 //     of block k and hands its two f32 accumulators to its partner through LDS, which continues them over K-steps
-//     22..35 for block k - 1 (the partial sums are the partner's MFMA C operand, so the K order is one sequential chain,
+//     24..35 for block k - 1 (the partial sums are the partner's MFMA C operand, so the K order is one sequential chain,
 //     exactly conv_gemm4's) and applies the gate in registers; one workgroup barrier per step;
 //   * the input rows come through a ring of 160 rows in LDS, DMA'd in 32-row groups (25 KiB) once each: the three taps
 //     of a block read its rows at offsets -dil, 0, +dil, so no row is fetched twice, and a group is issued 5 steps
@@ -45,11 +44,11 @@ constexpr int GW_C = 384;             // channels per tap
 constexpr int GW_N = 768;             // packed output columns (gate | filter per 64-column block)
 constexpr int GW_K = 3 * GW_C;        // 1152 = 36 K-steps of 32
 constexpr int GW_KS = 36;             // K-steps of 32
-constexpr int GW_KA_DEF = 22;         // K-steps of a pair's first wave (0..21); its partner takes 22..35. Unequal on
-                                      // purpose: the partner also runs the gate epilogue (18 / 18: partner 2248 vs
-                                      // 1672 cycles per step, r04m stamps). 18 / 20 / 22: 880.7 / 880.5 / 890.2 and
-                                      // 878.1 / 879.7 / 891.0 audio-s/s (r04n, alternating). SVC_GWS_KA (20 / 23 / 24)
-                                      // for A/B runs
+constexpr int GW_KA_DEF = 24;         // K-steps of a pair's first wave (0..23: taps 0 and 1); its partner takes 24..35
+                                      // (tap 2) and also runs the gate epilogue. 18 / 18 left the partner at 2248 vs
+                                      // 1672 cycles per step (r04m stamps); end to end the split barely matters:
+                                      // 20 / 22 / 23 / 24: 884.0 / 883.9 / 883.3 / 885.9 and 885.2 / 883.6 / 884.0 /
+                                      // 886.6 audio-s/s (r04p, alternating). SVC_GWS_KA (18 / 22) for A/B runs
 constexpr int GW_HALO = 8;            // largest tap shift (dilation 8): ring row 0 = input row r_begin - 8
 constexpr int GW_GR = 32;             // rows per DMA group
 constexpr int GW_NG = 5;              // ring slots (groups): 160 rows
@@ -519,9 +518,8 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   if (!a.bf16 && gate_ws_stamps) fn = (const void*)gate_ws_kernel<false, 8>;
   else if (!a.bf16 && dbg == 2) fn = (const void*)gate_ws_kernel<false, 2>;
   else if (!a.bf16 && dbg == 4) fn = (const void*)gate_ws_kernel<false, 4>;
-  else if (!a.bf16 && ka == 20) fn = (const void*)gate_ws_kernel<false, 0, 20>;
-  else if (!a.bf16 && ka == 23) fn = (const void*)gate_ws_kernel<false, 0, 23>;
-  else if (!a.bf16 && ka == 24) fn = (const void*)gate_ws_kernel<false, 0, 24>;
+  else if (!a.bf16 && ka == 18) fn = (const void*)gate_ws_kernel<false, 0, 18>;
+  else if (!a.bf16 && ka == 22) fn = (const void*)gate_ws_kernel<false, 0, 22>;
   if (int st = ensure_dyn_lds(fn, GW_LDS)) return st;
   const int tok = prof_begin("gate_ws<16x128>", 2.0 * M * (double)GW_N * GW_K, 0.0, s);
   void* args[] = {&g};

@@ -23,3 +23,18 @@ for r in 1 2 3; do
     python3 -c "import json; d=json.loads(open('$O/b_$v.json').read().strip().splitlines()[-1]); k=d['kernels']; print('gate_ws=$v', d['value'], d['ms_per_step'], {kk: round(vv['ms_per_step'],2) for kk,vv in k.items() if 'dilated' in kk or 'outproj' in kk})"
   done
 done
+# HIP-event vs rocprof per-launch time of the same gate_ws launches: batched events (one pair around
+# 10 launches) and per-launch event pairs (as bench.py's live profile), each also under rocprofv3 --kernel-trace
+for mode in batched perlaunch; do
+  PL=""; [ $mode = perlaunch ] && PL=1
+  SVC_BENCH_PERLAUNCH=$PL GEMM_BENCH_WARM=1 GEMM_BENCH_TORCH=0 GEMM_BENCH_CUSTOM="29984,768,384,3,1" timeout -k 10 120 python3 tools/gemm_bench.py 40 > $O/rec_$mode.txt 2>&1 || exit $?
+  grep -v amdgpu $O/rec_$mode.txt | sed "s/^/events $mode: /"
+  SVC_BENCH_PERLAUNCH=$PL GEMM_BENCH_WARM=1 GEMM_BENCH_TORCH=0 GEMM_BENCH_CUSTOM="29984,768,384,3,1" timeout -k 10 180 rocprofv3 --kernel-trace --stats -f csv -d $O/rp_$mode -o run -- python3 tools/gemm_bench.py 40 > $O/rec_rp_$mode.txt 2>&1 || exit $?
+  grep -v amdgpu $O/rec_rp_$mode.txt | grep custom | sed "s/^/events under rocprof $mode: /"
+  python3 - $O/rp_$mode <<'PY'
+import csv, glob, sys
+f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
+d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(f)) if "gate_ws_kernel" in r["Kernel_Name"]]
+print(f"rocprof trace: {len(d)} gate_ws dispatches, last 10 avg {sum(d[-10:]) / 10 / 1000:.2f} us, all avg {sum(d) / len(d) / 1000:.2f} us")
+PY
+done
