@@ -85,7 +85,6 @@ struct GateWsArgs {
   int tv_mul, B;
   float invT;
   unsigned long long* stamps;  // diagnostics (SVC_GWS_STAMPS, svc_gemm_bench only): s_memtime per workgroup and step
-  int prio;           // static priority 1 for: 0 the second waves (default), 1 the first waves, 2 none (SVC_GWS_PRIO, A/B)
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -314,7 +313,6 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     GwRow row;
     row.init(a, tvt, r_begin + fr);
     gw_barrier();  // groups 0 and 1, the zero row and the length table
-    if (a.prio == 1) __builtin_amdgcn_s_setprio(1);
     // Block j reads groups j / 2 .. (j + 1) / 2, so group G's last reader is block 2 G + 1 (the second wave, step
     // 2 G + 2). Group g = (k + 7) / 2 >= 5 is issued at the start of odd steps k >= 3, into the slot of group g - 5,
     // whose last reader finished in step k - 1; its first reader is block 2 g - 1, 5 steps later. At the end of step k,
@@ -373,7 +371,9 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     row.init(a, tvt, r_begin + fr);
     gw_stamp<DBG>(a, 1);
     gw_barrier();  // (pairs with the first waves' prologue barrier)
-    if (a.prio == 0) __builtin_amdgcn_s_setprio(1);
+    // (priority 1 on the first waves instead, or on neither: 903.2 / 900.5 / 902.6 and 902.4 / 902.1 / 904.0 against
+    // 908.1 / 908.0 / 907.3 audio-s/s, r04s)
+    __builtin_amdgcn_s_setprio(1);
     gw_stamp<DBG>(a, 2);
     // gate of the lane's element i (conv_gemm4's DIRECT epilogue arithmetic, same order), and the block's store (rows
     // past the part are dropped)
@@ -512,9 +512,8 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   const int M = a.B * a.T_out;
   if (M == 0) return SVC_OK;
   static const int dbg = getenv("SVC_GWS_DBG") ? atoi(getenv("SVC_GWS_DBG")) : 0;  // (diagnostics, read once)
-  static const int prio = getenv("SVC_GWS_PRIO") ? atoi(getenv("SVC_GWS_PRIO")) : 0;     // (A/B runs, read once)
   GateWsArgs g{a.X, a.Wfrag, e.bias, e.cp, e.ld_cp, e.y16, e.ldy16, M, a.T_out, a.tap_mul, a.tv, a.tv_mul, a.B,
-               1.0f / (float)a.T_out, gate_ws_stamps, prio};
+               1.0f / (float)a.T_out, gate_ws_stamps};
   // diagnostics instances (fp16 only): 2 no MFMAs, 4 no gate arithmetic, 8 step stamps (SVC_GWS_STAMPS)
   static const int ka = getenv("SVC_GWS_KA") ? atoi(getenv("SVC_GWS_KA")) : GW_KA_DEF;  // (A/B runs, read once)
   const void* fn = a.bf16 ? (const void*)gate_ws_kernel<true, 0> : (const void*)gate_ws_kernel<false, 0>;
