@@ -189,6 +189,9 @@ svc_status svc_op_amp_conv(const float* x, int B, int L, int C, const float* alp
 /* Activation1d(SnakeBeta, logscale): x f32 [B*L][C] -> y f32 [B*L][C] */
 svc_status svc_op_activation1d(const float* x, int B, int L, int C, const float* alpha_log, const float* beta_log,
                                const float* filt12, float* y, void* stream);
+/* the same on an f16 input x16 [B*L][C] (binary16; the AMPBlock1 convs1 outputs in the product path) */
+svc_status svc_op_activation1d_x16(const void* x16, int B, int L, int C, const float* alpha_log, const float* beta_log,
+                                   const float* filt12, float* y, void* stream);
 /* attention on f32 q,k,v [B*L][D] (already projected; scaled inside by dh^-1/4 each) -> out f32 [B*L][D] */
 svc_status svc_op_attention(const float* q, const float* k, const float* v, int B, int L, int D, float* out,
                             void* stream);

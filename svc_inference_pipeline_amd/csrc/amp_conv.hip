@@ -22,6 +22,18 @@
 
 namespace svc {
 
+constexpr int AMP_NT = 256;
+
+// Activation run length for an image of `rows` rows: the shortest multiple of the row block that gives every
+// (channel group, run) task to its own thread (one exposed load latency per thread). The image is allocated for
+// whole runs (nruns * RUN rows), so that no run is partial: a partial run would take the edge form of the channel-pair
+// activation, and its lanes would make their whole wave run both forms before the barrier.
+__host__ __device__ constexpr int amp_run_len(int C, int rows) {
+  const int blk = C <= 48 ? 4 : 8, ngrp = C <= 48 ? C / 2 : C;
+  const int nr_fit = AMP_NT / ngrp > 1 ? AMP_NT / ngrp : 1;
+  return ((rows + nr_fit - 1) / nr_fit + blk - 1) / blk * blk;
+}
+
 template <int C>
 struct AmpCfg {
   static constexpr int BT = C <= 48 ? 256 : 128;    // output rows per workgroup (halo share of the act work)
@@ -29,14 +41,63 @@ struct AmpCfg {
   static constexpr int LDA = C == 24 ? 24 : C + 8;  // f16 row stride: 48/112/208 B, conflict-free fragment reads
   static constexpr int ROWS = BT + 2 * MAXP;
   static constexpr int FN = (C + 15) / 16;          // 16-column fragments
-  static constexpr int A_BYTES = ROWS * LDA * 2;
+  static constexpr int A_BYTES = (ROWS + amp_run_len(C, ROWS)) * LDA * 2;  // whole runs of the largest image
   // the epilogue works in registers (operand-swapped MFMAs, see below), so LDS holds only the activation image:
   // C = 48: 34 KiB -> 4 workgroups per CU (3 with the former 48 KiB C staging), C = 24: 15 KiB
   static constexpr int LDS = A_BYTES;
   static_assert(C % 8 == 0 && LDA % 8 == 0, "16-B fragment rows");
 };
 
-constexpr int AMP_NT = 256;
+// SnakeBeta of the channel pair (c, c+1) for global rows [rs, re) into the LDS image (row r of the image = global row
+// r0 + r), in blocks of BLK rows on packed f32 ops (snake.h); re - rs is a multiple of BLK. EDGE: the run lies within 6
+// rows of an utterance end: clamped loads, the up-sampled signal's replicate padding at both ends and zero rows outside
+// [0, Lb) (the conv's own zero padding). Other runs take none of these.
+template <typename TX, int BLK, int LDA, bool EDGE>
+__device__ __forceinline__ void amp_act_pair(__amdgpu_buffer_rsrc_t rx, uint32_t xo, uint32_t xs, f16* img, int r0,
+                                             int rs, int re, int Lb, int c, const float (&f)[12],
+                                             const float (&f2)[12], const SnakeCoef2& kc) {
+  auto xl = [&](int t) __attribute__((always_inline)) {
+    if (EDGE) t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
+    return act_load<TX>(rx, xo + (uint32_t)t * xs, 0);
+  };
+  f32x2 s0 = {0.f, 0.f}, sE = {0.f, 0.f};  // s at j = 0 and j = 2Lb-1
+  if (EDGE) {
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      s0 += xl(-3 + a) * f2[11 - 2 * a];
+      sE += xl(Lb - 3 + a) * f2[10 - 2 * a];
+    }
+    s0 = snake2(s0, kc);
+    sE = snake2(sE, kc);
+  }
+  auto s_at = [&](const f32x2* xw, int i, int j) __attribute__((always_inline)) {
+    const f32x2 o = snake_up(xw, i, f2, kc);
+    return EDGE ? (j < 0 ? s0 : (j > 2 * Lb - 1 ? sE : o)) : o;
+  };
+  f32x2 xw[BLK + 10], sw[2 * BLK + 10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) xw[k] = xl(rs - 5 + k);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) sw[i] = s_at(xw, i, 2 * rs - 5 + i);
+  for (int t = rs; t < re; t += BLK) {
+    const uint32_t xrow = xo + (uint32_t)(t + 5) * xs;
+#pragma unroll
+    for (int k = 0; k < BLK; ++k) xw[10 + k] = EDGE ? xl(t + 5 + k) : act_load<TX>(rx, xrow, k * xs);
+#pragma unroll
+    for (int p = 0; p < BLK; ++p) {
+      sw[10 + 2 * p] = s_at(xw, 10 + 2 * p, 2 * t + 5 + 2 * p);
+      sw[11 + 2 * p] = s_at(xw, 11 + 2 * p, 2 * t + 6 + 2 * p);
+      const int row = t + p;
+      f32x2 y = snake_down(sw + 2 * p, f);
+      if (EDGE && (row < 0 || row >= Lb)) y = f32x2{0.f, 0.f};
+      *reinterpret_cast<unsigned*>(img + (row - r0) * LDA + c) = f16x2_sat(y);
+    }
+#pragma unroll
+    for (int k = 0; k < 10; ++k) xw[k] = xw[BLK + k];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) sw[i] = sw[2 * BLK + i];
+  }
+}
 
 // Launch bound: 4 waves per SIMD, under which the compiler keeps the accumulators in the unified VGPR file (C = 24:
 // 79 registers, 6 waves per SIMD; without an occupancy target it split the file into VGPRs + AGPRs at 5 waves).
@@ -64,123 +125,141 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
     constexpr bool PK = C <= 48;
     constexpr int VEC = PK ? 2 : 1, BLK = PK ? 4 : 8;
     using V = ActVec<VEC>;
-    float f[12];
+    float f[12], f2[12];  // f2: the up-sampling taps with its factor 2 (exact)
 #pragma unroll
-    for (int q = 0; q < 12; ++q) f[q] = p.filt[q];
+    for (int q = 0; q < 12; ++q) {
+      f[q] = p.filt[q];
+      f2[q] = 2.0f * f[q];
+    }
     const int ngrp = C / VEC;
     // run length: the shortest multiple of BLK that gives every (channel, run) task to its own thread (one exposed
     // load latency per thread: a run's sliding window prefetches its next block across the whole run)
-    const int nr_fit = max(1, AMP_NT / ngrp);
     // (LDS conflicts, VERDICT r03 item 4: making the activation stores conflict-free by the choice of RUN moved the
     // kernel's conflict share only 0.47 -> 0.41 and no timing, r04q; the rest are the conv phase's fragment reads)
-    const int RUN = ((rows + nr_fit - 1) / nr_fit + BLK - 1) / BLK * BLK;
+    const int RUN = amp_run_len(C, rows);
     const int nruns = (rows + RUN - 1) / RUN;
     using TX = typename std::conditional<X16, f16, float>::type;
     const TX* xb = (X16 ? (const TX*)(const void*)p.x16 : (const TX*)(const void*)p.x) + (int64_t)b * L * C;
-    for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
-      const int cg = task % ngrp, ru = task / ngrp;
-      const int c = cg * VEC;
-      const int rs = t0 - P + ru * RUN;                       // first global row of this run
-      const int re = min(rs + RUN, t0 + CF::BT + P);
-      float as[VEC], ib[VEC];
-#pragma unroll
-      for (int v = 0; v < VEC; ++v) {
-        as[v] = expf(p.alpha_log[c + v]);
-        ib[v] = 1.0f / (expf(p.beta_log[c + v]) + 0.000000001f);
+    if constexpr (PK) {
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<void*>(X16 ? (const void*)p.x16 : (const void*)p.x), (short)0,
+          (int)((int64_t)p.B * L * C * sizeof(TX)), 0x00020000);
+      for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
+        const int cg = task % ngrp, ru = task / ngrp;
+        const int c = cg * 2;
+        const int rs = t0 - P + ru * RUN, re = rs + RUN;  // global rows of this run (whole runs: the image has room)
+        const SnakeCoef2 kc = snake_coef2(p.alpha_log, p.beta_log, c);
+        const uint32_t xo = (uint32_t)(((int64_t)b * L * C + c) * sizeof(TX)), xs = (uint32_t)(C * sizeof(TX));
+        if (rs - 6 < 0 || re + 6 > Lb)
+          amp_act_pair<TX, BLK, CF::LDA, true>(rx, xo, xs, As, t0 - P, rs, re, Lb, c, f, f2, kc);
+        else
+          amp_act_pair<TX, BLK, CF::LDA, false>(rx, xo, xs, As, t0 - P, rs, re, Lb, c, f, f2, kc);
       }
-      auto xload = [&](int t, float* o) {
-        t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
-        V::load(xb + (int64_t)t * C + c, o);
-      };
-      auto snake = [&](float* u) {
+    } else {
+      for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
+        const int cg = task % ngrp, ru = task / ngrp;
+        const int c = cg * VEC;
+        const int rs = t0 - P + ru * RUN;                       // first global row of this run
+        const int re = min(rs + RUN, t0 + CF::BT + P);
+        float ar[VEC], ib[VEC];  // alpha / 2pi: the sine's argument in revolutions (snake.h snake2)
 #pragma unroll
         for (int v = 0; v < VEC; ++v) {
-          u[v] *= 2.0f;
-          const float sn = sin_rev(u[v] * as[v]);
-          u[v] = u[v] + ib[v] * (sn * sn);
+          ar[v] = expf(p.alpha_log[c + v]) * 0.15915494309189535f;
+          ib[v] = 1.0f / (expf(p.beta_log[c + v]) + 0.000000001f);
         }
-      };
-      // s at the two ends of the up-sampled signal (the low-pass filter's replicate padding uses them); only runs
-      // within 6 rows of an utterance end need them (wave-uniform in practice: runs are 32-64 rows)
-      const bool edge = rs - 6 < 0 || re + 6 > Lb;
-      float s0[VEC], sE[VEC];
+        auto xload = [&](int t, float* o) {
+          t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
+          V::load(xb + (int64_t)t * C + c, o);
+        };
+        auto snake = [&](float* u) {
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) s0[v] = sE[v] = 0.f;
-      if (edge) {
+          for (int v = 0; v < VEC; ++v) {
+            const float sn = __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(u[v] * ar[v]));
+            u[v] = u[v] + ib[v] * (sn * sn);
+          }
+        };
+        // s at the two ends of the up-sampled signal (the low-pass filter's replicate padding uses them); only runs
+        // within 6 rows of an utterance end need them (wave-uniform in practice: runs are 32-64 rows)
+        const bool edge = rs - 6 < 0 || re + 6 > Lb;
+        float s0[VEC], sE[VEC];
 #pragma unroll
-      for (int a = 0; a < 6; ++a) {
-        float x0[VEC], x1[VEC];
-        xload(-3 + a, x0);         // j = 0: even, q = 0
-        xload(Lb - 3 + a, x1);     // j = 2Lb-1: odd, q = Lb-1
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          s0[v] += x0[v] * f[11 - 2 * a];
-          sE[v] += x1[v] * f[10 - 2 * a];
-        }
-      }
-      snake(s0);
-      snake(sE);
-      }
-      // s[2tb-5+i] from the window xw[q] = x[tb-5+q] (exact inside [0, 2L-1]), else the end value
-      auto s_at = [&](const float (*xw)[VEC], int i, int j, float* o) {
-        const int odd = (i + 1) & 1;
-        const int base = ((i - 5) >> 1) + 2 + odd;
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) o[v] = 0.f;
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          const float w = f[11 - odd - 2 * a];
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) o[v] += xw[base + a][v] * w;
-        }
-        snake(o);
+        for (int v = 0; v < VEC; ++v) s0[v] = sE[v] = 0.f;
         if (edge) {
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) o[v] = j < 0 ? s0[v] : (j > 2 * Lb - 1 ? sE[v] : o[v]);
-        }
-      };
-      float xw[BLK + 10][VEC], sw[2 * BLK + 10][VEC], xn[BLK][VEC];
+        for (int a = 0; a < 6; ++a) {
+          float x0[VEC], x1[VEC];
+          xload(-3 + a, x0);         // j = 0: even, q = 0
+          xload(Lb - 3 + a, x1);     // j = 2Lb-1: odd, q = Lb-1
 #pragma unroll
-      for (int q = 0; q < 10; ++q) xload(rs - 5 + q, xw[q]);
-#pragma unroll
-      for (int q = 0; q < BLK; ++q) xload(rs + 5 + q, xn[q]);  // first block, in flight during the warm-up
-#pragma unroll
-      for (int i = 0; i < 10; ++i) s_at(xw, i, 2 * rs - 5 + i, sw[i]);
-      for (int t = rs; t < re; t += BLK) {
-#pragma unroll
-        for (int q = 0; q < BLK; ++q)
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) xw[10 + q][v] = xn[q][v];
-        if (t + BLK < re) {  // next block's loads overlap this block's arithmetic
-#pragma unroll
-          for (int q = 0; q < BLK; ++q) xload(t + BLK + 5 + q, xn[q]);
-        }
-#pragma unroll
-        for (int i = 10; i < 2 * BLK + 10; ++i) s_at(xw, i, 2 * t - 5 + i, sw[i]);
-#pragma unroll
-        for (int q = 0; q < BLK; ++q) {
-          const int row = t + q;
-          if (row < re) {
-            float y[VEC];
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) y[v] = 0.f;
-            if (row >= 0 && row < Lb) {
-#pragma unroll
-              for (int kk = 0; kk < 12; ++kk)
-#pragma unroll
-                for (int v = 0; v < VEC; ++v) y[v] += f[kk] * sw[2 * q + kk][v];
-            }
-            V::store(As + (row - (t0 - P)) * CF::LDA + c, y);
+          for (int v = 0; v < VEC; ++v) {
+            s0[v] += x0[v] * f2[11 - 2 * a];
+            sE[v] += x1[v] * f2[10 - 2 * a];
           }
         }
+        snake(s0);
+        snake(sE);
+        }
+        // s[2tb-5+i] from the window xw[q] = x[tb-5+q] (exact inside [0, 2L-1]), else the end value
+        auto s_at = [&](const float (*xw)[VEC], int i, int j, float* o) {
+          const int odd = (i + 1) & 1;
+          const int base = ((i - 5) >> 1) + 2 + odd;
 #pragma unroll
-        for (int q = 0; q < 10; ++q)
+          for (int v = 0; v < VEC; ++v) o[v] = 0.f;
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) xw[q][v] = xw[BLK + q][v];
+          for (int a = 0; a < 6; ++a) {
+            const float w = f2[11 - odd - 2 * a];
 #pragma unroll
-        for (int i = 0; i < 10; ++i)
+            for (int v = 0; v < VEC; ++v) o[v] += xw[base + a][v] * w;
+          }
+          snake(o);
+          if (edge) {
 #pragma unroll
-          for (int v = 0; v < VEC; ++v) sw[i][v] = sw[2 * BLK + i][v];
+            for (int v = 0; v < VEC; ++v) o[v] = j < 0 ? s0[v] : (j > 2 * Lb - 1 ? sE[v] : o[v]);
+          }
+        };
+        float xw[BLK + 10][VEC], sw[2 * BLK + 10][VEC], xn[BLK][VEC];
+#pragma unroll
+        for (int q = 0; q < 10; ++q) xload(rs - 5 + q, xw[q]);
+#pragma unroll
+        for (int q = 0; q < BLK; ++q) xload(rs + 5 + q, xn[q]);  // first block, in flight during the warm-up
+#pragma unroll
+        for (int i = 0; i < 10; ++i) s_at(xw, i, 2 * rs - 5 + i, sw[i]);
+        for (int t = rs; t < re; t += BLK) {
+#pragma unroll
+          for (int q = 0; q < BLK; ++q)
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) xw[10 + q][v] = xn[q][v];
+          if (t + BLK < re) {  // next block's loads overlap this block's arithmetic
+#pragma unroll
+            for (int q = 0; q < BLK; ++q) xload(t + BLK + 5 + q, xn[q]);
+          }
+#pragma unroll
+          for (int i = 10; i < 2 * BLK + 10; ++i) s_at(xw, i, 2 * t - 5 + i, sw[i]);
+#pragma unroll
+          for (int q = 0; q < BLK; ++q) {
+            const int row = t + q;
+            if (row < re) {
+              float y[VEC];
+#pragma unroll
+              for (int v = 0; v < VEC; ++v) y[v] = 0.f;
+              if (row >= 0 && row < Lb) {
+#pragma unroll
+                for (int kk = 0; kk < 12; ++kk)
+#pragma unroll
+                  for (int v = 0; v < VEC; ++v) y[v] += f[kk] * sw[2 * q + kk][v];
+              }
+              V::store(As + (row - (t0 - P)) * CF::LDA + c, y);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 10; ++q)
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) xw[q][v] = xw[BLK + q][v];
+#pragma unroll
+          for (int i = 0; i < 10; ++i)
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) sw[i][v] = sw[2 * BLK + i][v];
+        }
       }
     }
   }
@@ -274,7 +353,8 @@ static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   // the activation image needs BT + 2P rows, not BT + 2 MAXP: sized per launch, C = 48 fits 5 workgroups per CU
   // (instead of 4) for every conv with P <= 15
   const int P = (p.k - 1) / 2 * p.d;
-  const int lds = (CF::BT + 2 * P) * CF::LDA * 2;
+  const int rows = CF::BT + 2 * P, run = amp_run_len(C, rows);
+  const int lds = (rows + run - 1) / run * run * CF::LDA * 2;
   hipLaunchKernelGGL((amp_conv_kernel<C, X16>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, p, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();

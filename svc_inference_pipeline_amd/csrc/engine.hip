@@ -2799,6 +2799,20 @@ svc_status svc_op_activation1d(const float* x, int B, int L, int C, const float*
   return f16_to_f32(y16, y, (int64_t)B * L * C, s);
 }
 
+svc_status svc_op_activation1d_x16(const void* x16, int B, int L, int C, const float* al, const float* be,
+                                   const float* f, float* y, void* stream) {
+  svc_ctx* c;
+  op_ws(&c);
+  TuningScope tuning_scope_(&c->tune);
+  hipStream_t s = (hipStream_t)stream;
+  int st;
+  if ((st = c->ws.reserve(std::max((size_t)B * L * C * 2 + 4096, c->ws.cap)))) return st;
+  c->ws.reset();
+  WS_GET(f16, y16, (size_t)B * L * C);
+  if ((st = activation1d(nullptr, y16, B, L, C, C, al, be, f, s, nullptr, 1, (const f16*)x16))) return st;
+  return f16_to_f32(y16, y, (int64_t)B * L * C, s);
+}
+
 svc_status svc_op_attention(const float* q, const float* k, const float* v, int B, int L, int D, float* out,
                             void* stream) {
   svc_ctx* c;

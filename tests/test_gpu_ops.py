@@ -83,19 +83,25 @@ def test_conv_transpose1d(B, T, Cin, Cout, k, s, variant, tune):
     assert rel_l2(out, ref.numpy()) < 2e-3
 
 
+@pytest.mark.parametrize("x16", [False, True])
 @pytest.mark.parametrize("B,L,C", [(2, 37, 24), (1, 1, 24), (1, 2, 48), (1, 3, 8), (2, 11, 12), (3, 129, 96),
-                                   (1, 300, 768), (2, 64, 40), (2, 257, 48), (2, 700, 1536)])
-def test_activation1d(B, L, C):
+                                   (1, 300, 768), (2, 64, 40), (2, 257, 48), (2, 700, 1536), (3, 1000, 192)])
+def test_activation1d(B, L, C, x16):
+    """f32 input (the generator's residual stream) and f16 input (an AMPBlock1 convs1 output): the reference runs on
+    the same f16-rounded values. L = 700 / 1000 hold runs clear of both utterance ends (the clamp-free form)."""
     from svc_inference_pipeline_amd import weights as W
     g = torch.Generator().manual_seed(2)
     x = torch.randn(B, C, L, generator=g) * 2
+    if x16:
+        x = x.half().float()
     al = torch.randn(C, generator=g) * 0.3
     be = torch.randn(C, generator=g) * 0.3
     f = W.kaiser_sinc_filter1d(0.25, 0.3, 12).view(-1)
     ref = OM.activation1d(x, al, be, f)
     y = torch.empty(B * L, C, device="cuda")
-    xd, ad, bd, fd = dev(_tm(x)), dev(al), dev(be), dev(f)
-    call("svc_op_activation1d", ptr(xd), B, L, C, ptr(ad), ptr(bd), ptr(fd), ptr(y), stream())
+    xd, ad, bd, fd = dev(_tm(x), torch.float16 if x16 else torch.float32), dev(al), dev(be), dev(f)
+    call("svc_op_activation1d_x16" if x16 else "svc_op_activation1d", ptr(xd), B, L, C, ptr(ad), ptr(bd), ptr(fd),
+         ptr(y), stream())
     out = y.cpu().view(B, L, C).permute(0, 2, 1).numpy()
     assert rel_l2(out, ref.numpy()) < 1e-3
     # fp16 output rounding bound, element-wise
