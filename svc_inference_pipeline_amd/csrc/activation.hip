@@ -51,6 +51,8 @@ __device__ __forceinline__ void act_run(__amdgpu_buffer_rsrc_t rx, __amdgpu_buff
   }
   for (int t = t0; t < t_end; t += P) {
     const uint32_t xrow = xo + (uint32_t)(t + 5) * xs, yrow = yo + (uint32_t)t * ys;
+    // (loading the next block's rows during this block's arithmetic, 106 registers: f32 input 3 % faster, f16 input
+    // 2-3 % slower, r04u)
 #pragma unroll
     for (int k = 0; k < P; ++k) xw[10 + k] = EDGE ? xl(t + 5 + k) : act_load<TX>(rx, xrow, k * xs);
     // output p needs s up to index 2p+11, i.e. x up to window row 10+p

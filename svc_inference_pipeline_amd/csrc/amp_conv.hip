@@ -10,9 +10,8 @@
 //      f16 into an LDS image. Rows outside [0, L) are zeros: the conv's own zero padding.
 //   2. conv: v_mfma_f32_16x16x32_f16 with A fragments read from the LDS image at row r + tap*d (row stride
 //      padded so 16-row fragment reads are conflict-free) and B = the packed weights [Npad][Kpad] (L1/L2).
-//   3. epilogue in registers (the MFMAs run with A and B swapped, so a lane holds 4 consecutive channels of a row):
-//      bias, residual add (add_row), resblock mean accumulation (acc32 / acc_div), f32 and/or f16 stores as 16-B /
-//      8-B vectors. No C staging, so LDS holds only the activation image and more workgroups share a CU.
+//   3. epilogue: bias, residual add (add_row), resblock mean accumulation (acc32 / acc_div), f32 and/or f16 stores
+//      as 16-B / 8-B vectors over whole contiguous rows (the C tile staged through the dead image's LDS in halves).
 // The activation never round-trips through HBM, and every HBM access is a coalesced 16-byte stream.
 #include <type_traits>
 
@@ -42,9 +41,11 @@ struct AmpCfg {
   static constexpr int ROWS = BT + 2 * MAXP;
   static constexpr int FN = (C + 15) / 16;          // 16-column fragments
   static constexpr int A_BYTES = (ROWS + amp_run_len(C, ROWS)) * LDA * 2;  // whole runs of the largest image
-  // the epilogue works in registers (operand-swapped MFMAs, see below), so LDS holds only the activation image:
-  // C = 48: 34 KiB -> 4 workgroups per CU (3 with the former 48 KiB C staging), C = 24: 15 KiB
-  static constexpr int LDS = A_BYTES;
+  // the epilogue stages the C tile in two row halves through the same LDS (the image is dead by then): C = 48 stays at
+  // the image's 31-36 KiB (4 workgroups per CU), C = 24 takes at least the 14 KiB staging half
+  static constexpr int LDC = C + 4;  // f32 staging row stride
+  static constexpr int STG_BYTES = BT / 2 * LDC * 4;
+  static constexpr int LDS = A_BYTES > STG_BYTES ? A_BYTES : STG_BYTES;
   static_assert(C % 8 == 0 && LDA % 8 == 0, "16-B fragment rows");
 };
 
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
   const int rows = CF::BT + 2 * P;
 
   // ------------------------------------------------------------------ 1. SnakeBeta -> LDS (f16)
-  {
+  if (!(p.dbg & 1)) {
     constexpr bool PK = C <= 48;
     constexpr int VEC = PK ? 2 : 1, BLK = PK ? 4 : 8;
     using V = ActVec<VEC>;
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
   half8 bn[CF::FN];  // weight fragments of the next k-step, loaded one step ahead (L2 latency off the MFMA path)
 #pragma unroll
   for (int j = 0; j < CF::FN; ++j) bn[j] = *reinterpret_cast<const half8*>(wrow + (int64_t)j * 16 * p.Kpad);
-  for (int s = 0; s < ks; ++s) {
+  for (int s = 0; s < ((p.dbg & 2) ? 0 : ks); ++s) {
     const int q = 4 * s + fk;
     int tap = q / CPT, cc = q - tap * CPT;
     if (tap >= p.k) tap = cc = 0;  // K tail: zero weights, any finite A
@@ -302,37 +303,71 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
       for (int j = 0; j < CF::FN; ++j)  // C^T fragment: acc[i][j][r] = C[row fr of block i][channel j*16 + fk*4 + r]
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
   }
-  // ------------------------------------------------------------------ 3. epilogue in registers: each lane owns 4
-  // consecutive channels of one row, so bias / residual / accumulator / outputs move as 16-byte vectors
-  const int nvalid = min(CF::BT, Lb - t0);
+  // ------------------------------------------------------------------ 3. epilogue: each lane owns 4 consecutive
+  // channels of one row (operand-swapped MFMAs). The workgroup's output block is [BT][C] contiguous in every tensor, so
+  // the C tile goes through LDS in two row halves (the activation image is dead after the k-loop) and the epilogue
+  // operands and outputs move as whole contiguous rows: a wave's 16-B accesses cover 1 KiB in a row instead of 16
+  // pieces of 64 B at the row stride (SVC_AMP_DBG 4: no epilogue; 8: that register epilogue instead).
+  const int nvalid = (p.dbg & 4) ? 0 : min(CF::BT, Lb - t0);
   const int64_t base = ((int64_t)b * L + t0) * C;
-#pragma unroll
-  for (int j = 0; j < CF::FN; ++j) {
-    const int c0 = j * 16 + fk * 4;
-    if (c0 >= C) continue;
-    const float4 bi = *reinterpret_cast<const float4*>(p.bias + c0);
-#pragma unroll
-    for (int i = 0; i < MW; ++i) {
-      const int row = (wave * MW + i) * 16 + fr;
-      if (row >= nvalid) continue;
-      const int64_t g = base + (int64_t)row * C + c0;
-      float4 w = make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w);
-      if (e.add_row) {
-        const float4 ar = *reinterpret_cast<const float4*>(e.add_row + g);
-        w.x += ar.x; w.y += ar.y; w.z += ar.z; w.w += ar.w;
+  auto epi = [&](float4 w, int64_t g) __attribute__((always_inline)) {
+    if (e.add_row) {
+      const float4 ar = *reinterpret_cast<const float4*>(e.add_row + g);
+      w.x += ar.x; w.y += ar.y; w.z += ar.z; w.w += ar.w;
+    }
+    if (e.acc32) {
+      const float4 ac = *reinterpret_cast<const float4*>(e.acc32 + g);
+      w.x = ac.x + w.x; w.y = ac.y + w.y; w.z = ac.z + w.z; w.w = ac.w + w.w;
+      if (e.acc_div != 1.0f) {
+        w.x = w.x / e.acc_div; w.y = w.y / e.acc_div; w.z = w.z / e.acc_div; w.w = w.w / e.acc_div;
       }
-      if (e.acc32) {
-        const float4 ac = *reinterpret_cast<const float4*>(e.acc32 + g);
-        w.x = ac.x + w.x; w.y = ac.y + w.y; w.z = ac.z + w.z; w.w = ac.w + w.w;
-        if (e.acc_div != 1.0f) {
-          w.x = w.x / e.acc_div; w.y = w.y / e.acc_div; w.z = w.z / e.acc_div; w.w = w.w / e.acc_div;
+    }
+    if (e.out32) *reinterpret_cast<float4*>(e.out32 + g) = w;  // may alias add_row / acc32: same element, same thread
+    if (e.out16) {
+      union { uint2 u2; f16 h[4]; } pk;
+      pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
+      *reinterpret_cast<uint2*>(e.out16 + g) = pk.u2;
+    }
+  };
+  if (!(p.dbg & 8)) {
+    float* stg = reinterpret_cast<float*>(amp_sm);
+    constexpr int HB = CF::BT / 2, C4 = C / 4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      __syncthreads();  // h = 0: the k-loop's image reads are done; h = 1: the first half has been consumed
+      if ((wave >> 1) == h) {
+#pragma unroll
+        for (int j = 0; j < CF::FN; ++j) {
+          const int c0 = j * 16 + fk * 4;
+          if (c0 >= C) continue;
+          const float4 bi = *reinterpret_cast<const float4*>(p.bias + c0);
+#pragma unroll
+          for (int i = 0; i < MW; ++i) {
+            const int r = ((wave & 1) * MW + i) * 16 + fr;
+            *reinterpret_cast<float4*>(stg + r * CF::LDC + c0) =
+                make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w);
+          }
         }
       }
-      if (e.out32) *reinterpret_cast<float4*>(e.out32 + g) = w;  // may alias add_row / acc32: same lane, same element
-      if (e.out16) {
-        union { uint2 u2; f16 h[4]; } pk;
-        pk.h[0] = f16_sat(w.x); pk.h[1] = f16_sat(w.y); pk.h[2] = f16_sat(w.z); pk.h[3] = f16_sat(w.w);
-        *reinterpret_cast<uint2*>(e.out16 + g) = pk.u2;
+      __syncthreads();
+      const int nv = min(HB, nvalid - h * HB);
+      for (int idx = tid; idx < nv * C4; idx += AMP_NT) {
+        const int r = idx / C4, c4 = idx - r * C4;
+        epi(*reinterpret_cast<const float4*>(stg + r * CF::LDC + 4 * c4), base + (int64_t)(h * HB + r) * C + 4 * c4);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < CF::FN; ++j) {
+      const int c0 = j * 16 + fk * 4;
+      if (c0 >= C) continue;
+      const float4 bi = *reinterpret_cast<const float4*>(p.bias + c0);
+#pragma unroll
+      for (int i = 0; i < MW; ++i) {
+        const int row = (wave * MW + i) * 16 + fr;
+        if (row >= nvalid) continue;
+        epi(make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w),
+            base + (int64_t)row * C + c0);
       }
     }
   }
@@ -354,8 +389,11 @@ static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   // (instead of 4) for every conv with P <= 15
   const int P = (p.k - 1) / 2 * p.d;
   const int rows = CF::BT + 2 * P, run = amp_run_len(C, rows);
-  const int lds = (rows + run - 1) / run * run * CF::LDA * 2;
-  hipLaunchKernelGGL((amp_conv_kernel<C, X16>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, p, e);
+  const int lds = std::max((rows + run - 1) / run * run * CF::LDA * 2, CF::STG_BYTES);
+  static const int dbg = getenv("SVC_AMP_DBG") ? atoi(getenv("SVC_AMP_DBG")) : 0;
+  AmpConvArgs pa = p;
+  pa.dbg = dbg;
+  hipLaunchKernelGGL((amp_conv_kernel<C, X16>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, pa, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
