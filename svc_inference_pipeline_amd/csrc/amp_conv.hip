@@ -28,7 +28,7 @@ constexpr int AMP_NT = 256;
 // whole runs (nruns * RUN rows), so that no run is partial: a partial run would take the edge form of the channel-pair
 // activation, and its lanes would make their whole wave run both forms before the barrier.
 __host__ __device__ constexpr int amp_run_len(int C, int rows) {
-  const int blk = C <= 48 ? 4 : 8, ngrp = C <= 48 ? C / 2 : C;
+  const int blk = 4, ngrp = C / 2;
   const int nr_fit = AMP_NT / ngrp > 1 ? AMP_NT / ngrp : 1;
   return ((rows + nr_fit - 1) / nr_fit + blk - 1) / blk * blk;
 }
@@ -100,11 +100,10 @@ __device__ __forceinline__ void amp_act_pair(__amdgpu_buffer_rsrc_t rx, uint32_t
   }
 }
 
-// Launch bound: 4 waves per SIMD, under which the compiler keeps the accumulators in the unified VGPR file (C = 24:
-// 79 registers, 6 waves per SIMD; without an occupancy target it split the file into VGPRs + AGPRs at 5 waves).
-// The activation of C <= 48 runs on channel pairs with packed f32 FMAs (v_pk_fma_f32) in 4-row blocks, C = 96 on
-// single channels in 8-row blocks. Round 1 measured these forms 7-20 % faster per launch than the unbounded
-// single-channel form (tools/amp_bench.py); the earlier forms were removed in round 3.
+// Launch bound: 4 waves per SIMD, under which the compiler keeps the accumulators in the unified VGPR file (without an
+// occupancy target it split the file into VGPRs + AGPRs at 5 waves). The activation runs on channel pairs with packed
+// f32 ops in 4-row blocks for every C (round 4: C = 96 had a single-channel 8-row form, removed with the packed
+// clamp-free form).
 template <int C, bool X16 = false>
 __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
   using CF = AmpCfg<C>;
@@ -123,145 +122,32 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
 
   // ------------------------------------------------------------------ 1. SnakeBeta -> LDS (f16)
   if (!(p.dbg & 1)) {
-    constexpr bool PK = C <= 48;
-    constexpr int VEC = PK ? 2 : 1, BLK = PK ? 4 : 8;
-    using V = ActVec<VEC>;
+    constexpr int BLK = 4;
+    using TX = typename std::conditional<X16, f16, float>::type;
     float f[12], f2[12];  // f2: the up-sampling taps with its factor 2 (exact)
 #pragma unroll
     for (int q = 0; q < 12; ++q) {
       f[q] = p.filt[q];
       f2[q] = 2.0f * f[q];
     }
-    const int ngrp = C / VEC;
-    // run length: the shortest multiple of BLK that gives every (channel, run) task to its own thread (one exposed
-    // load latency per thread: a run's sliding window prefetches its next block across the whole run)
+    constexpr int ngrp = C / 2;
     // (LDS conflicts, VERDICT r03 item 4: making the activation stores conflict-free by the choice of RUN moved the
     // kernel's conflict share only 0.47 -> 0.41 and no timing, r04q; the rest are the conv phase's fragment reads)
     const int RUN = amp_run_len(C, rows);
     const int nruns = (rows + RUN - 1) / RUN;
-    using TX = typename std::conditional<X16, f16, float>::type;
-    const TX* xb = (X16 ? (const TX*)(const void*)p.x16 : (const TX*)(const void*)p.x) + (int64_t)b * L * C;
-    if constexpr (PK) {
-      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<void*>(X16 ? (const void*)p.x16 : (const void*)p.x), (short)0,
-          (int)((int64_t)p.B * L * C * sizeof(TX)), 0x00020000);
-      for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
-        const int cg = task % ngrp, ru = task / ngrp;
-        const int c = cg * 2;
-        const int rs = t0 - P + ru * RUN, re = rs + RUN;  // global rows of this run (whole runs: the image has room)
-        const SnakeCoef2 kc = snake_coef2(p.alpha_log, p.beta_log, c);
-        const uint32_t xo = (uint32_t)(((int64_t)b * L * C + c) * sizeof(TX)), xs = (uint32_t)(C * sizeof(TX));
-        if (rs - 6 < 0 || re + 6 > Lb)
-          amp_act_pair<TX, BLK, CF::LDA, true>(rx, xo, xs, As, t0 - P, rs, re, Lb, c, f, f2, kc);
-        else
-          amp_act_pair<TX, BLK, CF::LDA, false>(rx, xo, xs, As, t0 - P, rs, re, Lb, c, f, f2, kc);
-      }
-    } else {
-      for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
-        const int cg = task % ngrp, ru = task / ngrp;
-        const int c = cg * VEC;
-        const int rs = t0 - P + ru * RUN;                       // first global row of this run
-        const int re = min(rs + RUN, t0 + CF::BT + P);
-        float ar[VEC], ib[VEC];  // alpha / 2pi: the sine's argument in revolutions (snake.h snake2)
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          ar[v] = expf(p.alpha_log[c + v]) * 0.15915494309189535f;
-          ib[v] = 1.0f / (expf(p.beta_log[c + v]) + 0.000000001f);
-        }
-        auto xload = [&](int t, float* o) {
-          t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
-          V::load(xb + (int64_t)t * C + c, o);
-        };
-        auto snake = [&](float* u) {
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) {
-            const float sn = __builtin_amdgcn_sinf(__builtin_amdgcn_fractf(u[v] * ar[v]));
-            u[v] = u[v] + ib[v] * (sn * sn);
-          }
-        };
-        // s at the two ends of the up-sampled signal (the low-pass filter's replicate padding uses them); only runs
-        // within 6 rows of an utterance end need them (wave-uniform in practice: runs are 32-64 rows)
-        const bool edge = rs - 6 < 0 || re + 6 > Lb;
-        float s0[VEC], sE[VEC];
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) s0[v] = sE[v] = 0.f;
-        if (edge) {
-#pragma unroll
-        for (int a = 0; a < 6; ++a) {
-          float x0[VEC], x1[VEC];
-          xload(-3 + a, x0);         // j = 0: even, q = 0
-          xload(Lb - 3 + a, x1);     // j = 2Lb-1: odd, q = Lb-1
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) {
-            s0[v] += x0[v] * f2[11 - 2 * a];
-            sE[v] += x1[v] * f2[10 - 2 * a];
-          }
-        }
-        snake(s0);
-        snake(sE);
-        }
-        // s[2tb-5+i] from the window xw[q] = x[tb-5+q] (exact inside [0, 2L-1]), else the end value
-        auto s_at = [&](const float (*xw)[VEC], int i, int j, float* o) {
-          const int odd = (i + 1) & 1;
-          const int base = ((i - 5) >> 1) + 2 + odd;
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) o[v] = 0.f;
-#pragma unroll
-          for (int a = 0; a < 6; ++a) {
-            const float w = f2[11 - odd - 2 * a];
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) o[v] += xw[base + a][v] * w;
-          }
-          snake(o);
-          if (edge) {
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) o[v] = j < 0 ? s0[v] : (j > 2 * Lb - 1 ? sE[v] : o[v]);
-          }
-        };
-        float xw[BLK + 10][VEC], sw[2 * BLK + 10][VEC], xn[BLK][VEC];
-#pragma unroll
-        for (int q = 0; q < 10; ++q) xload(rs - 5 + q, xw[q]);
-#pragma unroll
-        for (int q = 0; q < BLK; ++q) xload(rs + 5 + q, xn[q]);  // first block, in flight during the warm-up
-#pragma unroll
-        for (int i = 0; i < 10; ++i) s_at(xw, i, 2 * rs - 5 + i, sw[i]);
-        for (int t = rs; t < re; t += BLK) {
-#pragma unroll
-          for (int q = 0; q < BLK; ++q)
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) xw[10 + q][v] = xn[q][v];
-          if (t + BLK < re) {  // next block's loads overlap this block's arithmetic
-#pragma unroll
-            for (int q = 0; q < BLK; ++q) xload(t + BLK + 5 + q, xn[q]);
-          }
-#pragma unroll
-          for (int i = 10; i < 2 * BLK + 10; ++i) s_at(xw, i, 2 * t - 5 + i, sw[i]);
-#pragma unroll
-          for (int q = 0; q < BLK; ++q) {
-            const int row = t + q;
-            if (row < re) {
-              float y[VEC];
-#pragma unroll
-              for (int v = 0; v < VEC; ++v) y[v] = 0.f;
-              if (row >= 0 && row < Lb) {
-#pragma unroll
-                for (int kk = 0; kk < 12; ++kk)
-#pragma unroll
-                  for (int v = 0; v < VEC; ++v) y[v] += f[kk] * sw[2 * q + kk][v];
-              }
-              V::store(As + (row - (t0 - P)) * CF::LDA + c, y);
-            }
-          }
-#pragma unroll
-          for (int q = 0; q < 10; ++q)
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) xw[q][v] = xw[BLK + q][v];
-#pragma unroll
-          for (int i = 0; i < 10; ++i)
-#pragma unroll
-            for (int v = 0; v < VEC; ++v) sw[i][v] = sw[2 * BLK + i][v];
-        }
-      }
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(X16 ? (const void*)p.x16 : (const void*)p.x), (short)0,
+        (int)((int64_t)p.B * L * C * sizeof(TX)), 0x00020000);
+    for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
+      const int cg = task % ngrp, ru = task / ngrp;
+      const int c = cg * 2;
+      const int rs = t0 - P + ru * RUN, re = rs + RUN;  // global rows of this run (whole runs: the image has room)
+      const SnakeCoef2 kc = snake_coef2(p.alpha_log, p.beta_log, c);
+      const uint32_t xo = (uint32_t)(((int64_t)b * L * C + c) * sizeof(TX)), xs = (uint32_t)(C * sizeof(TX));
+      if (rs - 6 < 0 || re + 6 > Lb)
+        amp_act_pair<TX, BLK, CF::LDA, true>(rx, xo, xs, As, t0 - P, rs, re, Lb, c, f, f2, kc);
+      else
+        amp_act_pair<TX, BLK, CF::LDA, false>(rx, xo, xs, As, t0 - P, rs, re, Lb, c, f, f2, kc);
     }
   }
   __syncthreads();

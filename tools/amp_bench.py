@@ -8,7 +8,7 @@ import torch  # noqa: E402
 
 from svc_inference_pipeline_amd._lib import call, profile_enable, profile_read  # noqa: E402
 
-SHAPES = [(48, 119936), (24, 239872)]
+SHAPES = [(48, 119936), (24, 239872)] + ([(96, 59968)] if os.environ.get("AMP_BENCH_C96") else [])
 
 
 def main():
