@@ -35,9 +35,16 @@ __device__ __forceinline__ void act_run(__amdgpu_buffer_rsrc_t rx, __amdgpu_buff
   };
   auto s_win = [&](const f32x2* xw, int i) __attribute__((always_inline)) { return snake_up(xw, i, f2, kc); };
   const int t_end = EDGE ? min(t0 + R, Lb) : t0 + R;
-  f32x2 xw[P + 10], sw[2 * P + 10];
+  // f32 input: the next block's rows are loaded while this block computes (106 registers; f32 launches 3 % faster,
+  // the f16 ones 2-3 % slower with it, r04u)
+  constexpr bool PF = sizeof(TX) == 4;
+  f32x2 xw[P + 10], sw[2 * P + 10], xn[PF ? P : 1];
 #pragma unroll
   for (int k = 0; k < 10; ++k) xw[k] = xl(t0 - 5 + k);
+  if constexpr (PF) {
+#pragma unroll
+    for (int k = 0; k < P; ++k) xn[k] = xl(t0 + 5 + k);
+  }
 #pragma unroll
   for (int i = 0; i < 10; ++i) sw[i] = s_win(xw, i);
   if (EDGE) {
@@ -51,10 +58,17 @@ __device__ __forceinline__ void act_run(__amdgpu_buffer_rsrc_t rx, __amdgpu_buff
   }
   for (int t = t0; t < t_end; t += P) {
     const uint32_t xrow = xo + (uint32_t)(t + 5) * xs, yrow = yo + (uint32_t)t * ys;
-    // (loading the next block's rows during this block's arithmetic, 106 registers: f32 input 3 % faster, f16 input
-    // 2-3 % slower, r04u)
+    if constexpr (PF) {
 #pragma unroll
-    for (int k = 0; k < P; ++k) xw[10 + k] = EDGE ? xl(t + 5 + k) : act_load<TX>(rx, xrow, k * xs);
+      for (int k = 0; k < P; ++k) xw[10 + k] = xn[k];
+      if (t + P < t_end) {
+#pragma unroll
+        for (int k = 0; k < P; ++k) xn[k] = EDGE ? xl(t + P + 5 + k) : act_load<TX>(rx, xrow, (P + k) * xs);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < P; ++k) xw[10 + k] = EDGE ? xl(t + 5 + k) : act_load<TX>(rx, xrow, k * xs);
+    }
     // output p needs s up to index 2p+11, i.e. x up to window row 10+p
 #pragma unroll
     for (int p = 0; p < P; ++p) {
