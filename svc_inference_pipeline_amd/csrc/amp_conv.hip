@@ -298,14 +298,32 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
               "amp_conv: epilogue must be contiguous rows of C channels (bias / add_row / acc32 / out32 / out16)");
   const void* xin = p.x16 ? (const void*)p.x16 : (const void*)p.x;
   SVC_REQUIRE(((uintptr_t)xin & 15) == 0 && ((uintptr_t)p.W & 15) == 0, "amp_conv: alignment");
-  if (p.x16) {
-    if (C == 24) return launch_amp<24, true>(p, e, s);
-    if (C == 48) return launch_amp<48, true>(p, e, s);
-    return launch_amp<96, true>(p, e, s);
+  // the activation reads x through a buffer descriptor (32-bit record count and offsets): utterances per launch such
+  // that one launch's x span stays below 2^31 bytes; the rows of every tensor are contiguous [B*L][C]
+  const int64_t per_b = (int64_t)p.L * C * (p.x16 ? 2 : 4);
+  const int bchunk = (int)std::max<int64_t>(1, std::min<int64_t>(p.B, ((int64_t)1 << 31) / per_b - 1));
+  for (int b0 = 0; b0 < p.B; b0 += bchunk) {
+    const int64_t off = (int64_t)b0 * p.L * C;
+    AmpConvArgs q = p;
+    EpiArgs f = e;
+    q.B = std::min(bchunk, p.B - b0);
+    if (q.x) q.x += off;
+    if (q.x16) q.x16 += off;
+    if (q.tv) q.tv += b0;
+    if (f.out32) f.out32 += off;
+    if (f.out16) f.out16 += off;
+    if (f.acc32) f.acc32 += off;
+    if (f.add_row) f.add_row += off;
+    int st;
+    if (C == 24)
+      st = q.x16 ? launch_amp<24, true>(q, f, s) : launch_amp<24, false>(q, f, s);
+    else if (C == 48)
+      st = q.x16 ? launch_amp<48, true>(q, f, s) : launch_amp<48, false>(q, f, s);
+    else
+      st = q.x16 ? launch_amp<96, true>(q, f, s) : launch_amp<96, false>(q, f, s);
+    if (st) return st;
   }
-  if (C == 24) return launch_amp<24, false>(p, e, s);
-  if (C == 48) return launch_amp<48, false>(p, e, s);
-  return launch_amp<96, false>(p, e, s);
+  return SVC_OK;
 }
 
 }  // namespace svc

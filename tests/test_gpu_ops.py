@@ -132,6 +132,38 @@ def test_amp_conv(B, L, k, d, C):
     assert rel_l2(out, ref.numpy()) < 2e-3
 
 
+def test_bigvgan_activation_launch_chunks():
+    """Batches whose activation input spans more than 2 GiB: activation1d and amp_conv address x through 32-bit buffer
+    descriptors, so the host splits the batch into launches of < 2^31 bytes (98 + 2 utterances here). Each utterance
+    of the big batch must equal the same utterance run alone, bit for bit, on both sides of the split."""
+    from svc_inference_pipeline_amd import weights as W
+    B, L, C, k, d = 100, 224000, 24, 3, 1
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(B * L, C, device="cuda", generator=g) * 2
+    al = torch.randn(C, device="cuda", generator=g) * 0.3
+    be = torch.randn(C, device="cuda", generator=g) * 0.3
+    f = W.kaiser_sinc_filter1d(0.25, 0.3, 12).view(-1).cuda()
+    w = torch.randn(C, C, k, device="cuda", generator=g) / np.sqrt(C * k)
+    b = torch.randn(C, device="cuda", generator=g) * 0.1
+    y = torch.empty(B * L, C, device="cuda")
+    y1 = torch.empty(L, C, device="cuda")
+    for op in ("act", "amp"):
+        if op == "act":
+            call("svc_op_activation1d", ptr(x), B, L, C, ptr(al), ptr(be), ptr(f), ptr(y), stream())
+        else:
+            call("svc_op_amp_conv", ptr(x), B, L, C, ptr(al), ptr(be), ptr(f), ptr(w), ptr(b), k, d, None, ptr(y),
+                 stream())
+        for u in (0, 97, 98, 99):
+            xu = x[u * L:(u + 1) * L]
+            if op == "act":
+                call("svc_op_activation1d", ptr(xu), 1, L, C, ptr(al), ptr(be), ptr(f), ptr(y1), stream())
+            else:
+                call("svc_op_amp_conv", ptr(xu), 1, L, C, ptr(al), ptr(be), ptr(f), ptr(w), ptr(b), k, d, None,
+                     ptr(y1), stream())
+            torch.cuda.synchronize()
+            assert torch.equal(y[u * L:(u + 1) * L], y1), (op, u)
+
+
 @pytest.mark.parametrize("B,L,D", [(1, 1500, 1024), (2, 100, 128), (1, 64, 64), (2, 1, 64), (1, 129, 256)])
 def test_attention(B, L, D):
     g = torch.Generator().manual_seed(3)
