@@ -23,6 +23,10 @@ SHAPES = [  # name, M, N, Cin, taps, epi
     ("bigvgan.s2 k11", 32 * 14992, 384, 384, 11, 0),
     ("whisper.fc1", 48000, 4096, 1024, 1, 0),
     ("whisper.fc2", 48000, 1024, 4096, 1, 0),
+    ("whisper.qkv", 48000, 3072, 1024, 1, 0),
+    ("whisper.out", 48000, 1024, 1024, 1, 0),
+    ("bigvgan.s3 k11 (C192)", 32 * 29984, 192, 192, 11, 0),
+    ("bigvgan.s4 k11 (C96)", 32 * 59968, 96, 96, 11, 0),
     ("bigvgan.s1 k11", 32 * 3748, 768, 768, 11, 0),
     ("square 8192", 8192, 8192, 8192, 1, 0),
 ]
