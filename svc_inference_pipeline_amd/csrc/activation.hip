@@ -155,6 +155,7 @@ int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const flo
   const int tok = prof_begin("activation1d", 0.0, (double)B * L * C * ((x16 ? 2 : 4) + 2), s);
   // a channel pair per thread, 8-output blocks, 128-output runs (the register-streaming shape that measured fastest
   // in rounds 1-2, against other block / run shapes and an LDS-tiled form)
+  // (f16 input in 4-row blocks, 82 registers = 6 waves per SIMD: 10 % slower per launch, r04af)
   if (x16)
     launch_rs<8, 128>(x16, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   else
