@@ -96,7 +96,10 @@ svc_status svc_f0_ac(svc_ctx* ctx, const float* wav24k, int B, int64_t n_samples
    0.1-semitone bins, Viterbi decoding) and the unvoiced frames set to 0. wav [B][n_samples] f32 -> f0 [B*T] float64,
    utterance b's frames 1 + utt_samples[b] / hop_length, the rest of its T rows 0 (T >= 1 + n_samples / hop_length
    when every utterance is full length). Uses the feature-stage workspace, like svc_f0_ac; the context need not be
-   finalized. Parity is unpinned (librosa is absent here): tests/test_f0.py holds it to oracle/pyin.py. */
+   finalized. Parity is unpinned (librosa is absent here): tests/test_f0.py holds it to oracle/pyin.py, which restates
+   librosa 0.10.1 (its parabolic-interpolation shift and pyin's pad_mode="constant" default; librosa 0.9 / 0.10.0
+   compute the parabolic shift differently, and the reference pins no librosa version). The device tables are built
+   once per (fs, f0_min, f0_max, win_length, hop_length) and kept in the context. */
 svc_status svc_f0_pyin(svc_ctx* ctx, const float* wav, int B, int64_t n_samples, const int64_t* utt_samples, double fs,
                        int win_length, int hop_length, double f0_min, double f0_max, int T, double* f0, void* stream);
 
@@ -105,7 +108,11 @@ svc_status svc_f0_pyin(svc_ctx* ctx, const float* wav, int B, int64_t n_samples,
 svc_status svc_pitch_shift(svc_ctx* ctx, double* f0, int B, int T, double target_median, void* stream);
 
 /* A5+A6: wav16k [B][n_samples] f32 (int16-quantised, <= 480000 samples; zero-padded to 30 s)
-   -> Whisper encoder output feats [B*n_ctx][n_state] f32. */
+   -> Whisper encoder output feats [B*n_ctx][n_state] f32.
+   Non-finite input: the attention kernel is compiled with -fno-honor-nans (its softmax max tree skips NaN
+   canonicalisation), so a NaN reaching q / k / v gives undefined feats (possibly finite) instead of a propagated
+   NaN. The log-mel front end and LayerNorm keep finite audio finite; a NaN / inf sample in wav16k is the caller's
+   error. The same holds for svc_hubert_encode and svc_op_attention. */
 svc_status svc_whisper_encode(svc_ctx* ctx, const float* wav16k, int B, int64_t n_samples, float* feats, void* stream);
 
 /* A7: feats [B*src_rows][D] f32 -> content [B*T][D] f16 (IEEE binary16 bits), 15:8 repeat/average. T <= 2812. */

@@ -131,10 +131,13 @@ __global__ __launch_bounds__(256) void activation1d_rs_kernel(const TX* __restri
 }
 
 template <int P, int R, typename TX>
-static void launch_rs(const TX* x, f16* y, int B, int L, int C, int ldy, const float* al, const float* bl,
+static int launch_rs(const TX* x, f16* y, int B, int L, int C, int ldy, const float* al, const float* bl,
                       const float* filt, const int* tv, int tv_mul, hipStream_t s) {
   // utterances per launch: both tensors' spans below 2^31 bytes (buffer offsets and record counts are 32-bit)
   const int64_t per_b = (int64_t)L * std::max<int64_t>((int64_t)C * sizeof(TX), (int64_t)ldy * 2);
+  // one utterance must fit the 32-bit offsets itself (the split is per utterance; svc_bigvgan bounds T accordingly)
+  SVC_REQUIRE(per_b < ((int64_t)1 << 31), "activation1d: one utterance spans %lld bytes (L=%d C=%d), >= 2 GiB",
+                (long long)per_b, L, C);
   const int bchunk = (int)std::max<int64_t>(1, std::min<int64_t>(B, ((int64_t)1 << 31) / per_b - 1));
   for (int b0 = 0; b0 < B; b0 += bchunk) {
     const int nb = std::min(bchunk, B - b0);
@@ -143,6 +146,7 @@ static void launch_rs(const TX* x, f16* y, int B, int L, int C, int ldy, const f
                        x + (int64_t)b0 * L * C, y + (int64_t)b0 * L * ldy, nb, L, C, ldy, al, bl, filt,
                        tv ? tv + b0 : nullptr, tv_mul);
   }
+  return SVC_OK;
 }
 
 // tv / tv_mul (optional): ragged batches, utterance b's sequence is min(L, tv[b] * tv_mul) rows long.
@@ -156,11 +160,10 @@ int activation1d(const float* x, f16* y, int B, int L, int C, int ldy, const flo
   // a channel pair per thread, 8-output blocks, 128-output runs (the register-streaming shape that measured fastest
   // in rounds 1-2, against other block / run shapes and an LDS-tiled form)
   // (f16 input in 4-row blocks, 82 registers = 6 waves per SIMD: 10 % slower per launch, r04af)
-  if (x16)
-    launch_rs<8, 128>(x16, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
-  else
-    launch_rs<8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
+  const int st = x16 ? launch_rs<8, 128>(x16, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s)
+                     : launch_rs<8, 128>(x, y, B, L, C, ldy, alpha_log, beta_log, filt, tv, tv_mul, s);
   prof_end(tok, s);
+  if (st) return st;
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }

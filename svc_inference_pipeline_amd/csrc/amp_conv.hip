@@ -301,6 +301,9 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
   // the activation reads x through a buffer descriptor (32-bit record count and offsets): utterances per launch such
   // that one launch's x span stays below 2^31 bytes; the rows of every tensor are contiguous [B*L][C]
   const int64_t per_b = (int64_t)p.L * C * (p.x16 ? 2 : 4);
+  // one utterance must fit the 32-bit offsets itself (the split is per utterance; svc_bigvgan bounds T accordingly)
+  SVC_REQUIRE(per_b < ((int64_t)1 << 31), "amp_conv: one utterance spans %lld bytes (L=%d C=%d), >= 2 GiB",
+              (long long)per_b, p.L, C);
   const int bchunk = (int)std::max<int64_t>(1, std::min<int64_t>(p.B, ((int64_t)1 << 31) / per_b - 1));
   for (int b0 = 0; b0 < p.B; b0 += bchunk) {
     const int64_t off = (int64_t)b0 * p.L * C;

@@ -460,6 +460,10 @@ struct svc_ctx {
     return SVC_OK;
   }
   int hop_out = 256;
+  // pYIN's device tables (beta priors, banded log-transitions, bin frequencies) for the last (fs, f0_min, f0_max,
+  // win, hop): built once per parameter set; a new set gets a new buffer (an in-flight call may still read the old)
+  double* pyin_tab = nullptr;
+  double pyin_key[5] = {0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -1732,17 +1736,29 @@ svc_status svc_f0_pyin(svc_ctx* c, const float* wav, int B, int64_t n, const int
   const size_t need = pyin_workspace_bytes(B, T, fs, f0_min, f0_max, FL, win_length, hop_length);
   int st;
   if ((st = c->auxws.reserve(std::max(need + 4096, c->auxws.cap)))) return st;
-  // one staged table per call (the ring retires its last slot): [lengths int64 B][pyin tables f64]
-  std::vector<double> buf(B + nt);
-  if (n_samples) memcpy(buf.data(), n_samples, (size_t)B * 8);
-  if ((st = pyin_tables(fs, f0_min, f0_max, FL, win_length, hop_length, buf.data() + B))) return st;
+  // the tables depend only on (fs, f0_min, f0_max, win, hop): built and uploaded once per parameter set
+  const double key[5] = {fs, f0_min, f0_max, (double)win_length, (double)hop_length};
+  if (!c->pyin_tab || memcmp(key, c->pyin_key, sizeof(key)) != 0) {
+    std::vector<double> tab(nt);
+    if ((st = pyin_tables(fs, f0_min, f0_max, FL, win_length, hop_length, tab.data()))) return st;
+    void* p = nullptr;
+    SVC_HIP_CHECK(hipMalloc(&p, nt * 8));
+    c->allocs.push_back(p);
+    SVC_HIP_CHECK(hipMemcpy(p, tab.data(), nt * 8, hipMemcpyHostToDevice));
+    c->pyin_tab = reinterpret_cast<double*>(p);
+    memcpy(c->pyin_key, key, sizeof(key));
+  }
+  // only the per-call lengths are staged (the ring retires its last slot)
   hipStream_t s = (hipStream_t)stream;
   RingRetire retire_(c->lens_feat, s);
-  void* dev = nullptr;
-  if ((st = c->lens_feat.put(buf.data(), buf.size() * 8, s, &dev))) return st;
-  const int64_t* nb_dev = n_samples ? reinterpret_cast<const int64_t*>(dev) : nullptr;
+  const int64_t* nb_dev = nullptr;
+  if (n_samples) {
+    void* dev = nullptr;
+    if ((st = c->lens_feat.put(n_samples, (size_t)B * 8, s, &dev))) return st;
+    nb_dev = reinterpret_cast<const int64_t*>(dev);
+  }
   return f0_pyin(wav, B, n, nb_dev, n_samples, fs, f0_min, f0_max, FL, win_length, hop_length, T, f0, c->auxws.base,
-                 c->auxws.cap, reinterpret_cast<const double*>(dev) + B, s);
+                 c->auxws.cap, c->pyin_tab, s);
 }
 
 svc_status svc_pitch_shift(svc_ctx* c, double* f0, int B, int T, double target_median, void* stream) {
@@ -2482,6 +2498,12 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
     Lr *= S.rate;
     maxLC = std::max(maxLC, (Lr / T) * S.cout);
   }
+  // the activation kernels address one utterance's f32 stage buffer through 32-bit buffer offsets: T * maxLC * 4 bytes
+  // must stay below 2 GiB (87 381 frames = 15.5 min of 24 kHz audio for the reference config); longer utterances are
+  // rejected here rather than silently wrapped
+  SVC_REQUIRE((int64_t)T * maxLC * 4 < ((int64_t)1 << 31),
+              "bigvgan: T=%d frames per utterance exceeds the vocoder's limit of %lld frames (2 GiB stage span)", T,
+              (long long)((((int64_t)1 << 31) - 1) / ((int64_t)maxLC * 4)));
   const size_t big = (size_t)B * T * maxLC;
   const size_t need = (size_t)B * T * ldm * 2 + (size_t)B * T * c->v_c0 * 2 + big * (4 * 4 + 2 * 2) + 32 * 4096;
   int st;

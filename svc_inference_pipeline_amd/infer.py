@@ -97,7 +97,8 @@ def main(argv=None):
     ap.add_argument("--random-weights", default=None, choices=sorted(W.WHISPER_DIMS))
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--f0-method", default="parselmouth", choices=("parselmouth", "pyin"),
-                    help="F0 extractor: Praat AC (the reference's infer.py) or pYIN (utils/f0.py:95-117)")
+                    help="F0 extractor: Praat AC (the reference's infer.py) or pYIN (utils/f0.py:95-117; follows "
+                         "librosa 0.10.1's pyin, parity-unpinned: librosa is not installed here)")
     args = ap.parse_args(argv)
 
     cfg = C.load_config(args.config) if args.config else C.load_config()

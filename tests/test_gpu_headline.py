@@ -148,3 +148,86 @@ def test_headline_batch_convert(engine, cfg):
                            seed=1234, utt_ids=dev(uids[k:k + 1], torch.int32))
         assert torch.equal(one.x0[0], res.x0[k]), k
         assert torch.equal(one.wav[0], res.wav[k]), k
+
+
+def _headline_mels(cfg, frames):
+    """De-normalised ln-mels [100, T_b] of synthetic clips with T_b = frames[b] (utils/mel.py on the oracle), and
+    the normalised [B, max T, 100] sampler-output layout svc_bigvgan takes (rows past T_b zero)."""
+    stats = C.load_stats(cfg)
+    mels = []
+    for b, T in enumerate(frames):
+        w = ON.synth_clip(40 + b, T * cfg.hop_length / cfg.fs, cfg.fs)[:T * cfg.hop_length]
+        m = OF.mel_spectrogram(torch.from_numpy(w)[None], cfg)[0].numpy()
+        assert m.shape == (100, T)
+        mels.append(m)
+    x = np.zeros((len(frames), max(frames), 100), np.float32)
+    for b, m in enumerate(mels):
+        x[b, :m.shape[1]] = ((m - stats["mel_min"][:, None]) / (stats["mel_max"] - stats["mel_min"] + 1e-12)[:, None]
+                             * 2 - 1).T
+    return mels, x
+
+
+def _oracle_wav(vsd, cfg, mel, emulate=False):
+    """modules/bigvgan.py:600-622 Generator + modules/bigvgan_inference.py:29-44 trim and fade, on the CPU oracle (f32,
+    or with every conv operand and AMPBlock1's intermediate rounded to fp16 as the HIP path rounds them)."""
+    T = mel.shape[-1]
+    with torch.no_grad():
+        if emulate:
+            with OM.Fp16Operands():
+                return OF.synthesis_fade(OM.bigvgan_forward(vsd, cfg.vocoder, torch.from_numpy(mel)[None])[0, 0], T).numpy()
+        return OF.synthesis_fade(OM.bigvgan_forward(vsd, cfg.vocoder, torch.from_numpy(mel)[None])[0, 0], T).numpy()
+
+
+@pytest.mark.timeout(600)
+def test_bigvgan_headline_length_tamed_ragged(cfg, states):
+    """A14 + A15 at the headline length, tamed weights (every weight_g x 0.5, as test_bigvgan_tamed_weights_tight: the
+    generator does not saturate tanh, so fp16 rounding is the only expected difference) on a ragged batch of one
+    T = 937 utterance (10 s, the headline clip) and one T = 301 utterance, through svc_bigvgan's per-utterance length
+    table: the six up-sampling stages, the fused small-channel AMP convs, their 2 GiB launch split and the fade-out at
+    each utterance's own end. Each waveform against the f32 oracle (Generator + trim + fade run per utterance alone):
+    the waveform tolerance of DESIGN.md, rel-L2 <= 2e-3 and <= 1.2x (+2e-4) the distance of the fp16-operand-emulated
+    oracle; the padded utterance's samples past its end are zero."""
+    vsd = {k: (v * 0.5 if k.endswith("weight_g") else v) for k, v in states["vocoder"].items()}
+    frames = [937, 301]
+    mels, x = _headline_mels(cfg, frames)
+    e = SVCEngine(cfg, 0, mapper_state=states["mapper"], vocoder_state=vsd)
+    try:
+        wav = e.bigvgan(dev(x), frames=frames).cpu().numpy()
+    finally:
+        e.close()
+    hop = cfg.hop_length
+    for b, (T, mel) in enumerate(zip(frames, mels)):
+        ref = _oracle_wav(vsd, cfg, mel)
+        emu = _oracle_wav(vsd, cfg, mel, emulate=True)
+        got = wav[b, :T * hop]
+        sat = float(np.mean(np.abs(ref) > 0.97))
+        d_hip, d_emu = rel_l2(got, ref), rel_l2(emu, ref)
+        print(f"BigVGAN tamed T={T}: saturated {sat:.3f}, rel-L2 HIP {d_hip:.3e}, fp16 emulation {d_emu:.3e}")
+        assert sat < 0.05, sat
+        assert d_hip <= 2e-3 and d_hip <= 1.2 * d_emu + 2e-4, (T, d_hip, d_emu)
+        assert not np.any(wav[b, T * hop:]), T
+
+
+@pytest.mark.timeout(600)
+def test_bigvgan_headline_length_default_weights(engine, cfg, states):
+    """The production engine's mel -> waveform chain (de-normalise, Generator, trim, fade) at T = 937 with the default
+    random weights, whose generator runs in the chaotic tanh-saturated regime: against the f32 oracle within
+    test_bigvgan's rule, 1.5x the fp16-operand emulation's distance + 1e-3."""
+    mels, x = _headline_mels(cfg, [937])
+    wav, mel_d = engine.bigvgan(dev(x), return_mel=True)
+    assert np.max(np.abs(mel_d[0].cpu().numpy().T - mels[0])) < 1e-4
+    ref = _oracle_wav(states["vocoder"], cfg, mels[0])
+    emu = _oracle_wav(states["vocoder"], cfg, mels[0], emulate=True)
+    d_hip, d_emu = rel_l2(wav[0].cpu().numpy(), ref), rel_l2(emu, ref)
+    print(f"BigVGAN default weights T=937: rel-L2 HIP {d_hip:.3e}, fp16 emulation {d_emu:.3e}")
+    assert d_hip < 1.5 * d_emu + 1e-3, (d_hip, d_emu)
+
+
+def test_bigvgan_rejects_oversize_utterance(engine, cfg):
+    """The vocoder's activation kernels address one utterance's f32 stage buffer (T * 6144 floats for the reference
+    config) with 32-bit buffer offsets: an utterance past 2 GiB (87 382 frames, 15.5 min) is rejected with an error
+    instead of being silently corrupted."""
+    from svc_inference_pipeline_amd import _lib
+    x = torch.zeros(1, 87382, 100, device="cuda")
+    with pytest.raises(_lib.SVCError, match="vocoder's limit"):
+        engine.bigvgan(x)

@@ -15,6 +15,7 @@ from gpu_util import dev, rel_l2  # noqa: E402
 from oracle import features as OF  # noqa: E402
 from oracle import models as OM  # noqa: E402
 from oracle import noise as ON  # noqa: E402
+from svc_inference_pipeline_amd import _lib  # noqa: E402
 from svc_inference_pipeline_amd import config as C  # noqa: E402
 from svc_inference_pipeline_amd import weights as W  # noqa: E402
 from svc_inference_pipeline_amd.runtime import SVCEngine  # noqa: E402
@@ -171,16 +172,29 @@ def test_gate_ws_bit_identical(engine, B, T, frames, tune):
     """gate_ws.hip (the DiffSVC dilated conv + gate as a weight-stationary row stream: W in VGPRs, one LDS image per
     64-row super-block shared by the three taps, the K chain split over a wave pair through the MFMA C operand) against
     conv_gemm4<128,128,gate> (gate_ws = 0): the same 32-deep K order, MFMA operand order and epilogue arithmetic, so the
-    eps of every layer's dilation (1, 2, 4, 8) is bit for bit equal. Tiny (M < 16), ragged row counts (parts of 16-row
-    blocks, partial super-blocks, empty row parts), utterance boundaries inside blocks, ragged frame counts (taps past an
-    utterance's valid rows read the zero row), one of them a single frame."""
+    eps of every layer's dilation (1, 2, 4, 8) is bit for bit equal. Ragged row counts (parts of 16-row blocks, partial
+    super-blocks, empty row parts), utterance boundaries inside blocks, ragged frame counts (taps past an utterance's
+    valid rows read the zero row), one of them a single frame. gate_ws needs T >= 16 frames per batch row; (1, 5) checks
+    that a shorter batch falls back to conv_gemm4 (the profiler records which kernel ran: gate_ws launches exactly when
+    T >= 16, so no case passes by running conv_gemm4 on both sides)."""
     rng = np.random.default_rng(B * 29 + T)
     cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
     x = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
     tune(engine, gate_ws=0)
     ref = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
     tune(engine, gate_ws=1)
-    out = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
+    _lib.profile_enable(True)
+    try:
+        out = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
+        ran = _lib.profile_read()
+    finally:
+        _lib.profile_enable(False)
+    n_ws = sum(v["launches"] for k, v in ran.items() if k.startswith("gate_ws"))
+    n_g4 = sum(v["launches"] for k, v in ran.items() if k.startswith("conv_gemm4") and k.endswith("@diffsvc.dilated"))
+    if T >= 16:
+        assert n_ws > 0 and n_g4 == 0, ran.keys()
+    else:
+        assert n_ws == 0 and n_g4 > 0, ran.keys()
     for k in range(2):
         assert np.isfinite(out[k]).all()
         assert np.array_equal(out[k], ref[k]), (k, rel_l2(out[k], ref[k]))

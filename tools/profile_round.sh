@@ -1,9 +1,9 @@
 #!/bin/bash
-# round 4 profile of record: bench line (with the CPU baseline) + rocprofv3 trace + FETCH / WRITE passes on the
+# profile of record: bench line (with the CPU baseline) + rocprofv3 trace + FETCH / WRITE passes on the
 # headline kernel (tools/gpu_profile.sh), per-kernel PMC passes (tools/pmc_kernels.sh), and one issue-accounting pass
 # on gate_ws (counters checked against rocprofv3 -L first)
 set -o pipefail
-TAG=${TAG:-r04prof}
+TAG=${TAG:-prof}
 mkdir -p gpurun_out/$TAG
 timeout -k 10 60 rocprofv3 -L > gpurun_out/$TAG/counters.txt 2>&1 || true
 bash tools/gpu_profile.sh $TAG > gpurun_out/${TAG}_profile.log 2>&1 || { tail -20 gpurun_out/${TAG}_profile.log; exit 1; }
