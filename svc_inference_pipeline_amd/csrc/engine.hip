@@ -132,8 +132,11 @@ int layernorm_dual(const float* x, const float* g, const float* b, float* y32, f
 int pack_qkv(const float* q, const float* k, const float* v, f16* qkv, int64_t rows, int D, float scale, hipStream_t s);
 int f0_praat_ac(const float* wav, int B, int64_t n_samples, double fs, double time_step, double floor_hz,
                 double ceiling_hz, double voicing, int T, double* f0_out, void* workspace, size_t ws_bytes,
-                hipStream_t s, const int64_t* n_b = nullptr, const int* T_b = nullptr, StageRing* ring = nullptr);
+                const double* tables, hipStream_t s, const int64_t* n_b = nullptr, const int* T_b = nullptr,
+                StageRing* ring = nullptr);
 size_t f0_workspace_bytes(int B, int64_t n_samples, double fs, double time_step, double floor_hz);
+size_t f0_table_doubles(double fs, double floor_hz);
+int f0_tables(double fs, double floor_hz, double* out);
 size_t pyin_table_doubles(double sr, double fmin, double fmax, int frame_length, int win_length, int hop);
 size_t pyin_workspace_bytes(int B, int F, double sr, double fmin, double fmax, int frame_length, int win_length,
                             int hop);
@@ -464,6 +467,9 @@ struct svc_ctx {
   // win, hop): built once per parameter set; a new set gets a new buffer (an in-flight call may still read the old)
   double* pyin_tab = nullptr;
   double pyin_key[5] = {0, 0, 0, 0, 0};
+  // Praat-AC F0's window / window autocorrelation / FFT twiddle tables for (fs, f0_min) (f0.hip f0_tables), likewise
+  double* f0_tab = nullptr;
+  double f0_key[2] = {0, 0};
 };
 
 namespace {
@@ -1719,8 +1725,19 @@ svc_status svc_f0_ac(svc_ctx* c, const float* wav, int B, int64_t n, const int64
     Tb.resize(B);
     for (int b = 0; b < B; ++b) Tb[b] = (int)mel_frames_of(c, n_samples[b]);
   }
+  const double key[2] = {(double)c->fs, c->f0_min};
+  if (!c->f0_tab || memcmp(key, c->f0_key, sizeof(key)) != 0) {
+    std::vector<double> tab(f0_table_doubles(c->fs, c->f0_min));
+    if ((st = f0_tables(c->fs, c->f0_min, tab.data()))) return st;
+    void* p = nullptr;
+    SVC_HIP_CHECK(hipMalloc(&p, tab.size() * 8));
+    c->allocs.push_back(p);
+    SVC_HIP_CHECK(hipMemcpy(p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
+    c->f0_tab = reinterpret_cast<double*>(p);
+    memcpy(c->f0_key, key, sizeof(key));
+  }
   RingRetire retire_(c->lens_feat, (hipStream_t)stream);
-  return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->auxws.base, c->auxws.cap,
+  return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->auxws.base, c->auxws.cap, c->f0_tab,
                      (hipStream_t)stream, n_samples, n_samples ? Tb.data() : nullptr, &c->lens_feat);
 }
 
