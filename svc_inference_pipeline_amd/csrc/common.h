@@ -102,6 +102,24 @@ __device__ __forceinline__ float gate_act(float a, float b) {
 // 8-byte buffer store (range-checked: a voffset past the descriptor's range is dropped). Write-through (cache policy
 // sc1), so that the kernel-end release would find the outputs clean, measured slower for the row-stream kernels
 // (r04n: 855.8 / 857.1 against 879.6 / 881.3 audio-s/s): plain write-back
+// x / sqrt(2) (f32 sqrt(2)) exactly as the IEEE division rounds it, in one multiply and two FMAs (q0 = x r,
+// e = x - q0 sqrt(2) exactly, q0 + e r): equal to the division bit for bit for every float x with 2^-100 <= |x| < inf
+// (all 2^32 inputs checked against x86 fmaf / division; the differing inputs are |x| <= 2.2e-32 and +-inf). Those
+// lanes take the division, behind a branch no wave takes in practice. Replaces the ~10-instruction division sequence
+// (v_div_scale x2, v_rcp, 4 FMAs, v_div_fmas, v_div_fixup) of the DiffSVC residual epilogues (res_proj, dlayer).
+constexpr float SQRT2_F = 1.41421356237309515f;
+__device__ __forceinline__ float div_sqrt2_exact(float x) {
+  constexpr float r = 1.0f / SQRT2_F;
+  float q;
+  if (__builtin_expect(fabsf(x) >= 0x1p-100f && fabsf(x) <= 3.402823466e38f, 1)) {
+    const float q0 = x * r;
+    q = fmaf(fmaf(-q0, SQRT2_F, x), r, q0);
+  } else {
+    q = x / SQRT2_F;  // (NaN too) the IEEE division for this lane
+  }
+  return q;
+}
+
 __device__ __forceinline__ void buffer_store_b64(uint2 v, __amdgpu_buffer_rsrc_t r, uint32_t vo) {
   typedef unsigned int u32x2v __attribute__((vector_size(8)));
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, v), r, vo, 0, 0);
@@ -271,6 +289,12 @@ struct RingRetire {
   ~RingRetire() { r.retire(s); }
 };
 
+// dlayer.hip's residual half (the fused DiffSVC layer): W_res in res_proj_pack fragment order, its bias, dproj_i / dproj_{i+1},
+// the split residual stream's new high half (another buffer than the layer input) and its low half (updated in place)
+struct DLayerProj {
+  const f16* Wr; const float* br; const float* sub; const float* add; f16* hi_out; f16* lo;
+};
+
 // One PLMS update x' = x + d (A x - Bc e'), e' = (sum_k c_k e_k) / div (modules/diffsvcrepo_inference.py:91-130;
 // engine.hip svc_diffsvc_sample, elementwise.hip plms_update).
 struct PlmsArgs {
@@ -301,6 +325,7 @@ struct Tuning {
                             // > 1: that many row lanes of 2 workgroups instead of 1/2 (one sampler stream) or 3/8
                             // (several) of the CU count)
   int gate_ws = 1;          // DiffSVC dilated conv + gate on the weight-stationary row stream (gate_ws.hip; 0: conv_gemm4)
+  int dlayer = 0;           // DiffSVC layer with the rows held still and the weights streamed (dlayer.hip)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only, A/B runs)
   void from_env();
   bool set(const char* name, double v);  // false: unknown name ("reset" restores the creation-time values)

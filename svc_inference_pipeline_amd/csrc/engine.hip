@@ -109,6 +109,9 @@ int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
 bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e);
+bool dlayer_fits(const ConvGemmArgs& a, const EpiArgs& e);
+int dlayer(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s, const DLayerProj* pr);
+constexpr int kNotFused = 1000;  // run_gemm with a DLayerProj: the fused layer does not fit (the caller runs it unfused)
 extern unsigned long long* gate_ws_stamps;
 int gate_ws_nstamp();
 int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
@@ -328,7 +331,7 @@ static int* tuning_field(T& t, const char* name) {
               {"whisper_streams", &t.whisper_streams}, {"sampler_streams", &t.sampler_streams},
               {"vocoder_streams", &t.vocoder_streams}, {"diff_head", &t.diff_head},
               {"amp_maxc", &t.amp_maxc},               {"res_proj", &t.res_proj},
-              {"gate_ws", &t.gate_ws}};
+              {"gate_ws", &t.gate_ws},                 {"dlayer", &t.dlayer}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) return it.v;
   return nullptr;
@@ -336,7 +339,7 @@ static int* tuning_field(T& t, const char* name) {
 
 void Tuning::from_env() {
   for (const char* name : {"gemm_variant", "gemm3_direct", "whisper_streams", "sampler_streams", "vocoder_streams",
-                           "diff_head", "amp_maxc", "res_proj", "gate_ws"}) {
+                           "diff_head", "amp_maxc", "res_proj", "gate_ws", "dlayer"}) {
     std::string env = "SVC_";
     for (const char* q = name; *q; ++q) env += (char)toupper((unsigned char)*q);
     if (const char* v = getenv(env.c_str())) *tuning_field(*this, name) = atoi(v);
@@ -717,7 +720,8 @@ static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cv
 
 // tv / tv_mul: ragged batches, utterance b's valid input rows are tv[b] * tv_mul (ConvGemmArgs::tv; NULL = all)
 int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
-             hipStream_t s, const char* site = "", const int* tv = nullptr, int tv_mul = 1) {
+             hipStream_t s, const char* site = "", const int* tv = nullptr, int tv_mul = 1,
+             const DLayerProj* proj = nullptr) {
   prof_site(site);
   const Tuning& tu = tuning();
   // conv_gemm3's register epilogues (gemm3_direct mask, gemm3.hip) stay off inside the DiffSVC sampler unless
@@ -742,6 +746,9 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
       }
   }
   // the DiffSVC dilated conv + gate: the weight-stationary row stream (gate_ws.hip) where it fits, else conv_gemm4
+  // with proj: the whole residual layer in one launch (dlayer.hip), or kNotFused
+  if (proj) return (variant == 15 && pair && tu.dlayer && dlayer_fits(a, e)) ? dlayer(a, e, s, proj) : kNotFused;
+  if (variant == 15 && pair && tu.dlayer && dlayer_fits(a, e)) return dlayer(a, e, s, nullptr);
   if (variant == 15 && pair && tu.gate_ws && gate_ws_fits(a, e)) return gate_ws(a, e, s);
   if (variant == 15 && pair) variant = 24;
   // The skip-sum GEMM of a sampler sub-batch (K = 20 x 384, M <= 20 k rows) takes conv_gemm3's 256 x 128 tile although
@@ -2131,6 +2138,7 @@ struct DenoiseBufs {
   size_t g_ls;   // elements between layers of g16, also layer-major [NL][rows_total][C]: the gate GEMM writes and the
                  // residual GEMM reads one contiguous block; the skip GEMM reads the NL blocks as NL "taps" whose row
                  // shift is the layer stride (tap_mul = rows_total)
+  f16* y16b;     // [rows][C] the high half's second buffer (the fused layer writes the next layer's input there)
 };
 
 
@@ -2152,6 +2160,9 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
   if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
+  // the split residual stream's high half: in place (y16) through gate + res_proj; with the fused layer (dlayer.hip,
+  // tune.dlayer) a layer reads it as its rows' halo while it writes the next, so it alternates between y16 and y16b
+  f16* hi = bb.y16;
   for (int i = 0; i < NL; ++i) {
     EpiArgs g = epi();
     g.kind = EPI_GATE;
@@ -2159,7 +2170,20 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     g.ld_cp = 2 * C;
     g.y16 = bb.g16 + (size_t)i * bb.g_ls;
     g.ldy16 = C;
-    if ((st = run_gemm(c->dil[i], bb.y16, C, C, B, T, T, g, s, "diffsvc.dilated", tv, 1))) return st;
+    if (i + 1 < NL && tuning().dlayer && C == 384 && c->outres[i].Wfrag && c->outres[i].N == C &&
+        c->outres[i].K == C && bb.y16b) {
+      f16* hi_next = hi == bb.y16 ? bb.y16b : bb.y16;
+      const DLayerProj pr{c->outres[i].Wfrag, c->outres[i].bias, dp + (size_t)i * C, dp + (size_t)(i + 1) * C,
+                          hi_next, bb.lo16};
+      prof_site("diffsvc.layer");
+      st = run_gemm(c->dil[i], hi, C, C, B, T, T, g, s, "diffsvc.layer", tv, 1, &pr);
+      if (st == SVC_OK) {
+        hi = hi_next;
+        continue;
+      }
+      if (st != kNotFused) return st;
+    }
+    if ((st = run_gemm(c->dil[i], hi, C, C, B, T, T, g, s, "diffsvc.dilated", tv, 1))) return st;
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
     // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step):
     // x_i = (y16 + lo16) - dproj_i, and x_{i+1} + dproj_{i+1} goes back split into y16 / lo16
@@ -2167,7 +2191,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
       // weight-stationary row stream (res_proj.hip), bit-identical to the tiled GEMM below
       prof_site("diffsvc.outproj");
       if ((st = res_proj(bb.g16 + (size_t)i * bb.g_ls, c->outres[i].Wfrag, c->outres[i].bias,
-                         dp + (size_t)i * C, dp + (size_t)(i + 1) * C, 1.41421356237309515f, bb.y16, bb.lo16, rows,
+                         dp + (size_t)i * C, dp + (size_t)(i + 1) * C, 1.41421356237309515f, hi, bb.lo16, rows,
                          c->outres[i].bf16,
                          tuning().res_proj > 1 ? tuning().res_proj : (tuning().sampler_streams == 1 ? -2 : 0), s)))
         return st;
@@ -2176,11 +2200,11 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     EpiArgs r = epi();
     r.ld_acc = C;
     r.acc_div = 1.41421356237309515f;
-    r.acc16_hi = bb.y16;
+    r.acc16_hi = hi;
     r.acc16_lo = bb.lo16;
     r.acc_sub = dp + (size_t)i * C;
     r.lo16 = bb.lo16;
-    r.out16 = bb.y16;
+    r.out16 = hi;
     r.ld16 = C;
     r.add16 = dp + (size_t)(i + 1) * C;
     if ((st = run_gemm(c->outres[i], bb.g16 + (size_t)i * bb.g_ls, C, C, B, T, T, r, s, "diffsvc.outproj"))) return st;
@@ -2234,13 +2258,14 @@ static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   WS_GET(f16, s16, rows * C * 3);  // [hi | lo | hi] when head_split
   WS_GET(f16, u16, rows * C * 3);
   WS_GET(f16, lo16, rows * C);
-  bb = DenoiseBufs{cp16, y16, g16, s16, u16, lo16, rows * 2 * C, rows * C};
+  WS_GET(f16, y16b, rows * C);
+  bb = DenoiseBufs{cp16, y16, g16, s16, u16, lo16, rows * 2 * C, rows * C, y16b};
   return SVC_OK;
 }
 
 static size_t denoise_bytes(svc_ctx* c, int B, int T) {
   const size_t rows = (size_t)B * T, C = c->C;
-  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * 2 * 8 + 24 * 4096;
+  return rows * c->n_layers * 2 * C * 2 + rows * c->n_layers * C * 2 + rows * C * 2 * 9 + 26 * 4096;
 }
 
 static int project_cond(svc_ctx* c, const float* cond, int B, int T, const DenoiseBufs& bb, hipStream_t s) {
@@ -2374,7 +2399,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
     const size_t r = u.r0;
     const int C = c->C;
     return DenoiseBufs{bb.cp16 + r * 2 * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * 3 * C, bb.u16 + r * 3 * C,
-                       bb.lo16 + r * C, bb.cp_ls, bb.g_ls};
+                       bb.lo16 + r * C, bb.cp_ls, bb.g_ls, bb.y16b ? bb.y16b + r * C : nullptr};
   };
   SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
   for (int h = 0; h < S && S > 1; ++h) SVC_HIP_CHECK(hipStreamWaitEvent(sub[h].s, c->ev_fork, 0));
@@ -2897,9 +2922,9 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
   SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24 ||
                   (variant == 30 && epi_kind == 6 && N == 384 && Cin == 384 && taps == 1) ||
-                  (variant == 40 && epi_kind == 1 && N == 768 && Cin == 384 && taps == 3),
-              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap; 40: gate_ws, gate "
-              "epilogue, N = 768, Cin = 384, 3 taps)", variant);
+                  ((variant == 40 || variant == 41) && epi_kind == 1 && N == 768 && Cin == 384 && taps == 3),
+              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap; 40 / 41: gate_ws / "
+              "dlayer, gate epilogue, N = 768, Cin = 384, 3 taps)", variant);
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float *bias, *R = nullptr;
@@ -2945,7 +2970,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   if (variant == 30) {
     SVC_HIP_CHECK(hipMalloc(&Wf, res_proj_pack_elems() * sizeof(f16)));
     st = res_proj_pack(W, Kpad, Wf, 0);  // (on failure: no launches below, the buffers are freed at the end)
-  } else if (variant == 40) {
+  } else if (variant == 40 || variant == 41) {
     SVC_HIP_CHECK(hipMalloc(&Wf, gate_ws_pack_elems() * sizeof(f16)));
     st = gate_ws_pack(W, Kpad, Wf, 0);
     a.Wfrag = Wf;
@@ -2965,6 +2990,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
     if (variant == 30) return res_proj(X, Wf, bias, bias, bias, e.acc_div, Y, reinterpret_cast<f16*>(R), M, false, 0, 0);
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
     if (variant == 40) return gate_ws(a, e, 0);
+    if (variant == 41) return dlayer(a, e, 0, nullptr);
     return conv_gemm3(a, e, zero_page(), variant - 10, 0);
   };
   for (int w = 0; w < 2 && !st; ++w) st = run();

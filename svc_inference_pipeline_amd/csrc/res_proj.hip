@@ -106,23 +106,8 @@ __device__ __forceinline__ void rp_wait_tile(int t) {
 }
 
 // RP_D: ring slots (tiles); DMAs run RP_D - 1 tiles ahead
-// x / sqrt(2) (f32 sqrt(2)) exactly as the IEEE division rounds it, in one multiply and two FMAs (q0 = x r,
-// e = x - q0 sqrt(2) exactly, q0 + e r): equal to the division bit for bit for every float x with 2^-100 <= |x| < inf
-// (all 2^32 inputs checked against x86 fmaf / division; the differing inputs are |x| <= 2.2e-32 and +-inf). Those
-// lanes take the division, behind a branch no wave takes in practice. Replaces the ~10-instruction division sequence
-// (v_div_scale x2, v_rcp, 4 FMAs, v_div_fmas, v_div_fixup) of the epilogue's four elements per lane.
-constexpr float RP_SQRT2 = 1.41421356237309515f;
-__device__ __forceinline__ float rp_div_sqrt2(float x) {
-  constexpr float r = 1.0f / RP_SQRT2;
-  float q;
-  if (__builtin_expect(fabsf(x) >= 0x1p-100f && fabsf(x) <= 3.402823466e38f, 1)) {
-    const float q0 = x * r;
-    q = fmaf(fmaf(-q0, RP_SQRT2, x), r, q0);
-  } else {
-    q = x / RP_SQRT2;  // (NaN too) the IEEE division for this lane
-  }
-  return q;
-}
+constexpr float RP_SQRT2 = SQRT2_F;
+__device__ __forceinline__ float rp_div_sqrt2(float x) { return div_sqrt2_exact(x); }
 
 // 101-104 VGPRs as built (keep it at or under 104): three waves per SIMD (312 registers) then fit beside one gate GEMM
 // workgroup (184), which is what
