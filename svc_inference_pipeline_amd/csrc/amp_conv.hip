@@ -37,7 +37,11 @@ template <int C>
 struct AmpCfg {
   static constexpr int BT = C <= 48 ? 256 : 128;    // output rows per workgroup (halo share of the act work)
   static constexpr int MAXP = 32;                   // max conv padding (k-1)/2*d supported
-  static constexpr int LDA = C == 24 ? 24 : C + 8;  // f16 row stride: 48/112/208 B, conflict-free fragment reads
+  // f16 row stride (96 / 96 / 224 B). A K-step's ds_read_b128 mixes lanes of two taps (rows tap*d apart) and CPT
+  // chunks per tap, so the bank pattern depends on the stride: modelled over k in {3,7,11}, d in {1,3,5} with the
+  // guide's 4 x 16 lane groups, the round-4 strides 24 / 56 / 104 cost 1.94 / 1.94 / 2.0 LDS cycles per ideal one,
+  // these 1.44 / 1.06 / 1.0 (r05 search; C = 24 takes 48 halves, twice its row: the image stays within 4 WGs per CU)
+  static constexpr int LDA = C == 96 ? 112 : 48;
   static constexpr int ROWS = BT + 2 * MAXP;
   static constexpr int FN = (C + 15) / 16;          // 16-column fragments
   static constexpr int A_BYTES = (ROWS + amp_run_len(C, ROWS)) * LDA * 2;  // whole runs of the largest image

@@ -324,8 +324,9 @@ struct Tuning {
   int res_proj = 1;         // DiffSVC residual projection on the weight-stationary stream (res_proj.hip; 0: conv_gemm3;
                             // > 1: that many row lanes of 2 workgroups instead of 1/2 (one sampler stream) or 3/8
                             // (several) of the CU count)
-  int gate_ws = 1;          // DiffSVC dilated conv + gate on the weight-stationary row stream (gate_ws.hip; 0: conv_gemm4)
-  int dlayer = 0;           // DiffSVC layer with the rows held still and the weights streamed (dlayer.hip)
+  int gate_ws = 1;          // DiffSVC dilated conv + gate: 1 the weight-stationary row stream (gate_ws.hip), 0 conv_gemm4,
+                            // 2 / 3 the rows held still and the weights streamed (dlayer.hip: gate alone / with the
+                            // residual projection fused, the whole layer in one launch; measured no faster, r05k)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only, A/B runs)
   void from_env();
   bool set(const char* name, double v);  // false: unknown name ("reset" restores the creation-time values)

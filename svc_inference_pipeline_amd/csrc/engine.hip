@@ -121,6 +121,10 @@ int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, c
              f16* lo, int M, bool bf16, int lanes_cap, hipStream_t s);
 int res_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
 size_t res_proj_pack_elems();
+int mel_proj(const f16* x, int ldx, const f16* Wf, const float* bias, const float* add, f16* hi, f16* lo, int M,
+             bool bf16, hipStream_t s);
+int mel_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
+size_t mel_proj_pack_elems();
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
               int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
               bool bf16);
@@ -331,7 +335,7 @@ static int* tuning_field(T& t, const char* name) {
               {"whisper_streams", &t.whisper_streams}, {"sampler_streams", &t.sampler_streams},
               {"vocoder_streams", &t.vocoder_streams}, {"diff_head", &t.diff_head},
               {"amp_maxc", &t.amp_maxc},               {"res_proj", &t.res_proj},
-              {"gate_ws", &t.gate_ws},                 {"dlayer", &t.dlayer}};
+              {"gate_ws", &t.gate_ws}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) return it.v;
   return nullptr;
@@ -339,7 +343,7 @@ static int* tuning_field(T& t, const char* name) {
 
 void Tuning::from_env() {
   for (const char* name : {"gemm_variant", "gemm3_direct", "whisper_streams", "sampler_streams", "vocoder_streams",
-                           "diff_head", "amp_maxc", "res_proj", "gate_ws", "dlayer"}) {
+                           "diff_head", "amp_maxc", "res_proj", "gate_ws"}) {
     std::string env = "SVC_";
     for (const char* q = name; *q; ++q) env += (char)toupper((unsigned char)*q);
     if (const char* v = getenv(env.c_str())) *tuning_field(*this, name) = atoi(v);
@@ -747,8 +751,8 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   }
   // the DiffSVC dilated conv + gate: the weight-stationary row stream (gate_ws.hip) where it fits, else conv_gemm4
   // with proj: the whole residual layer in one launch (dlayer.hip), or kNotFused
-  if (proj) return (variant == 15 && pair && tu.dlayer && dlayer_fits(a, e)) ? dlayer(a, e, s, proj) : kNotFused;
-  if (variant == 15 && pair && tu.dlayer && dlayer_fits(a, e)) return dlayer(a, e, s, nullptr);
+  if (proj) return (variant == 15 && pair && tu.gate_ws == 3 && dlayer_fits(a, e)) ? dlayer(a, e, s, proj) : kNotFused;
+  if (variant == 15 && pair && tu.gate_ws >= 2 && dlayer_fits(a, e)) return dlayer(a, e, s, nullptr);
   if (variant == 15 && pair && tu.gate_ws && gate_ws_fits(a, e)) return gate_ws(a, e, s);
   if (variant == 15 && pair) variant = 24;
   // The skip-sum GEMM of a sampler sub-batch (K = 20 x 384, M <= 20 k rows) takes conv_gemm3's 256 x 128 tile although
@@ -1084,6 +1088,15 @@ int build_mapper(svc_ctx* c) {
   GETP(mpw, q + "mel_preprocess.projection.weight", C, nmel, 1);
   GETP(mpb, q + "mel_preprocess.projection.bias", C);
   if ((st = pack_conv1d(c, c->melpre, mpw->host, mpb->host, C, nmel, 1, (int)round_up(nmel, 8), 1, 0, 1))) return st;
+  if (C == 384 && c->melpre.Kpad == 128 && c->melpre.K <= 128) {  // mel_proj's shape: W_mel in its fragment order
+    void* wf = nullptr;
+    SVC_HIP_CHECK(hipMalloc(&wf, mel_proj_pack_elems() * sizeof(f16)));
+    c->allocs.push_back(wf);
+    c->weight_bytes += (int64_t)(mel_proj_pack_elems() * sizeof(f16));
+    c->melpre.Wfrag = reinterpret_cast<f16*>(wf);
+    if ((st = mel_proj_pack(c->melpre.W, c->melpre.Kpad, c->melpre.Wfrag, 0))) return st;
+    SVC_HIP_CHECK(hipStreamSynchronize(0));
+  }
   GETP(p1w, q + "diffusion_embedding.projection1.weight", fc, 128);
   GETP(p1b, q + "diffusion_embedding.projection1.bias", fc);
   GETP(p2w, q + "diffusion_embedding.projection2.weight", fc, fc);
@@ -2159,9 +2172,16 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   e.out16 = bb.y16;
   e.ld16 = C;
   e.add16 = dp;  // layer 0 diffusion projection
-  if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) return st;
+  if (tuning().res_proj && c->melpre.Wfrag && ldx16 <= 128) {
+    // weight-stationary store stream (res_proj.hip mel_proj), bit-identical to the tiled GEMM
+    prof_site("diffsvc.melpre");
+    if ((st = mel_proj(x16, ldx16, c->melpre.Wfrag, c->melpre.bias, dp, bb.y16, bb.lo16, rows, c->melpre.bf16, s)))
+      return st;
+  } else if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) {
+    return st;
+  }
   // the split residual stream's high half: in place (y16) through gate + res_proj; with the fused layer (dlayer.hip,
-  // tune.dlayer) a layer reads it as its rows' halo while it writes the next, so it alternates between y16 and y16b
+  // tune.gate_ws = 3) a layer reads it as its rows' halo while it writes the next, so it alternates between y16 and y16b
   f16* hi = bb.y16;
   for (int i = 0; i < NL; ++i) {
     EpiArgs g = epi();
@@ -2170,7 +2190,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     g.ld_cp = 2 * C;
     g.y16 = bb.g16 + (size_t)i * bb.g_ls;
     g.ldy16 = C;
-    if (i + 1 < NL && tuning().dlayer && C == 384 && c->outres[i].Wfrag && c->outres[i].N == C &&
+    if (i + 1 < NL && tuning().gate_ws == 3 && C == 384 && c->outres[i].Wfrag && c->outres[i].N == C &&
         c->outres[i].K == C && bb.y16b) {
       f16* hi_next = hi == bb.y16 ? bb.y16b : bb.y16;
       const DLayerProj pr{c->outres[i].Wfrag, c->outres[i].bias, dp + (size_t)i * C, dp + (size_t)(i + 1) * C,

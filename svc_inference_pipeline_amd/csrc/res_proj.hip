@@ -276,4 +276,170 @@ int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, c
   return SVC_OK;
 }
 
+// ---------------------------------------------------------------------------- input projection (round 5)
+// The denoiser's first step (modules/diffsvc.py:299-300, mel_preprocess: Conv1d(n_mel -> 384, 1) then ReLU) writes
+// the split residual stream's first value: h = relu(x W_mel^T + b), hi = f16(h + dproj_0), lo = f16((h + dproj_0) - hi)
+// (engine.hip denoise). K = 100 against 1536 B of hi / lo out per row: a store stream of 52 MB per sampler call, which
+// conv_gemm3's 128 x 128 tiles ran at MFMA busy 0.04 with 36 VALU per MFMA (24 us per launch).
+// Here one workgroup per CU walks 16-row tiles:
+//   * W_mel (384 x 128 f16, zero past k = 100) lives in VGPRs: each of 12 compute waves holds its 32 output columns as
+//     2 x 4 MFMA fragments (32 VGPRs), loaded once;
+//   * a 13th wave only loads: each tile's x rows (16 x ldx f16, one contiguous span) by LDS-DMA as four 1-KiB pieces
+//     into a ring of MP_D slots, MP_D - 1 tiles ahead (rows past M read 0). Its own counted vmcnt retires a tile before
+//     the barrier the compute waves pass to read it, and the compute waves' vmcnt holds only their stores, which so
+//     never delay a load wait;
+//   * per tile a compute wave runs 8 swapped v_mfma_f32_16x16x32 (a lane's accumulator holds 4 consecutive columns of
+//     one row; k chunks past the row's ldx / 8 read as zero, as the padded tile does), swaps its two column blocks'
+//     values between lane rows (8 consecutive columns per lane) and stores hi / lo, 16 B per lane and half.
+// (A first form gave each workgroup one 64-row span and no ring: 21.1 us against conv_gemm3's 25.3, r05p.)
+// Same 32-deep K order and epilogue arithmetic as conv_gemm3 with its LDS-staged epilogue: bit-identical
+// (tests/test_gpu_stages.py test_res_proj_bit_identical, switch res_proj).
+constexpr int MP_NW = 12, MP_NT = 64 * (MP_NW + 1);  // compute waves (32 output columns each) + the loader wave
+constexpr int MP_D = 4;                              // ring slots (16-row tiles)
+constexpr int MP_SLOT = 4096;                        // 16 rows x ldx f16 (ldx <= 128): four 1-KiB DMA pieces
+
+struct MelProjArgs {
+  const f16* x;       // [M][ldx] sampler input in the 16-bit operand format
+  const f16* Wf;      // W_mel in fragment order (mel_proj_pack)
+  const float* bias;  // [384]
+  const float* add;   // dproj_0 [384]
+  f16* hi;            // [M][384] split residual stream, written
+  f16* lo;
+  int M, ldx;
+  int iters;          // tiles per workgroup: ceil(ceil(M / 16) / gridDim.x)
+};
+
+template <bool BF>
+__global__ __launch_bounds__(MP_NT, 1) void mel_proj_kernel(MelProjArgs p) {
+  using O = Op16<BF>;
+  extern __shared__ __align__(16) unsigned char smm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int G = gridDim.x;
+  const int rowb = p.ldx * 2;  // bytes per x row
+  if (wave == MP_NW) {         // ---- loader
+    auto issue = [&](int t) {  // tile t of this workgroup into slot t % MP_D (tiles past the end read zeros)
+      const int row0 = (blockIdx.x + t * G) * 16;
+      const bool live = row0 < p.M;
+      const u32x4 d = rp_desc(p.x + (live ? (int64_t)row0 * p.ldx : 0), live ? (int64_t)(p.M - row0) * rowb : 0);
+      unsigned char* slot = smm + (t % MP_D) * MP_SLOT;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) rp_dma(d, (uint32_t)(v * 1024 + lane * 16), slot + v * 1024);
+    };
+#pragma unroll
+    for (int t = 0; t < MP_D - 1; ++t) issue(t);
+    for (int t = 0; t < p.iters; ++t) {
+      rp_vmwait<(MP_D - 2) * 4>();  // tile t landed (tiles t + 1 .. t + MP_D - 2 may be in flight)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // every compute wave finished tile t - 1: slot (t - 1) % MP_D is free
+      __builtin_amdgcn_sched_barrier(0);
+      issue(t + MP_D - 1);
+    }
+    rp_vmwait<0>();  // (the DMAs of tiles past the end land before the workgroup's LDS is released)
+    return;
+  }
+  // ---- compute waves
+  const int fr = lane & 15, fk = lane >> 4;
+  const int qmax = p.ldx / 8;  // 16-B chunks per x row
+  half8 w[2][4];
+  const f16* wf = p.Wf + (size_t)wave * 8 * 512 + lane * 8;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) w[j][kc] = *reinterpret_cast<const half8*>(wf + (j * 4 + kc) * 512);
+  float4 bi[2], ad[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = 32 * wave + 16 * j + 4 * fk;
+    bi[j] = *reinterpret_cast<const float4*>(p.bias + n);
+    ad[j] = *reinterpret_cast<const float4*>(p.add + n);
+  }
+  const __amdgpu_buffer_rsrc_t sh = rp_rsrc(p.hi, (int64_t)p.M * RP_C * 2), sl = rp_rsrc(p.lo, (int64_t)p.M * RP_C * 2);
+  const half8 zero = {};
+  for (int t = 0; t < p.iters; ++t) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // the loader retired tile t
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned char* slot = smm + (t % MP_D) * MP_SLOT;
+    floatx4 acc[2] = {floatx4{0.f, 0.f, 0.f, 0.f}, floatx4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int kc = 0; kc < 4; ++kc) {
+      const int q = kc * 4 + fk;
+      half8 a = *reinterpret_cast<const half8*>(slot + fr * rowb + (q < qmax ? q : 0) * 16);
+      if (q >= qmax) a = zero;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j] = O::mfma(w[j][kc], a, acc[j]);  // acc[r] = C[row fr][n + r]
+    }
+    const uint32_t rowo = (uint32_t)((blockIdx.x + t * G) * 16 + fr) * (RP_C * 2);
+    union { uint2 u; f16 h[4]; } ph[2], pl[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float b4[4] = {bi[j].x, bi[j].y, bi[j].z, bi[j].w}, a4[4] = {ad[j].x, ad[j].y, ad[j].z, ad[j].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {  // conv_gemm3's LDS-staged epilogue: relu(acc + bias) + add16, split
+        const float wv = fmaxf(acc[j][r] + b4[r], 0.f) + a4[r];
+        ph[j].h[r] = O::enc(wv);
+        pl[j].h[r] = O::enc_lo(wv - O::dec(ph[j].h[r]));
+      }
+    }
+    // the two 16-column blocks' values swapped between lane rows fk and fk ^ 1 (same output row): each lane then holds
+    // 8 consecutive columns, and a store covers 16 rows x 64 B (conv_gemm3's block-pair epilogue)
+    const auto hx = __builtin_amdgcn_permlane16_swap(ph[0].u.x, ph[1].u.x, false, false);
+    const auto hy = __builtin_amdgcn_permlane16_swap(ph[0].u.y, ph[1].u.y, false, false);
+    const auto lx = __builtin_amdgcn_permlane16_swap(pl[0].u.x, pl[1].u.x, false, false);
+    const auto ly = __builtin_amdgcn_permlane16_swap(pl[0].u.y, pl[1].u.y, false, false);
+    const uint32_t vo = rowo + (uint32_t)(32 * wave + 8 * (2 * (fk & 1) + (fk >> 1))) * 2;
+    // rows past M fall outside the descriptor's range and are dropped
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{hx[0], hy[0], hx[1], hy[1]}, sh, vo, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{lx[0], ly[0], lx[1], ly[1]}, sl, vo, 0, 0);
+  }
+}
+
+// W_mel (packed [>= 384][ldw], W[n][k], zero for k >= K) -> fragment order Wf[wave][j][kc][lane][8]
+__global__ void mel_proj_pack_kernel(const f16* __restrict__ W, int ldw, f16* __restrict__ Wf) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= RP_C * 128 / 8) return;
+  const int lane = i & 63, kc = (i >> 6) & 3, j = (i >> 8) & 1, wave = i >> 9;
+  const int n = 32 * wave + 16 * j + (lane & 15), k = kc * 32 + (lane >> 4) * 8;
+  *reinterpret_cast<uint4*>(Wf + (size_t)i * 8) = *reinterpret_cast<const uint4*>(W + (size_t)n * ldw + k);
+}
+
+int mel_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s) {
+  SVC_REQUIRE(ldw >= 128 && ldw % 8 == 0 && ((uintptr_t)W & 15) == 0 && ((uintptr_t)Wf & 15) == 0,
+              "mel_proj_pack: ldw %d", ldw);
+  hipLaunchKernelGGL(mel_proj_pack_kernel, dim3(cdiv(RP_C * 128 / 8, 256)), dim3(256), 0, s, W, ldw, Wf);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+size_t mel_proj_pack_elems() { return (size_t)RP_C * 128; }
+
+// M rows of the input projection (K = n_mel <= 128 channels of x at row stride ldx, ldx % 8 == 0, ldx <= 128; the
+// columns K .. ldx - 1 of x hold zeros and W is zero past K) into the split residual stream hi / lo [M][384]
+int mel_proj(const f16* x, int ldx, const f16* Wf, const float* bias, const float* add, f16* hi, f16* lo, int M,
+             bool bf16, hipStream_t s) {
+  SVC_REQUIRE(M >= 0 && Wf && ldx >= 8 && ldx <= 128 && ldx % 8 == 0, "mel_proj: M %d ldx %d", M, ldx);
+  if (M == 0) return SVC_OK;
+  SVC_REQUIRE((int64_t)M * RP_C * 2 < (1ll << 31) - (1 << 20), "mel_proj: %d rows exceed the 32-bit buffer range", M);
+  SVC_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)Wf & 15) == 0 && ((uintptr_t)hi & 15) == 0 &&
+                  ((uintptr_t)lo & 15) == 0,
+              "mel_proj: 16-B alignment");
+  static int ncu_dev[16] = {};  // the CU count (one workgroup per CU) per device
+  int dev = 0;
+  SVC_HIP_CHECK(hipGetDevice(&dev));
+  SVC_REQUIRE(dev >= 0 && dev < 16, "mel_proj: device %d", dev);
+  int& ncu = ncu_dev[dev];
+  if (!ncu) SVC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  const int tiles = cdiv(M, 16), grid = std::min(tiles, ncu);
+  MelProjArgs a{x, Wf, bias, add, hi, lo, M, ldx, cdiv(tiles, grid)};
+  const void* fn = bf16 ? (const void*)mel_proj_kernel<true> : (const void*)mel_proj_kernel<false>;
+  const int lds = MP_D * MP_SLOT;
+  if (int st = ensure_dyn_lds(fn, lds)) return st;
+  const int tok = prof_begin("mel_proj<16x384>", 2.0 * M * RP_C * ldx, (double)M * (ldx * 2 + RP_C * 4), s);
+  void* args[] = {&a};
+  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3(grid), dim3(MP_NT), args, lds, s));
+  prof_end(tok, s);
+  SVC_LAUNCH_CHECK();
+  return SVC_OK;
+}
+
 }  // namespace svc

@@ -210,9 +210,9 @@ def test_dlayer_gate_bit_identical(engine, B, T, frames, tune):
     rng = np.random.default_rng(B * 31 + T)
     cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
     x = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
-    tune(engine, dlayer=0)
+    tune(engine, gate_ws=1)
     ref = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
-    tune(engine, dlayer=1)
+    tune(engine, gate_ws=2)
     _lib.profile_enable(True)
     try:
         out = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
