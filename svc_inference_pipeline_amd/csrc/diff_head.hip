@@ -1,7 +1,8 @@
 // Fused DiffSVC head for gfx950 (modules/diffsvc.py:311-321) after the skip sum, one launch per 128-row tile:
 //   GEMM A  u = relu(s . W_sp + b_sp): s = the split-fp16 skip sum [hi | lo | hi] (K = 1152), N = 384, through a
 //           4-slot ring of 32-deep K-steps (A 128 x 64 B + B 384 x 64 B = 32 KiB per slot, three steps ahead: one
-//           tile per CU, so the step time is the DMA latency over the steps in flight);
+//           tile per CU, so the step time is the DMA latency over the steps in flight); a step's DMAs are issued
+//           between its MFMAs (round 5: 58.5 -> 57.0 us per full-batch launch, r05v);
 //   GEMM B  eps = [u_hi | u_lo | u_hi] . W_out + b_out, N = 100 (packed rows to 128): u_hi as an f16 image in LDS
 //           (over GEMM A's ring), u_lo packed in registers and written over the image for the last third, so the
 //           138 MB split-fp16 intermediate of a full-batch call never reaches HBM; W_out K-steps through a 4-slot ring
@@ -89,19 +90,27 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
   }
   const int orow = wave * 16 + (lane >> 2);  // GEMM B weight rows (128)
   const f16* o_p = p.Wout + (int64_t)orow * LDS_ + dl_sw64(orow, lane & 3) * 8;
+  // A K-step's DMAs (GEMM A: 1 A piece + 3 B pieces per wave; GEMM B: 1 piece), issued between the step's MFMAs (below).
+  // Steps past the end DMA the zero page into the free slot, so every step's vmcnt count is the same.
+  auto dmaA = [&](int s, int v) __attribute__((always_inline)) {  // v = 0: A piece, 1..3: B pieces
+    unsigned char* st = sm + (s & 3) * DH_SLOT_A;
+    const bool live = s < DH_S1;
+    if (v == 0)
+      dl_dma(live && a_p ? (const void*)(a_p + s * 32) : (const void*)zsrc, st + wave * 1024);
+    else
+      dl_dma(live ? (const void*)(b_p[v - 1] + s * 32) : (const void*)zsrc, st + 8192 + (wave * 3 + v - 1) * 1024);
+  };
   auto issueA = [&](int s_in) {
     int s;
     asm volatile("s_mov_b32 %0, %1" : "=s"(s) : "s"(s_in));
-    unsigned char* st = sm + (s & 3) * DH_SLOT_A;
-    dl_dma(a_p ? (const void*)(a_p + s * 32) : (const void*)zsrc, st + wave * 1024);
 #pragma unroll
-    for (int v = 0; v < 3; ++v) dl_dma(b_p[v] + s * 32, st + 8192 + (wave * 3 + v) * 1024);
+    for (int v = 0; v < 4; ++v) dmaA(s, v);
   };
   auto issueB = [&](int s_in) {  // GEMM B step s reads weight K-step 0-11, 24-35, 12-23 (see GEMM B)
     int s;
     asm volatile("s_mov_b32 %0, %1" : "=s"(s) : "s"(s_in));
     const int ws = s < DL_KS2 ? s : (s < 2 * DL_KS2 ? s + DL_KS2 : s - DL_KS2);
-    dl_dma(o_p + ws * 32, sm + DH_RING_B + (s & 3) * 8192 + wave * 1024);
+    dl_dma(s < DH_S1 ? (const void*)(o_p + ws * 32) : (const void*)zsrc, sm + DH_RING_B + (s & 3) * 8192 + wave * 1024);
   };
 
   // ---- GEMM A
@@ -116,11 +125,15 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
   issueA(0);
   issueA(1);
   issueA(2);
+  // Each step's four DMAs go between its MFMAs (one after every six), not in a burst after the barrier: both waves of a
+  // SIMD leave the barrier together, and an LDS-DMA costs its wave ~60 issue cycles among MFMAs but 100-185 in a
+  // burst (MI355X_MICROARCH.md), so the burst had left the matrix pipe idle (~0.75 us per step, round 5)
+#pragma unroll 1
   for (int s = 0; s < DH_S1; ++s) {
-    // step s landed (s + 1, s + 2 may be in flight: 4 DMAs each)
-    if (s + 2 < DH_S1) dl_vmwait<8>(); else if (s + 1 < DH_S1) dl_vmwait<4>(); else dl_vmwait<0>();
-    dl_barrier();  // every wave finished step s - 1: its slot (s + 3) & 3 is free
-    if (s + 3 < DH_S1) issueA(s + 3);
+    dl_vmwait<8>();  // step s landed (steps s + 1, s + 2 may be in flight: 4 DMAs each)
+    dl_barrier();    // every wave finished step s - 1: its slot (s + 3) & 3 is free
+    int sn;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(sn) : "s"(s + 3));
     const unsigned char* A = sm + (s & 3) * DH_SLOT_A;
     const unsigned char* Bm = A + 8192;
     half8 af[4], bf[6];
@@ -136,11 +149,19 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < 6; ++j) acc[i][j] = O::mfma(bf[j], af[i], acc[i][j]);
+      dmaA(sn, i);
+    }
     __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // six MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one DMA
+    }
   }
+  dl_vmwait<0>();  // the dummy DMAs of the last steps land before the image overlays the ring
   // u = relu(acc + b_sp); hi = f16(u) goes to the LDS image, lo = f16(u - hi) stays in registers (packed, half the
   // registers of u), so GEMM A's f32 accumulators die here
   const int nb = wn * 96 + fk * 4;
@@ -190,10 +211,11 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
         }
       }
     }
-    if (s + 2 < DH_S1) dl_vmwait<2>(); else if (s + 1 < DH_S1) dl_vmwait<1>(); else dl_vmwait<0>();
+    dl_vmwait<2>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's image writes
     dl_barrier();
-    if (s + 3 < DH_S1) issueB(s + 3);
+    int sn;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(sn) : "s"(s + 3));
     const int k2 = s % DL_KS2;  // K-step within the 384-channel image
     const unsigned char* Bm = sm + DH_RING_B + (s & 3) * 8192;
     half8 af[4], bf[2];
@@ -210,12 +232,18 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
     }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
         acc2[i][j] = O::mfma(bf[j], af[i], acc2[i][j]);
+      if (i == 1) issueB(sn);
+    }
     __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
   }
+  dl_vmwait<0>();  // the dummy DMAs of the last steps land before the workgroup's LDS is released
   // ---- eps = acc + b_out, columns < n_out
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
