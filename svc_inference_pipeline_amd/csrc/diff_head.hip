@@ -1,8 +1,9 @@
 // Fused DiffSVC head for gfx950 (modules/diffsvc.py:311-321) after the skip sum, one launch per 128-row tile:
 //   GEMM A  u = relu(s . W_sp + b_sp): s = the split-fp16 skip sum [hi | lo | hi] (K = 1152), N = 384, through a
 //           4-slot ring of 32-deep K-steps (A 128 x 64 B + B 384 x 64 B = 32 KiB per slot, three steps ahead: one
-//           tile per CU, so the step time is the DMA latency over the steps in flight); a step's DMAs are issued
-//           between its MFMAs (round 5: 58.5 -> 57.0 us per full-batch launch, r05v);
+//           tile per CU, so the step time is the DMA latency over the steps in flight); software-pipelined: a step's
+//           MFMAs run on fragments read during the previous step, with the next step's reads and DMAs between them
+//           (round 5: 58.5 -> 57.0 -> 56.2 us per full-batch launch, r05v / r05x);
 //   GEMM B  eps = [u_hi | u_lo | u_hi] . W_out + b_out, N = 100 (packed rows to 128): u_hi as an f16 image in LDS
 //           (over GEMM A's ring), u_lo packed in registers and written over the image for the last third, so the
 //           138 MB split-fp16 intermediate of a full-batch call never reaches HBM; W_out K-steps through a 4-slot ring
@@ -125,41 +126,76 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
   issueA(0);
   issueA(1);
   issueA(2);
-  // Each step's four DMAs go between its MFMAs (one after every six), not in a burst after the barrier: both waves of a
-  // SIMD leave the barrier together, and an LDS-DMA costs its wave ~60 issue cycles among MFMAs but 100-185 in a
-  // burst (MI355X_MICROARCH.md), so the burst had left the matrix pipe idle (~0.75 us per step, round 5)
-#pragma unroll 1
-  for (int s = 0; s < DH_S1; ++s) {
-    dl_vmwait<8>();  // step s landed (steps s + 1, s + 2 may be in flight: 4 DMAs each)
-    dl_barrier();    // every wave finished step s - 1: its slot (s + 3) & 3 is free
-    int sn;
-    asm volatile("s_mov_b32 %0, %1" : "=s"(sn) : "s"(s + 3));
+  // Software-pipelined K-loop: step s's MFMAs run from fragments read during step s - 1, and between them go step
+  // s + 1's fragment reads and step s + 3's four DMAs (one after every six MFMAs). Before, each step read its own
+  // fragments after the barrier and waited on them, and both waves of a SIMD issued their DMAs in one burst (an
+  // LDS-DMA costs its wave ~60 issue cycles among MFMAs but 100-185 in a burst, MI355X_MICROARCH.md): the matrix pipe
+  // idled ~0.75 us per step (round 5). The wait before step s retires step s + 1 (one DMA step less in flight).
+  half8 af[2][4], bf[2][6];
+  auto readA = [&](int s, half8 (&a4)[4], half8 (&b6)[6], int part) __attribute__((always_inline)) {
     const unsigned char* A = sm + (s & 3) * DH_SLOT_A;
     const unsigned char* Bm = A + 8192;
-    half8 af[4], bf[6];
+    if (part == 0 || part < 0)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = wm * 64 + i * 16 + fr;
-      af[i] = *reinterpret_cast<const half8*>(A + row * 64 + (dl_sw64(row, fk) << 4));
-    }
+      for (int j = 0; j < 3; ++j) {
+        const int row = wn * 96 + j * 16 + fr;
+        b6[j] = *reinterpret_cast<const half8*>(Bm + row * 64 + (dl_sw64(row, fk) << 4));
+      }
+    if (part == 1 || part < 0)
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int row = wn * 96 + j * 16 + fr;
-      bf[j] = *reinterpret_cast<const half8*>(Bm + row * 64 + (dl_sw64(row, fk) << 4));
-    }
+      for (int j = 3; j < 6; ++j) {
+        const int row = wn * 96 + j * 16 + fr;
+        b6[j] = *reinterpret_cast<const half8*>(Bm + row * 64 + (dl_sw64(row, fk) << 4));
+      }
+    if (part == 2 || part < 0)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        a4[i] = *reinterpret_cast<const half8*>(A + row * 64 + (dl_sw64(row, fk) << 4));
+      }
+    if (part == 3 || part < 0)
+#pragma unroll
+      for (int i = 2; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        a4[i] = *reinterpret_cast<const half8*>(A + row * 64 + (dl_sw64(row, fk) << 4));
+      }
+  };
+  auto stepA = [&](int s, half8 (&ca)[4], half8 (&cb)[6], half8 (&na)[4], half8 (&nb6)[6])
+                   __attribute__((always_inline)) {
+    dl_vmwait<4>();  // step s + 1 landed (step s + 2 may be in flight)
+    dl_barrier();    // ... for every wave; every wave finished reading step s - 1: its slot (s + 3) & 3 is free
+    int sn;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(sn) : "s"(s + 3));
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int j = 0; j < 6; ++j) acc[i][j] = O::mfma(bf[j], af[i], acc[i][j]);
+      for (int j = 0; j < 6; ++j) acc[i][j] = O::mfma(cb[j], ca[i], acc[i][j]);
       dmaA(sn, i);
+      readA(s + 1, na, nb6, i);
     }
     __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);  // six MFMAs
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // one DMA
-    }
+    // per quarter: six MFMAs, one DMA, the next step's fragment reads (3, 3, 2, 2)
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);
+    __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+  };
+  dl_vmwait<8>();  // step 0 landed
+  dl_barrier();
+  readA(0, af[0], bf[0], -1);
+#pragma unroll 1
+  for (int s = 0; s < DH_S1; s += 2) {
+    stepA(s, af[0], bf[0], af[1], bf[1]);
+    stepA(s + 1, af[1], bf[1], af[0], bf[0]);
   }
   dl_vmwait<0>();  // the dummy DMAs of the last steps land before the image overlays the ring
   // u = relu(acc + b_sp); hi = f16(u) goes to the LDS image, lo = f16(u - hi) stays in registers (packed, half the
