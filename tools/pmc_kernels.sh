@@ -10,7 +10,7 @@ R=$(pwd); TAG=${TAG:-pmc}; O=$R/gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
 ( while sleep 30; do date +%s >> $R/gpurun_out/heartbeat; done ) &
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
-KRE=${KRE:-gate_ws_kernel|conv_gemm4_kernel|conv_gemm3_kernel|res_proj_kernel|attention_kernel|amp_conv_kernel|activation1d}
+KRE=${KRE:-gate_ws_kernel|conv_gemm4_kernel|conv_gemm3_kernel|res_proj_kernel|mel_proj_kernel|diff_head_kernel|attention_kernel|amp_conv_kernel|activation1d}
 i=0
 for set in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
            "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
