@@ -224,6 +224,11 @@ struct EpiArgs {
   // split-fp16 operand output ("fp16x3", elementwise.hip f32_to_f16x3): when > 0, out16 also receives the
   // residual lo = f16(v - hi) at column split16 + n and hi again at 2 * split16 + n
   int split16;
+  // column blocks (LDS-staged generic epilogue, out16 only): when > 0, output column n goes to block n / col_block,
+  // which starts col_block_stride elements after the previous one (the layer-major conditioner projections of all
+  // DiffSVC layers as one GEMM); a tile's columns lie in one block
+  int col_block;
+  int64_t col_block_stride;
   // split residual stream (the DiffSVC x): x + add16 is held as hi (out16 / acc16_hi, the next GEMM's operand) plus
   // lo16 = f16((x + add16) - hi), ~22 significand bits in 4 bytes. acc16_hi / acc16_lo / acc_sub: the residual read
   // as acc = (hi + lo) - acc_sub (the add16 it was stored with), in place of acc32; lo16: also write the lo half

@@ -78,7 +78,8 @@ __device__ __forceinline__ void epilogue_pass(const float* Cs, int m0, int nbase
         }
         union { uint2 u; f16 h[4]; } pk;
         pk.h[0] = O::enc(w.x); pk.h[1] = O::enc(w.y); pk.h[2] = O::enc(w.z); pk.h[3] = O::enc(w.w);
-        *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
+        const int64_t ocol = e.col_block ? (int64_t)(n / e.col_block) * e.col_block_stride + n % e.col_block : n;
+        *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + ocol) = pk.u;
         if (e.lo16) {
           union { uint2 u; f16 h[4]; } lo;
           lo.h[0] = O::enc_lo(w.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(w.y - O::dec(pk.h[1]));

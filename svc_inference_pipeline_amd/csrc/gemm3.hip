@@ -467,7 +467,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
 // the DiffSVC 3-tap store 12 %, skip sum 3 %); inside the 3-stream sampler the gate GEMMs beside them ran slower.
 static int direct_form3(const ConvGemmArgs& a, const EpiArgs& e) {
   const int mask = tuning().gemm3_direct;
-  if (e.no_reg_epi || e.kind != EPI_GENERIC || e.add_t) return G3_LDS;
+  if (e.no_reg_epi || e.col_block || e.kind != EPI_GENERIC || e.add_t) return G3_LDS;
   const bool acc16 = e.acc16_hi || e.acc16_lo || e.acc_sub || e.lo16;
   if (e.out16 && !e.out32 && !e.add_row && !e.acc32 && !acc16 && !e.add16) return (mask & 1) ? G3_F16 : G3_LDS;
   if (e.act != ACT_NONE || e.scale_cols > 0 || e.split16) return G3_LDS;
