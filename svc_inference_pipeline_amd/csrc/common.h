@@ -326,7 +326,8 @@ struct Tuning {
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
   int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip)
   int amp_maxc = 48;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none)
-  int res_proj = 1;         // DiffSVC residual projection on the weight-stationary stream (res_proj.hip; 0: conv_gemm3;
+  int res_proj = 1;         // DiffSVC residual and input projections on the weight-stationary streams (res_proj.hip
+                            // res_proj / mel_proj; 0: conv_gemm3;
                             // > 1: that many row lanes of 2 workgroups instead of 1/2 (one sampler stream) or 3/8
                             // (several) of the CU count)
   int gate_ws = 1;          // DiffSVC dilated conv + gate: 1 the weight-stationary row stream (gate_ws.hip), 0 conv_gemm4,
