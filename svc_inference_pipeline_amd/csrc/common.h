@@ -318,7 +318,7 @@ struct PlmsArgs {
 // running (tuning(), set per call by TuningScope) instead of the environment.
 struct Tuning {
   int gemm_variant = 15;    // GEMM kernel: 15 fitted choice (conv_gemm3 tile by pick3; the DiffSVC gate GEMM on
-                            // conv_gemm4 with its register gate epilogue), 10..14 a fixed conv_gemm3 tile, 20 / 24
+                            // conv_gemm4 with its register gate epilogue), 10..14 / 16 a fixed conv_gemm3 tile (16: 256 x 192), 20 / 24
                             // conv_gemm4 with the LDS-staged / register epilogue where N > 64
   int gemm3_direct = 3;     // conv_gemm3 register-epilogue forms in use (mask, gemm3.hip direct_form3)
   int whisper_streams = 1;  // Whisper encoder sub-batch streams

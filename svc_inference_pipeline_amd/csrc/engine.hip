@@ -759,7 +759,7 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
   // pick3's fit prefers narrower-M tiles alone: beside the other sampler stream it measured +1.5 % end to end (826-828
   // vs 813-818 audio-s/s in three alternating rounds, profiles/r03w_skipsum_tile_ab.txt)
   if (variant == 15 && site && strcmp(site, "diffsvc.skipsum") == 0 && (int64_t)B * T_out <= 20000) variant = 12;
-  SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24, "gemm_variant %d: 10..15, 20 or 24",
+  SVC_REQUIRE((variant >= 10 && variant <= 16) || variant == 20 || variant == 24, "gemm_variant %d: 10..16, 20 or 24",
               variant);
   // N <= 64 (the last BigVGAN up-sampling phases, 48 / 24 channels) takes conv_gemm3's 128 x 128 tile: 1.9 vs
   // 3.0 ms per step on the round-1 256 x 64 / 256 x 32 tiles (tools/ab_ups.sh), although 63-81 % of its N is padding
@@ -2937,7 +2937,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   SVC_REQUIRE(M > 0 && N > 0 && Cin % 8 == 0 && taps >= 1 && iters != 0, "gemm_bench: bad args");
   SVC_REQUIRE(epi_kind < 3 || epi_kind == 6 || variant == 24,
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
-  SVC_REQUIRE((variant >= 10 && variant <= 15) || variant == 20 || variant == 24 ||
+  SVC_REQUIRE((variant >= 10 && variant <= 16) || variant == 20 || variant == 24 ||
                   (variant == 30 && epi_kind == 6 && N == 384 && Cin == 384 && taps == 1) ||
                   ((variant == 40 || variant == 41) && epi_kind == 1 && N == 768 && Cin == 384 && taps == 3),
               "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap; 40 / 41: gate_ws / "

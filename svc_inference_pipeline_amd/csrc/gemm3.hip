@@ -37,19 +37,25 @@ namespace svc {
 template <int BM, int BN>
 struct G3 {
   static constexpr int NT = 512;
-  static constexpr int WTM = BM / 2, WTN = BN / 4;   // wave tile
+  // waves: WMW (M) x WNW (N) = 2 x 4, or 4 x 2 for BN = 192 (the BigVGAN C = 192 convs without 64 idle columns:
+  // a quadrant of 48 columns = 3 fragments)
+  static constexpr int WNW = BN % 128 == 0 ? 4 : 2, WMW = 8 / WNW;
+  static constexpr int WTM = BM / WMW, WTN = BN / WNW;  // wave tile
   static constexpr int QM = WTM / 2, QN = WTN / 2;   // quadrant (one phase)
   static constexpr int FQM = QM / 16, FQN = QN / 16; // 16x16 fragments per quadrant
   static constexpr int TILE = (BM + BN) * 128;       // bytes of one K-tile image (A rows, then B rows)
   static constexpr int RING = 2 * TILE;
   static constexpr int AH = BM / 128;                // DMA instructions per wave per A half-tile
-  static constexpr int BH = BN / 128;
+  // B half-tile: BN / 16 DMA instructions over the 8 waves: BH per wave, or (BN = 192: 12) two on waves 0-3 and one on
+  // waves 4-7 (BHL); each wave's vmcnt counts use its own number
+  static constexpr int BH = (BN / 16 + 7) / 8, BHL = (BN / 16) / 8;
   static constexpr int EP = (BM * (BN + 4) * 4 <= 163840) ? 1 : 2;
   static constexpr int LDC = BN / EP + 4;
   static constexpr int C_BYTES = BM * LDC * 4;
   static constexpr int LDS = RING > C_BYTES ? RING : C_BYTES;
   static_assert(LDS <= 163840, "LDS budget");
-  static_assert(QM % 16 == 0 && QN % 16 == 0 && QM % 8 == 0 && QN % 8 == 0 && AH >= 1 && BH >= 1, "tile shape");
+  static_assert(QM % 16 == 0 && QN % 16 == 0 && QM % 8 == 0 && QN % 8 == 0 && AH >= 1 && BHL >= 1 &&
+                    BM % 128 == 0, "tile shape");
 };
 
 // 16-B chunk swizzle of the 128-B-row LDS images: conflict-free ds_read_b128 fragment reads (16 consecutive
@@ -98,7 +104,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   extern __shared__ __align__(16) unsigned char sm3[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
+  const int wm = wave / CF::WNW, wn = wave % CF::WNW;
+  const int grp = wave >> 2;  // stagger group: one wave of each per SIMD
+  const bool bfull = CF::BH == CF::BHL || wave < 4;  // this wave issues BH (else BHL) B pieces per half-tile
 
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -146,7 +154,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int v = 0; v < CF::BH; ++v) {
-      const int u = wave + 8 * v;
+      const int u = min(wave + 8 * v, BN / 16 - 1);  // (u past the half-tile: a wave with BHL pieces, never issued)
       const int rb = half_row(8 * u, h, CF::QN, CF::WTN);
       const int row = rb + (lane >> 3);
       b_rb[h][v] = rb;
@@ -205,15 +213,22 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
     if constexpr (CP64) {
 #pragma unroll
       for (int v = 0; v < CF::BH; ++v)
-        g3_bdma(rw, kt < nk ? b_voff[h][v] : G3_OOR, (uint32_t)(kt * 128), dst + b_rb[h][v] * 128);
+        if (v < CF::BHL || bfull)
+          g3_bdma(rw, kt < nk ? b_voff[h][v] : G3_OOR, (uint32_t)(kt * 128), dst + b_rb[h][v] * 128);
     } else {
       const int koff = kt * 64;
 #pragma unroll
       for (int v = 0; v < CF::BH; ++v)
-        g3_dma(kt < nk ? (const void*)(b_p[h][v] + koff) : (const void*)zsrc, dst + b_rb[h][v] * 128);
+        if (v < CF::BHL || bfull)
+          g3_dma(kt < nk ? (const void*)(b_p[h][v] + koff) : (const void*)zsrc, dst + b_rb[h][v] * 128);
     }
   };
 
+  // a phase's wait: this wave's pieces of the two half-tiles issued after the ones to retire (2 AH + 2 B pieces)
+  auto g3_wait = [&]() __attribute__((always_inline)) {
+    if (bfull) vm_wait<2 * CF::AH + 2 * CF::BH>();
+    else vm_wait<2 * CF::AH + 2 * CF::BHL>();
+  };
   floatx4 acc[2][2][CF::FQM][CF::FQN];
 #pragma unroll
   for (int x = 0; x < 2; ++x)
@@ -260,15 +275,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
     // restage one half-tile; each wait retires the half-tiles the next phase reads (3 phases read; phase 3 none)
     if constexpr (P == 0) {
       issue_b(1, kt + 1);
-      vm_wait<2 * CF::AH + 2 * CF::BH>();
+      g3_wait();
     } else if constexpr (P == 1) {
       issue_a(1, kt + 1);
-      vm_wait<2 * CF::AH + 2 * CF::BH>();
+      g3_wait();
     } else if constexpr (P == 2) {
       issue_a(0, kt + 2);
     } else {
       issue_b(0, kt + 2);
-      vm_wait<2 * CF::AH + 2 * CF::BH>();
+      g3_wait();
     }
     g3_barrier();
     // ---- M section
@@ -297,9 +312,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   issue_a(1, 0);
   issue_a(0, 1);
   issue_b(0, 1);
-  vm_wait<2 * CF::AH + 2 * CF::BH>();
+  g3_wait();
   g3_barrier();
-  if (wm == 1) g3_barrier();  // stagger: group 1 runs one barrier behind group 0
+  if (grp == 1) g3_barrier();  // stagger: group 1 runs one barrier behind group 0
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   for (int kt = 0; kt < nk; ++kt) {
@@ -308,7 +323,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
     phase(I1{}, I0{}, kt);
     phase(I1{}, I1{}, kt);
   }
-  if (wm == 0) g3_barrier();
+  if (grp == 0) g3_barrier();
   vm_wait<0>();  // trailing dummy DMAs land before the ring is reused for C staging (or the workgroup ends)
   if constexpr (FORM != G3_LDS) {
     union H4 { uint2 u; f16 h[4]; };
@@ -441,7 +456,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   float* Cs = reinterpret_cast<float*>(sm3);
 #pragma unroll
   for (int pass = 0; pass < EP; ++pass) {
-    if (wn / (4 / EP) == pass) {
+    if (wn / (CF::WNW / EP) == pass) {
 #pragma unroll
       for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -521,14 +536,17 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
 // 256x256 round, fitted to tools/gemm_bench.py on MI355X (profiles/r01_gemm_bench.txt):
 //   256x128 / 128x256 0.62; 128x384 0.87 (N = 384 without the 256-wide tile's idle half);
 //   128x128 0.6, or 0.4 when K <= 512 where the fixed prologue/epilogue share dominates. 128x128 needs
-//   68 KiB of LDS, so two workgroups share a CU (512 slots).
+//   68 KiB of LDS, so two workgroups share a CU (512 slots). 256x192 (index 6, 4 x 2 waves): only where N is
+//   a multiple of 192 and of neither 256 nor 384 (the BigVGAN C = 192 convs: k = 11 977 -> 885-893 us against the
+//   256x256 tile's 64 idle columns; at N = 384 it ran 5 % behind 128x384, r05af)
 static int pick3(int M, int N, int Kpad) {
-  const int bms[5] = {256, 128, 256, 128, 128}, bns[5] = {256, 256, 128, 128, 384};
-  const double cost[5] = {1.0, 0.62, 0.62, Kpad <= 512 ? 0.4 : 0.6, 0.87};
-  const int slots[5] = {256, 256, 256, 512, 256};
+  const int bms[6] = {256, 128, 256, 128, 128, 256}, bns[6] = {256, 256, 128, 128, 384, 192};
+  const double cost[6] = {1.0, 0.62, 0.62, Kpad <= 512 ? 0.4 : 0.6, 0.87, 0.78};
+  const int slots[6] = {256, 256, 256, 512, 256, 256};
+  const int nv = (N % 192 == 0 && N % 256 != 0 && N % 384 != 0) ? 6 : 5;
   int best = 0;
   double best_t = 1e300;
-  for (int v = 0; v < 5; ++v) {
+  for (int v = 0; v < nv; ++v) {
     const int64_t tiles = (int64_t)cdiv(M, bms[v]) * cdiv(N, bns[v]);
     const double t = (double)cdiv64(tiles, slots[v]) * cost[v];
     if (t < best_t - 1e-9) {
@@ -536,7 +554,7 @@ static int pick3(int M, int N, int Kpad) {
       best = v;
     }
   }
-  return best;
+  return best == 5 ? 6 : best;
 }
 
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s) {
@@ -546,7 +564,7 @@ int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
               "conv_gemm3: epilogue leading dimensions must be multiples of 4 (vector epilogue)");
   SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm3: 16-B alignment");
   const int M = a.B * a.T_out;
-  const int v = (variant >= 0 && variant < 5) ? variant : pick3(M, a.N, a.Kpad);
+  const int v = ((variant >= 0 && variant < 5) || variant == 6) ? variant : pick3(M, a.N, a.Kpad);
   if (e.kind == EPI_GATE) {
     SVC_REQUIRE(a.N % 64 == 0, "conv_gemm3: paired epilogue needs N %% 64 == 0");
     switch (v) {
@@ -554,6 +572,7 @@ int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
       case 1: return launch3<128, 256, true>(a, e, zpage, s, "conv_gemm3<128,256,pair>");
       case 2: return launch3<256, 128, true>(a, e, zpage, s, "conv_gemm3<256,128,pair>");
       case 4: return launch3<128, 384, true>(a, e, zpage, s, "conv_gemm3<128,384,pair>");
+      case 6: return launch3<256, 192, true>(a, e, zpage, s, "conv_gemm3<256,192,pair>");
       default: return launch3<128, 128, true>(a, e, zpage, s, "conv_gemm3<128,128,pair>");
     }
   }
@@ -562,6 +581,7 @@ int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
     case 1: return launch3<128, 256, false>(a, e, zpage, s, "conv_gemm3<128,256>");
     case 2: return launch3<256, 128, false>(a, e, zpage, s, "conv_gemm3<256,128>");
     case 4: return launch3<128, 384, false>(a, e, zpage, s, "conv_gemm3<128,384>");
+    case 6: return launch3<256, 192, false>(a, e, zpage, s, "conv_gemm3<256,192>");
     default: return launch3<128, 128, false>(a, e, zpage, s, "conv_gemm3<128,128>");
   }
 }

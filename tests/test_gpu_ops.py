@@ -22,8 +22,8 @@ def _tm(x):  # [B, C, T] -> time-major [B*T, C]
 
 # (gemm_variant, gemm3_direct kernel switches): every conv_gemm3 tile and conv_gemm4 with conv_gemm3's register
 # epilogues (15 = every form), and the LDS-staged epilogue (0) on the tiles pick3 chooses in production
-_GEMM_MODES = ([(v, "15") for v in ("10", "11", "12", "13", "14", "15", "20", "24")] +
-               [(v, "0") for v in ("10", "13", "14")])
+_GEMM_MODES = ([(v, "15") for v in ("10", "11", "12", "13", "14", "15", "16", "20", "24")] +
+               [(v, "0") for v in ("10", "13", "14", "16")])
 
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k,stride,dil,pad,act", [
@@ -46,7 +46,8 @@ _GEMM_MODES = ([(v, "15") for v in ("10", "11", "12", "13", "14", "15", "20", "2
 ])
 @pytest.mark.parametrize("variant,direct", _GEMM_MODES)
 def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, direct, tune):
-    # gemm_variant 10..14: conv_gemm3 tiles, 15: auto, 20/24: conv_gemm4; gemm3_direct: conv_gemm3 register epilogues
+    # gemm_variant 10..14 / 16: conv_gemm3 tiles (16: 256 x 192 on 4 x 2 waves), 15: auto, 20/24: conv_gemm4;
+    # gemm3_direct: conv_gemm3 register epilogues
     # (all forms) or the LDS-staged C tile
     tune(None, gemm_variant=variant, gemm3_direct=direct)
     g = torch.Generator().manual_seed(0)
@@ -65,7 +66,7 @@ def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, direct, tune
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k,s", [(2, 25, 768, 384, 8, 4), (1, 40, 96, 48, 4, 2), (2, 33, 48, 24, 4, 2),
                                               (1, 9, 1536, 768, 8, 4)])
-@pytest.mark.parametrize("variant", ["10", "14", "15", "20", "24"])
+@pytest.mark.parametrize("variant", ["10", "14", "15", "16", "20", "24"])
 def test_conv_transpose1d(B, T, Cin, Cout, k, s, variant, tune):
     tune(None, gemm_variant=variant)
     g = torch.Generator().manual_seed(1)
