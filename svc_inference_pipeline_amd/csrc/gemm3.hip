@@ -37,8 +37,9 @@ namespace svc {
 template <int BM, int BN>
 struct G3 {
   static constexpr int NT = 512;
-  // waves: WMW (M) x WNW (N) = 2 x 4, or 4 x 2 for BN = 192 (the BigVGAN C = 192 convs without 64 idle columns:
-  // a quadrant of 48 columns = 3 fragments)
+  // waves: WMW (M) x WNW (N) = 2 x 4, or 4 x 2 for BN = 192 (the BigVGAN C = 192 convs without idle columns: a quadrant
+  // of 48 columns = 3 fragments). (A 256 x 96 tile on 8 x 1 waves for the C = 96 convs ran no faster than 128 x 128 with
+  // its idle quarter: 815.7 / 606.0 / 388.3 against 811.3 / 602.5 / 371.1 us at k = 11 / 7 / 3, r05ah.)
   static constexpr int WNW = BN % 128 == 0 ? 4 : 2, WMW = 8 / WNW;
   static constexpr int WTM = BM / WMW, WTN = BN / WNW;  // wave tile
   static constexpr int QM = WTM / 2, QN = WTN / 2;   // quadrant (one phase)
@@ -46,16 +47,16 @@ struct G3 {
   static constexpr int TILE = (BM + BN) * 128;       // bytes of one K-tile image (A rows, then B rows)
   static constexpr int RING = 2 * TILE;
   static constexpr int AH = BM / 128;                // DMA instructions per wave per A half-tile
-  // B half-tile: BN / 16 DMA instructions over the 8 waves: BH per wave, or (BN = 192: 12) two on waves 0-3 and one on
-  // waves 4-7 (BHL); each wave's vmcnt counts use its own number
-  static constexpr int BH = (BN / 16 + 7) / 8, BHL = (BN / 16) / 8;
+  // B half-tile: BN / 16 DMA instructions over the 8 waves: BH per wave, or BH on waves 0 .. BW - 1 and BHL = BH - 1
+  // on the others (BN = 192: two on waves 0-3, one on 4-7); each wave's vmcnt counts use its own number
+  static constexpr int BH = (BN / 16 + 7) / 8, BW = BN / 16 - 8 * (BH - 1), BHL = BW == 8 ? BH : BH - 1;
   static constexpr int EP = (BM * (BN + 4) * 4 <= 163840) ? 1 : 2;
   static constexpr int LDC = BN / EP + 4;
   static constexpr int C_BYTES = BM * LDC * 4;
   static constexpr int LDS = RING > C_BYTES ? RING : C_BYTES;
   static_assert(LDS <= 163840, "LDS budget");
-  static_assert(QM % 16 == 0 && QN % 16 == 0 && QM % 8 == 0 && QN % 8 == 0 && AH >= 1 && BHL >= 1 &&
-                    BM % 128 == 0, "tile shape");
+  static_assert(QM % 16 == 0 && QN % 16 == 0 && QM % 8 == 0 && QN % 8 == 0 && AH >= 1 && BH >= 1 &&
+                    BM % 128 == 0 && BN % 16 == 0, "tile shape");
 };
 
 // 16-B chunk swizzle of the 128-B-row LDS images: conflict-free ds_read_b128 fragment reads (16 consecutive
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / CF::WNW, wn = wave % CF::WNW;
   const int grp = wave >> 2;  // stagger group: one wave of each per SIMD
-  const bool bfull = CF::BH == CF::BHL || wave < 4;  // this wave issues BH (else BHL) B pieces per half-tile
+  const bool bfull = CF::BH == CF::BHL || wave < CF::BW;  // this wave issues BH (else BHL) B pieces per half-tile
 
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
