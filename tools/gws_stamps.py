@@ -33,6 +33,8 @@ for M in [int(v) for v in (sys.argv[1:] or ["29984", "14992"])]:
     print("  end (last stamp) spread:", np.percentile([rel[w, n[w] - 1] for w in range(len(rel))], [0, 50, 100]))
     # per step roles: D_{k-1} = end of the previous barrier (kind 0 index 2 + k)
     fw, wt, sw, bw = [], [], [], []
+    by3 = {0: [], 1: [], 2: []}  # second wave's step time by k mod 3 (its steady loop is unrolled by 3 from k = 2)
+    late = {0: [], 1: [], 2: []}  # (second-wave arrival - first-wave arrival) at the step's barrier, by k mod 3
     for w in range(len(full)):
         nsub = n[w] - 4  # stamps 3..3+nsub
         for k in range(1, nsub):
@@ -41,6 +43,13 @@ for M in [int(v) for v in (sys.argv[1:] or ["29984", "14992"])]:
             if min(a1, b2, c3, d1, d0) <= 0:
                 continue
             fw.append(a1 - d0); wt.append(b2 - a1); sw.append(c3 - d0); bw.append(d1 - max(b2, c3))
+            if k >= 2:
+                by3[k % 3].append(c3 - d0)
+                late[k % 3].append(c3 - b2)
     for name, v in (("first wave: MFMAs + partial write", fw), ("first wave: ring vmcnt wait", wt),
                     ("second wave: cp load + MFMAs + epilogue", sw), ("barrier release after the later arrival", bw)):
         print(f"  {name}: pctl 10/50/90", np.percentile(v, [10, 50, 90]).astype(int))
+    for r in range(3):
+        if by3[r]:
+            print(f"  k % 3 == {r}: second wave step median {int(np.median(by3[r]))}, second minus first arrival "
+                  f"median {int(np.median(late[r]))}")
