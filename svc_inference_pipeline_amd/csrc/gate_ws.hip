@@ -61,9 +61,9 @@ constexpr int GW_PART = GW_NG * GW_GBYTES;    // partial accumulators: [2 buffer
 constexpr int GW_ZERO = GW_PART + 2 * 4 * 2048;  // 768 B of zeros
 constexpr int GW_TVT = GW_ZERO + 768;  // ragged batches: valid input rows per utterance
 constexpr int GW_MAXB = 1024;
-constexpr int GW_STL = GW_TVT + GW_MAXB * 4;   // diagnostics: in-LDS step stamps [3 kinds][GW_NSTAMP] u64
+constexpr int GW_STL = GW_TVT + GW_MAXB * 4;   // diagnostics: in-LDS step stamps [4 kinds][GW_NSTAMP] u64
 constexpr int GW_NSTAMP = 128;
-constexpr int GW_LDS = GW_STL + 3 * GW_NSTAMP * 8;  // 152,320 B
+constexpr int GW_LDS = GW_STL + 4 * GW_NSTAMP * 8;  // 153,344 B
 constexpr int GW_PARTS = 42;          // row parts (x 6 column groups)
 constexpr int GW_GRID = 256;
 constexpr int GW_NT = 512;
@@ -117,15 +117,15 @@ union GwH4 { uint2 u; f16 h[4]; };
 
 // Diagnostics (compile-time DBG, svc_gemm_bench / SVC_GWS_DBG / SVC_GWS_STAMPS only): 2 no MFMAs, 4 no gate arithmetic,
 // 8 step stamps. Stamps: s_memtime at step boundaries, [workgroup][kind][GW_NSTAMP] in a buffer nothing else reads.
-// Kind 0: the first second wave after each barrier (stored directly: its vector-memory operations are the compiler's
-// to count); kinds 1 / 2: the first first wave before / after its ring wait, kind 3: the first second wave before its
-// barrier, kept in LDS and copied out after the loop (a first wave's vmcnt waits are hand-counted, so it stores
-// nothing inside)
+// Kind 0: the first second wave after each barrier; kinds 1 / 2: the first first wave before / after its ring wait,
+// kind 3: the first second wave before its barrier. All kept in LDS (kind 0 in the fourth slot) and copied out after
+// the loop, so the stamped kernel issues no extra vector-memory operations inside it (a first wave's vmcnt waits are
+// hand-counted; a per-step store in the second waves would change their waits: kind 0 was a direct store before r05ap)
 template <int DBG>
-__device__ __forceinline__ void gw_stamp(const GateWsArgs& a, int i) {
+__device__ __forceinline__ void gw_stamp(unsigned char* smw, int i) {
   if constexpr ((DBG & 8) != 0)
     if (threadIdx.x == 256 && i < GW_NSTAMP)
-      a.stamps[(size_t)blockIdx.x * 4 * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
+      reinterpret_cast<unsigned long long*>(smw + GW_STL)[3 * GW_NSTAMP + i] = __builtin_amdgcn_s_memtime();
 }
 template <int DBG>
 __device__ __forceinline__ void gw_stamp_lds(unsigned char* smw, int kind, int i, int thread) {
@@ -136,7 +136,8 @@ __device__ __forceinline__ void gw_stamp_lds(unsigned char* smw, int kind, int i
 template <int DBG>
 __device__ __forceinline__ void gw_stamp_flush(const GateWsArgs& a, const unsigned char* smw, int kind, int n) {
   if constexpr ((DBG & 8) != 0) {
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(smw + GW_STL) + (kind - 1) * GW_NSTAMP;
+    const unsigned long long* src =
+        reinterpret_cast<const unsigned long long*>(smw + GW_STL) + (kind == 0 ? 3 : kind - 1) * GW_NSTAMP;
     for (int i = threadIdx.x & 63; i < n && i < GW_NSTAMP; i += 64)
       a.stamps[((size_t)blockIdx.x * 4 + kind) * GW_NSTAMP + i] = src[i];
   }
@@ -354,7 +355,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     const __amdgpu_buffer_rsrc_t rcp =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.cp), (short)0, a.M * a.ld_cp * 2, GW_CFG);
     const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(a.y, (short)0, a.M * a.ldy * 2, GW_CFG);
-    gw_stamp<DBG>(a, 0);
+    gw_stamp<DBG>(smw, 0);
     load_w(GW_KA, std::integral_constant<int, GW_KB>());
     const float4 bg = *reinterpret_cast<const float4*>(a.bias + ng + 4 * fk);
     const float4 bfv = *reinterpret_cast<const float4*>(a.bias + nf + 4 * fk);
@@ -369,12 +370,12 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     floatx4 pg = {0.f, 0.f, 0.f, 0.f}, pf = {0.f, 0.f, 0.f, 0.f};  // accumulators of the block awaiting its epilogue
     GwRow row;
     row.init(a, tvt, r_begin + fr);
-    gw_stamp<DBG>(a, 1);
+    gw_stamp<DBG>(smw, 1);
     gw_barrier();  // (pairs with the first waves' prologue barrier)
     // (priority 1 on the first waves instead, or on neither: 903.2 / 900.5 / 902.6 and 902.4 / 902.1 / 904.0 against
     // 908.1 / 908.0 / 907.3 audio-s/s, r04s)
     __builtin_amdgcn_s_setprio(1);
-    gw_stamp<DBG>(a, 2);
+    gw_stamp<DBG>(smw, 2);
     // gate of the lane's element i (conv_gemm4's DIRECT epilogue arithmetic, same order), and the block's store (rows
     // past the part are dropped)
     auto gate_el = [&](int i, const GwH4* cp, const floatx4& ag, const floatx4& af) __attribute__((always_inline)) {
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
     auto end_step = [&](int k) __attribute__((always_inline)) {
       gw_stamp_lds<DBG>(smw, 3, k, 256);
       gw_barrier();
-      gw_stamp<DBG>(a, 3 + k);
+      gw_stamp<DBG>(smw, 3 + k);
     };
     // steady step k (2 <= k < nsub): cp(k) into LS, MFMAs of block k - 1 with the epilogue of block k - 2 (cp from ES)
     // in their K-step segments: element i at the end of segment (i + 1) GW_KB / 4 - 1 (every element, for any split),
@@ -462,7 +463,10 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       end_step(nsub);
     }
     epi_set(nsub - 1);  // the last block's epilogue
-    if (wave == 4) gw_stamp_flush<DBG>(a, smw, 3, nsub + 1);
+    if (wave == 4) {
+      gw_stamp_flush<DBG>(a, smw, 3, nsub + 1);
+      gw_stamp_flush<DBG>(a, smw, 0, nsub + 4);
+    }
   }
 }
 
