@@ -106,7 +106,7 @@ __device__ __forceinline__ float gate_act(float a, float b) {
 // e = x - q0 sqrt(2) exactly, q0 + e r): equal to the division bit for bit for every float x with 2^-100 <= |x| < inf
 // (all 2^32 inputs checked against x86 fmaf / division; the differing inputs are |x| <= 2.2e-32 and +-inf). Those
 // lanes take the division, behind a branch no wave takes in practice. Replaces the ~10-instruction division sequence
-// (v_div_scale x2, v_rcp, 4 FMAs, v_div_fmas, v_div_fixup) of the DiffSVC residual epilogues (res_proj, dlayer).
+// (v_div_scale x2, v_rcp, 4 FMAs, v_div_fmas, v_div_fixup) of the DiffSVC residual epilogues (res_proj).
 constexpr float SQRT2_F = 1.41421356237309515f;
 __device__ __forceinline__ float div_sqrt2_exact(float x) {
   constexpr float r = 1.0f / SQRT2_F;
@@ -294,11 +294,6 @@ struct RingRetire {
   ~RingRetire() { r.retire(s); }
 };
 
-// dlayer.hip's residual half (the fused DiffSVC layer): W_res in res_proj_pack fragment order, its bias, dproj_i / dproj_{i+1},
-// the split residual stream's new high half (another buffer than the layer input) and its low half (updated in place)
-struct DLayerProj {
-  const f16* Wr; const float* br; const float* sub; const float* add; f16* hi_out; f16* lo;
-};
 
 // One PLMS update x' = x + d (A x - Bc e'), e' = (sum_k c_k e_k) / div (modules/diffsvcrepo_inference.py:91-130;
 // engine.hip svc_diffsvc_sample, elementwise.hip plms_update).
@@ -330,9 +325,9 @@ struct Tuning {
                             // res_proj / mel_proj; 0: conv_gemm3;
                             // > 1: that many row lanes of 2 workgroups instead of 1/2 (one sampler stream) or 3/8
                             // (several) of the CU count)
-  int gate_ws = 1;          // DiffSVC dilated conv + gate: 1 the weight-stationary row stream (gate_ws.hip), 0 conv_gemm4,
-                            // 2 / 3 the rows held still and the weights streamed (dlayer.hip: gate alone / with the
-                            // residual projection fused, the whole layer in one launch; measured no faster, r05k)
+  int gate_ws = 1;          // DiffSVC dilated conv + gate: 1 the weight-stationary row stream (gate_ws.hip), 0 conv_gemm4
+                            // (the A-stationary dlayer.hip of round 5, gate alone or the whole layer, measured no
+                            // faster and was removed: DESIGN.md, r05k)
   std::string site_variant;  // "site=variant,...": per-call-site GEMM kernel override (environment only, A/B runs)
   void from_env();
   bool set(const char* name, double v);  // false: unknown name ("reset" restores the creation-time values)

@@ -109,9 +109,6 @@ int f32_to_f16x3(const float* x, int ldx, f16* y, int rows, int C, hipStream_t s
 int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int variant, hipStream_t s);
 int conv_gemm4(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, hipStream_t s, bool direct_gate);
 bool gate_ws_fits(const ConvGemmArgs& a, const EpiArgs& e);
-bool dlayer_fits(const ConvGemmArgs& a, const EpiArgs& e);
-int dlayer(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s, const DLayerProj* pr);
-constexpr int kNotFused = 1000;  // run_gemm with a DLayerProj: the fused layer does not fit (the caller runs it unfused)
 extern unsigned long long* gate_ws_stamps;
 int gate_ws_nstamp();
 int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s);
@@ -389,6 +386,46 @@ int ensure_dyn_lds(const void* fn, int bytes) {
 
 using namespace svc;
 
+// Device tables keyed by a parameter set (F0 front ends): an entry is built once and reused by every call with the same
+// key, so a server alternating between parameter sets allocates nothing after the first call of each. At most kMax
+// entries: beyond that the least recently used one is freed after the device has drained (a call in flight on any
+// stream may still read it).
+struct TableCache {
+  static constexpr int kMax = 8;
+  struct Entry {
+    std::vector<double> key;
+    double* dev;
+    uint64_t used;
+  };
+  std::vector<Entry> e;
+  uint64_t clock = 0;
+  double* find(const double* key, int nk) {
+    for (auto& x : e)
+      if ((int)x.key.size() == nk && memcmp(x.key.data(), key, nk * sizeof(double)) == 0) {
+        x.used = ++clock;
+        return x.dev;
+      }
+    return nullptr;
+  }
+  // takes ownership of dev (hipMalloc'd)
+  int insert(const double* key, int nk, double* dev) {
+    if ((int)e.size() >= kMax) {
+      size_t lru = 0;
+      for (size_t i = 1; i < e.size(); ++i)
+        if (e[i].used < e[lru].used) lru = i;
+      SVC_HIP_CHECK(hipDeviceSynchronize());
+      (void)hipFree(e[lru].dev);
+      e.erase(e.begin() + (long)lru);
+    }
+    e.push_back(Entry{std::vector<double>(key, key + nk), dev, ++clock});
+    return SVC_OK;
+  }
+  void clear() {
+    for (auto& x : e) (void)hipFree(x.dev);
+    e.clear();
+  }
+};
+
 struct svc_ctx {
   int device = 0;
   Tuning tune, tune0;  // kernel switches (tune0: their values at creation, for "tune.reset")
@@ -470,13 +507,14 @@ struct svc_ctx {
     return SVC_OK;
   }
   int hop_out = 256;
-  // pYIN's device tables (beta priors, banded log-transitions, bin frequencies) for the last (fs, f0_min, f0_max,
-  // win, hop): built once per parameter set; a new set gets a new buffer (an in-flight call may still read the old)
-  double* pyin_tab = nullptr;
-  double pyin_key[5] = {0, 0, 0, 0, 0};
-  // Praat-AC F0's window / window autocorrelation / FFT twiddle tables for (fs, f0_min) (f0.hip f0_tables), likewise
-  double* f0_tab = nullptr;
-  double f0_key[2] = {0, 0};
+  // pYIN's device tables (beta priors, banded log-transitions, bin frequencies) per (fs, f0_min, f0_max, win, hop), and
+  // Praat-AC F0's window / window autocorrelation / FFT twiddle tables per (fs, f0_min) (f0.hip f0_tables): built once per
+  // parameter set and reused by every later call with that set (TableCache)
+  TableCache pyin_tabs, f0_tabs;
+  ~svc_ctx() {
+    pyin_tabs.clear();
+    f0_tabs.clear();
+  }
 };
 
 namespace {
@@ -724,8 +762,7 @@ static ConvGemmArgs gemm_args(const PackedGemm& g, const f16* X, int ldx, int Cv
 
 // tv / tv_mul: ragged batches, utterance b's valid input rows are tv[b] * tv_mul (ConvGemmArgs::tv; NULL = all)
 int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int T_in, int T_out, EpiArgs e,
-             hipStream_t s, const char* site = "", const int* tv = nullptr, int tv_mul = 1,
-             const DLayerProj* proj = nullptr) {
+             hipStream_t s, const char* site = "", const int* tv = nullptr, int tv_mul = 1) {
   prof_site(site);
   const Tuning& tu = tuning();
   // conv_gemm3's register epilogues (gemm3_direct mask, gemm3.hip) stay off inside the DiffSVC sampler unless
@@ -750,9 +787,6 @@ int run_gemm(const PackedGemm& g, const f16* X, int ldx, int Cvalid, int B, int 
       }
   }
   // the DiffSVC dilated conv + gate: the weight-stationary row stream (gate_ws.hip) where it fits, else conv_gemm4
-  // with proj: the whole residual layer in one launch (dlayer.hip), or kNotFused
-  if (proj) return (variant == 15 && pair && tu.gate_ws == 3 && dlayer_fits(a, e)) ? dlayer(a, e, s, proj) : kNotFused;
-  if (variant == 15 && pair && tu.gate_ws >= 2 && dlayer_fits(a, e)) return dlayer(a, e, s, nullptr);
   if (variant == 15 && pair && tu.gate_ws && gate_ws_fits(a, e)) return gate_ws(a, e, s);
   if (variant == 15 && pair) variant = 24;
   // The skip-sum GEMM of a sampler sub-batch (K = 20 x 384, M <= 20 k rows) takes conv_gemm3's 256 x 128 tile although
@@ -1746,18 +1780,20 @@ svc_status svc_f0_ac(svc_ctx* c, const float* wav, int B, int64_t n, const int64
     for (int b = 0; b < B; ++b) Tb[b] = (int)mel_frames_of(c, n_samples[b]);
   }
   const double key[2] = {(double)c->fs, c->f0_min};
-  if (!c->f0_tab || memcmp(key, c->f0_key, sizeof(key)) != 0) {
+  double* f0_tab = c->f0_tabs.find(key, 2);
+  if (!f0_tab) {
     std::vector<double> tab(f0_table_doubles(c->fs, c->f0_min));
     if ((st = f0_tables(c->fs, c->f0_min, tab.data()))) return st;
     void* p = nullptr;
     SVC_HIP_CHECK(hipMalloc(&p, tab.size() * 8));
-    c->allocs.push_back(p);
-    SVC_HIP_CHECK(hipMemcpy(p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice));
-    c->f0_tab = reinterpret_cast<double*>(p);
-    memcpy(c->f0_key, key, sizeof(key));
+    const hipError_t me = hipMemcpy(p, tab.data(), tab.size() * 8, hipMemcpyHostToDevice);
+    if (me != hipSuccess) (void)hipFree(p);
+    SVC_HIP_CHECK(me);
+    f0_tab = reinterpret_cast<double*>(p);
+    if ((st = c->f0_tabs.insert(key, 2, f0_tab))) return st;
   }
   RingRetire retire_(c->lens_feat, (hipStream_t)stream);
-  return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->auxws.base, c->auxws.cap, c->f0_tab,
+  return f0_praat_ac(wav, B, n, c->fs, ts, c->f0_min, c->f0_max, 0.6, T, f0, c->auxws.base, c->auxws.cap, f0_tab,
                      (hipStream_t)stream, n_samples, n_samples ? Tb.data() : nullptr, &c->lens_feat);
 }
 
@@ -1775,15 +1811,17 @@ svc_status svc_f0_pyin(svc_ctx* c, const float* wav, int B, int64_t n, const int
   if ((st = c->auxws.reserve(std::max(need + 4096, c->auxws.cap)))) return st;
   // the tables depend only on (fs, f0_min, f0_max, win, hop): built and uploaded once per parameter set
   const double key[5] = {fs, f0_min, f0_max, (double)win_length, (double)hop_length};
-  if (!c->pyin_tab || memcmp(key, c->pyin_key, sizeof(key)) != 0) {
+  double* pyin_tab = c->pyin_tabs.find(key, 5);
+  if (!pyin_tab) {
     std::vector<double> tab(nt);
     if ((st = pyin_tables(fs, f0_min, f0_max, FL, win_length, hop_length, tab.data()))) return st;
     void* p = nullptr;
     SVC_HIP_CHECK(hipMalloc(&p, nt * 8));
-    c->allocs.push_back(p);
-    SVC_HIP_CHECK(hipMemcpy(p, tab.data(), nt * 8, hipMemcpyHostToDevice));
-    c->pyin_tab = reinterpret_cast<double*>(p);
-    memcpy(c->pyin_key, key, sizeof(key));
+    const hipError_t me = hipMemcpy(p, tab.data(), nt * 8, hipMemcpyHostToDevice);
+    if (me != hipSuccess) (void)hipFree(p);
+    SVC_HIP_CHECK(me);
+    pyin_tab = reinterpret_cast<double*>(p);
+    if ((st = c->pyin_tabs.insert(key, 5, pyin_tab))) return st;
   }
   // only the per-call lengths are staged (the ring retires its last slot)
   hipStream_t s = (hipStream_t)stream;
@@ -1795,7 +1833,7 @@ svc_status svc_f0_pyin(svc_ctx* c, const float* wav, int B, int64_t n, const int
     nb_dev = reinterpret_cast<const int64_t*>(dev);
   }
   return f0_pyin(wav, B, n, nb_dev, n_samples, fs, f0_min, f0_max, FL, win_length, hop_length, T, f0, c->auxws.base,
-                 c->auxws.cap, c->pyin_tab, s);
+                 c->auxws.cap, pyin_tab, s);
 }
 
 svc_status svc_pitch_shift(svc_ctx* c, double* f0, int B, int T, double target_median, void* stream) {
@@ -2151,7 +2189,6 @@ struct DenoiseBufs {
   size_t g_ls;   // elements between layers of g16, also layer-major [NL][rows_total][C]: the gate GEMM writes and the
                  // residual GEMM reads one contiguous block; the skip GEMM reads the NL blocks as NL "taps" whose row
                  // shift is the layer stride (tap_mul = rows_total)
-  f16* y16b;     // [rows][C] the high half's second buffer (the fused layer writes the next layer's input there)
 };
 
 
@@ -2180,8 +2217,7 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   } else if ((st = run_gemm(c->melpre, x16, ldx16, c->n_mel, B, T, T, e, s, "diffsvc.melpre"))) {
     return st;
   }
-  // the split residual stream's high half: in place (y16) through gate + res_proj; with the fused layer (dlayer.hip,
-  // tune.gate_ws = 3) a layer reads it as its rows' halo while it writes the next, so it alternates between y16 and y16b
+  // the split residual stream's high half, updated in place (y16) by gate + res_proj
   f16* hi = bb.y16;
   for (int i = 0; i < NL; ++i) {
     EpiArgs g = epi();
@@ -2190,19 +2226,6 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
     g.ld_cp = 2 * C;
     g.y16 = bb.g16 + (size_t)i * bb.g_ls;
     g.ldy16 = C;
-    if (i + 1 < NL && tuning().gate_ws == 3 && C == 384 && c->outres[i].Wfrag && c->outres[i].N == C &&
-        c->outres[i].K == C && bb.y16b) {
-      f16* hi_next = hi == bb.y16 ? bb.y16b : bb.y16;
-      const DLayerProj pr{c->outres[i].Wfrag, c->outres[i].bias, dp + (size_t)i * C, dp + (size_t)(i + 1) * C,
-                          hi_next, bb.lo16};
-      prof_site("diffsvc.layer");
-      st = run_gemm(c->dil[i], hi, C, C, B, T, T, g, s, "diffsvc.layer", tv, 1, &pr);
-      if (st == SVC_OK) {
-        hi = hi_next;
-        continue;
-      }
-      if (st != kNotFused) return st;
-    }
     if ((st = run_gemm(c->dil[i], hi, C, C, B, T, T, g, s, "diffsvc.dilated", tv, 1))) return st;
     if (i + 1 == NL) break;  // the last layer's residual output is unused (only skips feed the head)
     // x = (x + residual) / sqrt(2); next input x + diffusion_projection_{i+1}(step):
@@ -2278,8 +2301,7 @@ static int alloc_denoise(svc_ctx* c, int B, int T, DenoiseBufs& bb) {
   WS_GET(f16, s16, rows * C * 3);  // [hi | lo | hi] when head_split
   WS_GET(f16, u16, rows * C * 3);
   WS_GET(f16, lo16, rows * C);
-  WS_GET(f16, y16b, rows * C);
-  bb = DenoiseBufs{cp16, y16, g16, s16, u16, lo16, rows * 2 * C, rows * C, y16b};
+  bb = DenoiseBufs{cp16, y16, g16, s16, u16, lo16, rows * 2 * C, rows * C};
   return SVC_OK;
 }
 
@@ -2416,7 +2438,7 @@ static int sample_impl(svc_ctx* c, const float* cond, int B, int T, const int* t
     const size_t r = u.r0;
     const int C = c->C;
     return DenoiseBufs{bb.cp16 + r * 2 * C, bb.y16 + r * C, bb.g16 + r * C, bb.s16 + r * 3 * C, bb.u16 + r * 3 * C,
-                       bb.lo16 + r * C, bb.cp_ls, bb.g_ls, bb.y16b ? bb.y16b + r * C : nullptr};
+                       bb.lo16 + r * C, bb.cp_ls, bb.g_ls};
   };
   SVC_HIP_CHECK(hipEventRecord(c->ev_fork, s));
   for (int h = 0; h < S && S > 1; ++h) SVC_HIP_CHECK(hipStreamWaitEvent(sub[h].s, c->ev_fork, 0));
@@ -2939,9 +2961,9 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
               "gemm_bench: the diagnostic gate epilogues (3-5) exist in variant 24 only");
   SVC_REQUIRE((variant >= 10 && variant <= 16) || variant == 20 || variant == 24 ||
                   (variant == 30 && epi_kind == 6 && N == 384 && Cin == 384 && taps == 1) ||
-                  ((variant == 40 || variant == 41) && epi_kind == 1 && N == 768 && Cin == 384 && taps == 3),
-              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap; 40 / 41: gate_ws / "
-              "dlayer, gate epilogue, N = 768, Cin = 384, 3 taps)", variant);
+                  (variant == 40 && epi_kind == 1 && N == 768 && Cin == 384 && taps == 3),
+              "gemm_bench: variant %d (30: res_proj, split residual epilogue, N = Cin = 384, 1 tap; 40: gate_ws, "
+              "gate epilogue, N = 768, Cin = 384, 3 taps)", variant);
   const int K = taps * Cin, Kpad = (int)round_up(K, 64), Npad = (int)std::max(round_up(N, 256), round_up(N, 384));
   f16 *X, *W, *Y, *cp;
   float *bias, *R = nullptr;
@@ -2987,7 +3009,7 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
   if (variant == 30) {
     SVC_HIP_CHECK(hipMalloc(&Wf, res_proj_pack_elems() * sizeof(f16)));
     st = res_proj_pack(W, Kpad, Wf, 0);  // (on failure: no launches below, the buffers are freed at the end)
-  } else if (variant == 40 || variant == 41) {
+  } else if (variant == 40) {
     SVC_HIP_CHECK(hipMalloc(&Wf, gate_ws_pack_elems() * sizeof(f16)));
     st = gate_ws_pack(W, Kpad, Wf, 0);
     a.Wfrag = Wf;
@@ -3007,7 +3029,6 @@ extern "C" svc_status svc_gemm_bench(int M, int N, int Cin, int taps, int epi_ki
     if (variant == 30) return res_proj(X, Wf, bias, bias, bias, e.acc_div, Y, reinterpret_cast<f16*>(R), M, false, 0, 0);
     if (variant == 20 || variant == 24) return conv_gemm4(a, e, zero_page(), 0, variant == 24);
     if (variant == 40) return gate_ws(a, e, 0);
-    if (variant == 41) return dlayer(a, e, 0, nullptr);
     return conv_gemm3(a, e, zero_page(), variant - 10, 0);
   };
   for (int w = 0; w < 2 && !st; ++w) st = run();

@@ -20,6 +20,12 @@
 //      chosen frequencies are written zero-padded to the mel length (utils/f0.py:156-157).
 // The Hann window, its normalised autocorrelation wR and the FFT's quarter twiddle table are host-built per parameter
 // set and kept by the context (f0_tables).
+//
+// Provenance: the reference calls Praat through parselmouth; Praat (GPL v2 or later, P. Boersma & D. Weenink) is not in
+// this image. sinc_interp / brent_neg_sinc below restate Praat's published NUM_interpolate_sinc and NUMminimize_brent
+// (keeping Praat's variable names: midleft, halfsina, cosaa, daa ...) and the pitch path restates Sound_to_Pitch /
+// Pitch_pathFinder (Boersma 1993), so that the F0 is comparable with what the reference computes; oracle/praat_ac.py
+// restates the same algorithm in Python. Parity with Praat itself is unpinned (tests/test_f0.py).
 #include <math.h>
 
 #include <algorithm>
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(F0_NT) void f0_frame_kernel(const float* __restrict
                                                          const double* __restrict__ tab,
                                                          const double* __restrict__ gpart, F0Out o,
                                                          const F0Utt* __restrict__ utt) {
-  static_assert(2 * N == 1024 || 2 * N == 2048 || 2 * N == 4096, "nfft");
+  static_assert(2 * N == 512 || 2 * N == 1024 || 2 * N == 2048 || 2 * N == 4096, "nfft");
   constexpr int PR = (N + F0_NT - 1) / F0_NT;  // complex points per thread
   extern __shared__ __align__(16) unsigned char f0sm[];
   double2* zs = reinterpret_cast<double2*>(f0sm);              // [N]
@@ -389,7 +395,9 @@ __global__ __launch_bounds__(F0_NT) void f0_frame_kernel(const float* __restrict
     fft_stage<N, 4, 4, F0_NT>(zs, tw, tid);
     fft_stage<N, 4, 16, F0_NT>(zs, tw, tid);
     fft_stage<N, 4, 64, F0_NT>(zs, tw, tid);
-    if constexpr (N == 1024) {
+    if constexpr (N == 256) {
+      // (4^4: done)
+    } else if constexpr (N == 1024) {
       fft_stage<N, 4, 256, F0_NT>(zs, tw, tid);
     } else if constexpr (N == 2048) {
       fft_stage<N, 4, 256, F0_NT>(zs, tw, tid);
@@ -797,7 +805,8 @@ int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double
     utt = (const F0Utt*)dev;
   }
   SVC_REQUIRE(P.nw <= 2048 && P.maxc <= F0_MAXC, "f0: window %d / candidates %d too large", P.nw, P.maxc);
-  SVC_REQUIRE(P.nfft == 1024 || P.nfft == 2048 || P.nfft == 4096, "f0: autocorrelation FFT of %d points", P.nfft);
+  SVC_REQUIRE(P.nfft == 512 || P.nfft == 1024 || P.nfft == 2048 || P.nfft == 4096,
+              "f0: autocorrelation FFT of %d points (window %d samples)", P.nfft, P.nw);
   P.voicing = voicing;
   P.silence = 0.03;
   P.octave_cost = 0.01;
@@ -823,13 +832,14 @@ int f0_praat_ac(const float* wav, int B, int64_t n, double fs, double ts, double
   o.work = (int*)take((1 + nf * (F0_MAXC - 1)) * 4);
   double* gpart = (double*)take((size_t)B * F0_GP * 3 * 8);
   // the frame pass's LDS holds r (2 bmax + 1 doubles) and the peak lists (3 x (iend + 1) / 2 + 6 words) in the FFT's
-  // 2 * nfft / 2 doubles
-  SVC_REQUIRE((2 * P.bmax + 2) + 3 * ((std::min(P.maxlag, P.bmax) + 1) / 2 + 2) <= P.nfft,
+  // 2 * nfft / 2 doubles and the quarter twiddle table after it (nfft / 2 doubles, dead after the inverse FFT)
+  SVC_REQUIRE((2 * P.bmax + 2) + 3 * ((std::min(P.maxlag, P.bmax) + 1) / 2 + 2) <= 3 * P.nfft / 2,
               "f0: r and peak lists exceed the FFT buffer");
   hipLaunchKernelGGL(f0_global_kernel, dim3(F0_GP, B), dim3(256), 0, s, wav, n, utt, gpart, o.work);
   SVC_LAUNCH_CHECK();
   int st = P.nfft == 2048   ? launch_f0_frames<1024>(wav, B, n, P, tab, gpart, o, utt, s)
            : P.nfft == 1024 ? launch_f0_frames<512>(wav, B, n, P, tab, gpart, o, utt, s)
+           : P.nfft == 512  ? launch_f0_frames<256>(wav, B, n, P, tab, gpart, o, utt, s)
                             : launch_f0_frames<2048>(wav, B, n, P, tab, gpart, o, utt, s);
   if (st) return st;
   const int64_t items = (int64_t)nf * (P.maxc - 1);

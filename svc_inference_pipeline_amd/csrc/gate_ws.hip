@@ -63,7 +63,8 @@ constexpr int GW_TVT = GW_ZERO + 768;  // ragged batches: valid input rows per u
 constexpr int GW_MAXB = 1024;
 constexpr int GW_STL = GW_TVT + GW_MAXB * 4;   // diagnostics: in-LDS step stamps [4 kinds][GW_NSTAMP] u64
 constexpr int GW_NSTAMP = 128;
-constexpr int GW_LDS = GW_STL + 4 * GW_NSTAMP * 8;  // 153,344 B
+constexpr int GW_LDS = GW_STL;                      // 149,248 B (the production instances hold no stamp region)
+constexpr int GW_LDS_STAMPS = GW_STL + 4 * GW_NSTAMP * 8;  // 153,344 B: the stamped diagnostics instance (DBG & 8)
 constexpr int GW_PARTS = 42;          // row parts (x 6 column groups)
 constexpr int GW_GRID = 256;
 constexpr int GW_NT = 512;
@@ -526,10 +527,11 @@ int gate_ws(const ConvGemmArgs& a, const EpiArgs& e, hipStream_t s) {
   else if (!a.bf16 && dbg == 4) fn = (const void*)gate_ws_kernel<false, 4>;
   else if (!a.bf16 && ka == 18) fn = (const void*)gate_ws_kernel<false, 0, 18>;
   else if (!a.bf16 && ka == 22) fn = (const void*)gate_ws_kernel<false, 0, 22>;
-  if (int st = ensure_dyn_lds(fn, GW_LDS)) return st;
+  const int lds = fn == (const void*)gate_ws_kernel<false, 8> ? GW_LDS_STAMPS : GW_LDS;
+  if (int st = ensure_dyn_lds(fn, lds)) return st;
   const int tok = prof_begin("gate_ws<16x128>", 2.0 * M * (double)GW_N * GW_K, 0.0, s);
   void* args[] = {&g};
-  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3(GW_GRID), dim3(GW_NT), args, GW_LDS, s));
+  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3(GW_GRID), dim3(GW_NT), args, lds, s));
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;

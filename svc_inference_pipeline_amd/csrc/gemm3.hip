@@ -101,6 +101,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
                                                            float inv_cp) {
   static_assert(FORM == G3_LDS || !PAIR, "register epilogues: generic epilogues only");
   using CF = G3<BM, BN>;
+  // the paired gate epilogue (epilogue_pass<PAIR>) walks 64-column gate | filter blocks: every LDS pass must hold whole
+  // blocks (the 256 x 192 tile's two 96-column passes do not)
+  static_assert(!PAIR || (BN / CF::EP) % 64 == 0, "paired epilogue: pass width must be a multiple of 64 columns");
   using O = Op16<BF>;  // operand format (binary16 or bfloat16)
   extern __shared__ __align__(16) unsigned char sm3[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -574,16 +577,18 @@ int conv_gemm3(const ConvGemmArgs& a, const EpiArgs& e, const f16* zpage, int va
                   e.ld_cp % 4 == 0 && e.ldy16 % 4 == 0 && e.ld_emb % 4 == 0,
               "conv_gemm3: epilogue leading dimensions must be multiples of 4 (vector epilogue)");
   SVC_REQUIRE(((uintptr_t)a.X & 15) == 0 && ((uintptr_t)a.W & 15) == 0, "conv_gemm3: 16-B alignment");
+  // column blocks (EpiArgs::col_block) re-address the out16 high-half store only
+  SVC_REQUIRE(!e.col_block || (!e.lo16 && !e.split16 && !e.out32), "conv_gemm3: col_block with lo16 / split16 / out32");
   const int M = a.B * a.T_out;
   const int v = ((variant >= 0 && variant < 5) || variant == 6) ? variant : pick3(M, a.N, a.Kpad);
   if (e.kind == EPI_GATE) {
     SVC_REQUIRE(a.N % 64 == 0, "conv_gemm3: paired epilogue needs N %% 64 == 0");
     switch (v) {
+      case 6:  // (the 256 x 192 tile's epilogue passes split the 64-column gate | filter blocks: the 256 x 256 tile)
       case 0: return launch3<256, 256, true>(a, e, zpage, s, "conv_gemm3<256,256,pair>");
       case 1: return launch3<128, 256, true>(a, e, zpage, s, "conv_gemm3<128,256,pair>");
       case 2: return launch3<256, 128, true>(a, e, zpage, s, "conv_gemm3<256,128,pair>");
       case 4: return launch3<128, 384, true>(a, e, zpage, s, "conv_gemm3<128,384,pair>");
-      case 6: return launch3<256, 192, true>(a, e, zpage, s, "conv_gemm3<256,192,pair>");
       default: return launch3<128, 128, true>(a, e, zpage, s, "conv_gemm3<128,128,pair>");
     }
   }

@@ -1,7 +1,8 @@
 """F0 (Praat to_pitch_ac, utils/f0.py:120-161). PARITY UNPINNED: parselmouth/Praat is absent, so the
 oracle (oracle/praat_ac.py, a restatement of Praat's published algorithm) is checked with known-answer
 tests on synthetic tones (CPU), and the HIP kernel is checked against the oracle (GPU): frame count and
-voicing decisions exact, frequencies to 2e-7 relative (Brent tolerance; f64 direct-sum autocorrelation vs numpy FFT)."""
+voicing decisions exact, frequencies to 2e-7 relative (Brent tolerance; the kernel's own f64 radix-4/2 FFT
+autocorrelation vs numpy's FFT: the same transform, rounded differently)."""
 import numpy as np
 import pytest
 
@@ -76,6 +77,35 @@ def test_gpu_f0_matches_oracle():
         if v.any():
             exp = f0[b] * (223.25784012425046 / np.median(f0[b][v]))
             np.testing.assert_array_equal(f0d[b].cpu().numpy(), exp)
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fs,floor", [(24000, 250.0), (16000, 150.0), (24000, 150.0), (44100, 65.0)])
+def test_gpu_f0_fft_sizes(fs, floor):
+    """The autocorrelation FFT at every size the frame kernel has a plan for (nfft = the power of two >= 1.5 x the
+    3-period window): 512 (24 kHz with a 250 Hz floor, 16 kHz with 150 Hz), 1024 (24 kHz, 150 Hz) and 4096 (44.1 kHz,
+    65 Hz); the default configuration (2048) is test_gpu_f0_matches_oracle. Same bar as there."""
+    import torch
+    from svc_inference_pipeline_amd import config as C
+    from svc_inference_pipeline_amd.runtime import SVCEngine
+    P = PA.analysis_params(3 * fs, fs, 256 / fs, floor, 800.0)
+    cfg = C.load_config()
+    cfg.fs, cfg.f0_min = fs, floor
+    eng = SVCEngine(cfg, 0)
+    t = np.arange(3 * fs) / fs
+    clips = [(0.3 * np.sin(2 * np.pi * 330.0 * t * (1 + 0.03 * np.sin(2 * np.pi * 5.5 * t)))).astype(np.float32),
+             np.concatenate([np.sin(2 * np.pi * 420.0 * t[:fs]) * 0.2, np.zeros(2 * fs)]).astype(np.float32),
+             (np.random.default_rng(2).standard_normal(3 * fs) * 0.05).astype(np.float32)]
+    wav = torch.from_numpy(np.stack(clips)).cuda()
+    T = 3 * fs // 256 + 1
+    f0 = eng.f0(wav, T).cpu().numpy()
+    for b, x in enumerate(clips):
+        ref = PA.f0_features(x, T, fs=fs, floor=floor)
+        assert np.array_equal(f0[b] > 0, ref > 0), (P["nfft"], b)
+        rel = np.abs(f0[b] - ref) / np.maximum(np.abs(ref), 1e-300)
+        assert np.all(rel <= 1e-5), (P["nfft"], b, rel.max())
+        assert np.mean(rel > 2e-7) <= 0.01, (P["nfft"], b)
     eng.close()
 
 

@@ -200,31 +200,6 @@ def test_gate_ws_bit_identical(engine, B, T, frames, tune):
         assert np.array_equal(out[k], ref[k]), (k, rel_l2(out[k], ref[k]))
 
 
-@pytest.mark.parametrize("B,T,frames", [(1, 93, None), (3, 50, None), (2, 700, None), (5, 937, None), (16, 937, None),
-                                         (4, 301, [301, 17, 160, 299]), (3, 40, [9, 40, 1]), (40, 16, None)])
-def test_dlayer_gate_bit_identical(engine, B, T, frames, tune):
-    """dlayer.hip (the DiffSVC dilated conv + gate with the rows held in LDS and the weights streamed, 128-row tiles)
-    against gate_ws (the same 32-deep K order on one accumulator chain and the same gate arithmetic): eps bit for bit
-    equal on uniform, ragged-length (taps past an utterance's valid rows read zeros) and partial-tile batches, every
-    dilation (1, 2, 4, 8), and utterances of 16 frames (several utterance boundaries per tile)."""
-    rng = np.random.default_rng(B * 31 + T)
-    cond = dev(rng.standard_normal((B, T, 384)).astype(np.float32))
-    x = dev(rng.standard_normal((B, T, 100)).astype(np.float32))
-    tune(engine, gate_ws=1)
-    ref = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
-    tune(engine, gate_ws=2)
-    _lib.profile_enable(True)
-    try:
-        out = [engine.diffsvc_eps(cond, x, t, frames=frames).cpu().numpy() for t in (250, 7)]
-        ran = _lib.profile_read()
-    finally:
-        _lib.profile_enable(False)
-    assert sum(v["launches"] for k, v in ran.items() if k.startswith("dlayer")) > 0, ran.keys()
-    for k in range(2):
-        assert np.isfinite(out[k]).all()
-        assert np.array_equal(out[k], ref[k]), (k, rel_l2(out[k], ref[k]))
-
-
 @pytest.mark.parametrize("B,T", [(1, 93), (3, 50), (2, 700), (5, 937)])
 def test_fused_head(engine, states, cfg, B, T, tune):
     """diff_head.hip (relu(skip_projection) + output_projection in one launch, u kept on chip) against the
@@ -276,7 +251,7 @@ def test_fused_head_plms(engine, golden, tune):
     assert rel_l2(x4[0].cpu().numpy().T, g["plms4"]) < 1e-3
 
 
-@pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "15lds", "15reg", "20", "24"])
+@pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "16", "15lds", "15reg", "20", "24"])
 def test_eps_gemm_variants(engine, golden, variant, tune):
     """The paired gate epilogue and the residual / skip GEMMs under every GEMM tile variant (unfused path); 15lds:
     conv_gemm3 with the LDS-staged epilogue everywhere; 15reg: with every register form, in the sampler too."""
