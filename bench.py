@@ -83,6 +83,152 @@ def host_cpus():
                      "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
+class ClockSampler:
+    """The bench GPU's shader (SCLK) and memory (MCLK) clocks, read in-process from sysfs while the timed region runs
+    (a thread reading the card's pp_dpm_sclk / pp_dpm_mclk current level and hwmon's measured sclk every `period` s; no
+    subprocess), so that a box-speed shift shows next to `value`. Falls back to the amdsmi Python API when the card's
+    sysfs files are not readable. Every failure leaves the fields null with the reason."""
+
+    def __init__(self, device, period=0.05):
+        import threading
+        self.period = period
+        self.samples = []  # (t, sclk_dpm, mclk_dpm, sclk_hwmon) in MHz (None where unread)
+        self.err = None
+        self.src = None
+        self._stop = threading.Event()
+        self._thread = None
+        self._smi = None
+        self.files = {}
+        try:
+            p = torch.cuda.get_device_properties(device)
+            pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+            root = f"/sys/bus/pci/devices/{pci}"
+            self.pci = pci
+            for k, f in (("sclk", "pp_dpm_sclk"), ("mclk", "pp_dpm_mclk")):
+                if os.access(os.path.join(root, f), os.R_OK):
+                    self.files[k] = os.path.join(root, f)
+            hw = os.path.join(root, "hwmon")
+            if os.path.isdir(hw):
+                for h in sorted(os.listdir(hw)):
+                    lab = os.path.join(hw, h, "freq1_label")
+                    if os.path.exists(lab) and open(lab).read().strip() == "sclk":
+                        self.files["sclk_hwmon"] = os.path.join(hw, h, "freq1_input")
+            if self.files:
+                self.src = f"sysfs {root}"
+            else:
+                self._smi_init(p)
+        except Exception as e:  # noqa: BLE001 (reported, never fatal)
+            self.err = f"{type(e).__name__}: {e}"
+
+    def _smi_init(self, props):
+        import amdsmi
+        amdsmi.amdsmi_init()
+        want = props.pci_bus_id
+        for h in amdsmi.amdsmi_get_processor_handles():
+            bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)
+            if int(bdf.split(":")[1], 16) == want:
+                self._smi = (amdsmi, h)
+                self.src = f"amdsmi {bdf}"
+                return
+        raise RuntimeError("no amdsmi handle for the bench GPU")
+
+    @staticmethod
+    def _dpm_now(path):
+        for line in open(path):
+            if line.rstrip().endswith("*"):
+                return float(re.search(r"(\d+)\s*[Mm]hz", line).group(1))
+        return None
+
+    def read(self):
+        sc = mc = hw = None
+        if self._smi:
+            amdsmi, h = self._smi
+            sc = float(amdsmi.amdsmi_get_clock_info(h, amdsmi.AmdSmiClkType.GFX)["clk"])
+            mc = float(amdsmi.amdsmi_get_clock_info(h, amdsmi.AmdSmiClkType.MEM)["clk"])
+        else:
+            if "sclk" in self.files:
+                sc = self._dpm_now(self.files["sclk"])
+            if "mclk" in self.files:
+                mc = self._dpm_now(self.files["mclk"])
+            if "sclk_hwmon" in self.files:
+                hw = int(open(self.files["sclk_hwmon"]).read()) / 1e6
+        return sc, mc, hw
+
+    def _run(self):
+        t0 = time.perf_counter()
+        while not self._stop.is_set():
+            try:
+                self.samples.append((time.perf_counter() - t0,) + self.read())
+            except Exception as e:  # noqa: BLE001
+                self.err = f"{type(e).__name__}: {e}"
+                return
+            self._stop.wait(self.period)
+
+    def start(self):
+        import threading
+        if self.src and not self.err:
+            self._thread = threading.Thread(target=self._run, daemon=True)
+            self._thread.start()
+
+    def stop(self):
+        if self._thread:
+            self._stop.set()
+            self._thread.join()
+            try:
+                self.samples.append((None,) + self.read())  # the end of the timed region
+            except Exception as e:  # noqa: BLE001
+                self.err = f"{type(e).__name__}: {e}"
+
+    def summary(self):
+        out = {"source": self.src, "error": self.err, "samples": len(self.samples),
+               "period_s": self.period}
+        for i, k in ((1, "sclk_mhz"), (2, "mclk_mhz"), (3, "sclk_hwmon_mhz")):
+            v = [smp[i] for smp in self.samples if smp[i] is not None]
+            if v:
+                out[k] = {"start": v[0], "end": v[-1], "median": float(np.median(v)), "min": min(v), "max": max(v)}
+        return out
+
+
+def calibrate(device, seconds=1.0):
+    """A fixed box-speed probe, timed in this process after the timed region: torch.matmul (hipBLASLt) of two 4096 x
+    4096 fp16 matrices of seeded random values, back to back for about `seconds`, and a 1 GiB device copy. The same
+    code on every box and in every round, so a shift of `value` that the calibration shifts with is the box, not the
+    build. -> {"gemm_us": per GEMM, "gemm_tflops", "copy_gbs": read + write bytes / s}"""
+    g = torch.Generator(device=f"cuda:{device}").manual_seed(0)
+    a = torch.randn(4096, 4096, device=f"cuda:{device}", dtype=torch.float16, generator=g)
+    b = torch.randn(4096, 4096, device=f"cuda:{device}", dtype=torch.float16, generator=g)
+    for _ in range(5):
+        c = a @ b
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t0 < 0.2:  # size the loop
+        c = a @ b
+        n += 1
+        torch.cuda.synchronize()
+    reps = max(10, int(n * seconds / 0.2))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        c = a @ b
+    e1.record()
+    torch.cuda.synchronize()
+    gemm_us = e0.elapsed_time(e1) * 1000.0 / reps
+    x = torch.empty(1 << 29, device=f"cuda:{device}", dtype=torch.float16)
+    y = torch.empty_like(x)
+    y.copy_(x)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(20):
+        y.copy_(x)
+    e1.record()
+    torch.cuda.synchronize()
+    copy_gbs = 2.0 * x.numel() * 2 * 20 / (e0.elapsed_time(e1) / 1000.0) / 1e9
+    del a, b, c, x, y
+    return {"gemm": "torch.matmul fp16 4096^3, seeded random", "gemm_reps": reps, "gemm_us": round(gemm_us, 2),
+            "gemm_tflops": round(2 * 4096 ** 3 / (gemm_us * 1e-6) / 1e12, 1), "copy_gbs": round(copy_gbs, 1)}
+
+
 def cpu_baseline(cfg, ws, ms, vs, seconds, speedup, threads, hs=None, fast=True, host=None):
     """The oracle (CPU restatement of the reference path, torch-CPU fp32) on ONE clip of the same
     workload, timed on this host: mel/energy, F0, pitch shift, Whisper-medium, map, conditioner,
@@ -235,6 +381,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=10.0)
     ap.add_argument("--speedup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-calib", action="store_true", help="skip the box-speed calibration GEMM / copy")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads for the CPU baseline (default: every CPU available to the process)")
     ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -361,6 +508,8 @@ def main():
         _lib.profile_filter(dom_name)
         _lib.profile_enable(True)
     gather_s.clear()
+    clocks = ClockSampler(dist.local_rank)
+    clocks.start()
     t0 = time.time()
     for i in range(args.steps):
         out = step()
@@ -369,6 +518,7 @@ def main():
     torch.cuda.synchronize()
     dist.barrier()
     per_rank = [r[0] for r in dist.all_gather_floats([time.time() - t0])]
+    clocks.stop()
     gather_ms = [r[0] for r in dist.all_gather_floats([1000.0 * sum(gather_s) / max(len(gather_s), 1)])]
     elapsed = max(per_rank)
     if not timed_events:
@@ -461,6 +611,12 @@ def main():
                    "gbs": round(v["bytes"] / max(v["ms"], 1e-9) / 1e6, 1) if v["bytes"] else None}
                for k, v in sorted(prof_all.items(), key=lambda kv: -kv[1]["ms"])}
 
+    calib = None
+    if not args.no_calib:
+        try:
+            calib = calibrate(dist.local_rank)
+        except Exception as e:  # noqa: BLE001 (reported, never fatal)
+            calib = {"error": f"{type(e).__name__}: {e}"}
     cpu = None
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, 1 clip)...")
@@ -490,6 +646,9 @@ def main():
                        "global_batch": dist.world * B, "seq_len_frames": int((d24.shape[1] + 768 - 1024) // 256 + 1),
                        "parallelism": f"dp{dist.world} (per-utterance shards, RCCL gather)"},
             "roofline": roof, "cpu_baseline": cpu,
+            # box speed beside the value: rank 0's GPU clocks sampled through the timed region, and a fixed hipBLASLt
+            # GEMM / HBM copy calibration timed in this process after it (calib_us = that GEMM's time per launch)
+            "clocks": clocks.summary(), "calib": calib, "calib_us": calib.get("gemm_us") if calib else None,
             # SURVEY.md §8(d) algorithmic work (the reference's model FLOPs) and the end-to-end fraction of the MFMA
             # peak it sustains; executed_* counts the MFMA work actually issued (split-fp16 / weight-split duplicates)
             "algorithmic_tflops_per_step": round(alg_tf, 2),

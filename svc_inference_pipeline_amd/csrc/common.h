@@ -68,6 +68,25 @@ __device__ __forceinline__ float erf_fast(float x) {
   return copysignf(fmaf(-p * t, e, 1.0f), x);
 }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+// gelu_erf on a pair of values with the packed f32 VALU (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two values per
+// issue): erf_fast's and gelu_erf's operations per element, in the same order, so bit for bit gelu_erf's results.
+// For VALU-only epilogue stretches (the Whisper fc1 GELU of conv_gemm3's register epilogue).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 az = __builtin_elementwise_abs(z);
+  f32x2 t = __builtin_elementwise_fma(f32x2{0.3275911f, 0.3275911f}, az, f32x2{1.0f, 1.0f});
+  t = f32x2{__builtin_amdgcn_rcpf(t.x), __builtin_amdgcn_rcpf(t.y)};
+  f32x2 p = __builtin_elementwise_fma(f32x2{1.061405429f, 1.061405429f}, t, f32x2{-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, f32x2{1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, f32x2{-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, f32x2{0.254829592f, 0.254829592f});
+  const f32x2 q = (-1.4426950408889634f * az) * az;
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  const f32x2 r = __builtin_elementwise_fma(-p * t, e, f32x2{1.0f, 1.0f});
+  const f32x2 erf = f32x2{copysignf(r.x, z.x), copysignf(r.y, z.y)};
+  return (0.5f * x) * (1.0f + erf);
+}
 // saturating fp32 -> fp16 store (NaN stays NaN): random-weight regimes can exceed the fp16 range
 __device__ __forceinline__ f16 f16_sat(float v) { return (f16)(v > 65504.f ? 65504.f : (v < -65504.f ? -65504.f : v)); }
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
@@ -305,6 +324,26 @@ struct PlmsArgs {
   float* e_avg_out;  // optional: store e' (used for the first PLMS step's x_pred path)
   int bf16;          // x16 holds bfloat16 operands (the bf16 variant)
 };
+// The PLMS update of 4 consecutive channels of one row, e_k = ev[k] (k < p.ne), x the row's current values:
+// e' = (c_0 e_0 + c_1 e_1 + ...) / div in the reference's left-to-right order, x' = x + d (A x - Bc e') (the x16 copy is
+// the caller's). One definition for plms4_kernel and the fused diff_head epilogue, so both issue the same operations.
+__device__ __forceinline__ void plms_math4(const PlmsArgs& p, const float4* ev, float4 x, float4& e_out, float4& x_out) {
+  float e[4] = {p.c[0] * ev[0].x, p.c[0] * ev[0].y, p.c[0] * ev[0].z, p.c[0] * ev[0].w};
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    if (p.ne > k) {
+      e[0] = e[0] + p.c[k] * ev[k].x;
+      e[1] = e[1] + p.c[k] * ev[k].y;
+      e[2] = e[2] + p.c[k] * ev[k].z;
+      e[3] = e[3] + p.c[k] * ev[k].w;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) e[k] = e[k] / p.div;
+  e_out = make_float4(e[0], e[1], e[2], e[3]);
+  x_out = make_float4(x.x + p.d * (p.A * x.x - p.Bc * e[0]), x.y + p.d * (p.A * x.y - p.Bc * e[1]),
+                      x.z + p.d * (p.A * x.z - p.Bc * e[2]), x.w + p.d * (p.A * x.w - p.Bc * e[3]));
+}
 // Kernel-selection switches: the measured production choices by default, other values select the earlier or
 // alternative kernel forms that the parity tests cover and the A/B benches compare (DESIGN.md records each result).
 // A context copies the defaults at creation, where an SVC_<NAME> environment variable overrides each (so a whole
@@ -319,7 +358,8 @@ struct Tuning {
   int whisper_streams = 1;  // Whisper encoder sub-batch streams
   int sampler_streams = 1;  // DiffSVC sampler sub-batch streams (round 4: 1 with gate_ws; 2 was the conv_gemm4 default)
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
-  int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip)
+  int diff_head = 2;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip); 2: with the
+                            // PLMS update in its epilogue, 1: the update as its own launch, 0: two GEMMs
   int amp_maxc = 48;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none)
   int res_proj = 1;         // DiffSVC residual and input projections on the weight-stationary streams (res_proj.hip
                             // res_proj / mel_proj; 0: conv_gemm3;

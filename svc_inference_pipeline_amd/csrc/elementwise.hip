@@ -379,24 +379,14 @@ __global__ void plms4_kernel(PlmsArgs p, int rows, int C) {
   if (i4 >= (int64_t)rows * C4) return;
   const int64_t i = i4 * 4;
   auto ld = [&](const float* q) { return *reinterpret_cast<const float4*>(q + i); };
-  float4 e0 = ld(p.e[0]);
-  float e[4] = {p.c[0] * e0.x, p.c[0] * e0.y, p.c[0] * e0.z, p.c[0] * e0.w};
+  float4 ev[4];
+  ev[0] = ld(p.e[0]);
 #pragma unroll
-  for (int k = 1; k < 4; ++k) {
-    if (p.ne > k) {
-      const float4 v = ld(p.e[k]);
-      e[0] = e[0] + p.c[k] * v.x;
-      e[1] = e[1] + p.c[k] * v.y;
-      e[2] = e[2] + p.c[k] * v.z;
-      e[3] = e[3] + p.c[k] * v.w;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) e[k] = e[k] / p.div;
-  if (p.e_avg_out) *reinterpret_cast<float4*>(p.e_avg_out + i) = make_float4(e[0], e[1], e[2], e[3]);
-  const float4 x = ld(p.xin);
-  const float4 xn = make_float4(x.x + p.d * (p.A * x.x - p.Bc * e[0]), x.y + p.d * (p.A * x.y - p.Bc * e[1]),
-                                x.z + p.d * (p.A * x.z - p.Bc * e[2]), x.w + p.d * (p.A * x.w - p.Bc * e[3]));
+  for (int k = 1; k < 4; ++k)
+    if (p.ne > k) ev[k] = ld(p.e[k]);
+  float4 e, xn;
+  plms_math4(p, ev, ld(p.xin), e, xn);
+  if (p.e_avg_out) *reinterpret_cast<float4*>(p.e_avg_out + i) = e;
   *reinterpret_cast<float4*>(p.xout + i) = xn;
   if (p.x16) {
     const int64_t r = i4 / C4;
@@ -408,13 +398,18 @@ __global__ void plms4_kernel(PlmsArgs p, int rows, int C) {
   }
 }
 
-int plms_update(const PlmsArgs& p, int rows, int C, hipStream_t s) {
-  int64_t n = (int64_t)rows * C;
+// the 4-channel form's layout conditions (plms4_kernel, and the fused diff_head epilogue that uses the same form)
+bool plms_vec4_ok(const PlmsArgs& p, int C) {
   bool vec = C % 4 == 0 && (!p.x16 || p.ld16 % 4 == 0);
   const void* ptrs[] = {p.e[0], p.ne > 1 ? p.e[1] : nullptr, p.ne > 2 ? p.e[2] : nullptr, p.ne > 3 ? p.e[3] : nullptr,
                         p.xin, p.xout, p.e_avg_out, p.x16};
   for (int k = 0; k < 8; ++k) vec = vec && ((uintptr_t)ptrs[k] & (k == 7 ? 7 : 15)) == 0;
-  if (vec)
+  return vec;
+}
+
+int plms_update(const PlmsArgs& p, int rows, int C, hipStream_t s) {
+  int64_t n = (int64_t)rows * C;
+  if (plms_vec4_ok(p, C))
     hipLaunchKernelGGL(plms4_kernel, dim3(cdiv(n / 4, 256)), dim3(256), 0, s, p, rows, C);
   else
     hipLaunchKernelGGL(plms_kernel, dim3(cdiv(n, 256)), dim3(256), 0, s, p, rows, C);

@@ -392,8 +392,9 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
             const floatx4& c = acc[x][y][i][j];
             float4 v = make_float4(c[0] + cb[y][j].x, c[1] + cb[y][j].y, c[2] + cb[y][j].z, c[3] + cb[y][j].w);
             if constexpr (FORM == G3_F16) {
-              if (e.act == ACT_GELU) {
-                v.x = gelu_erf(v.x); v.y = gelu_erf(v.y); v.z = gelu_erf(v.z); v.w = gelu_erf(v.w);
+              if (e.act == ACT_GELU) {  // on value pairs (packed VALU), bit for bit gelu_erf
+                const f32x2 g0 = gelu_erf2(f32x2{v.x, v.y}), g1 = gelu_erf2(f32x2{v.z, v.w});
+                v = make_float4(g0.x, g0.y, g1.x, g1.y);
               } else if (e.act == ACT_RELU) {
                 v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
               }

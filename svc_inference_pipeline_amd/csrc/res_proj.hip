@@ -284,10 +284,13 @@ int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, c
 // Here one workgroup per CU walks 16-row tiles:
 //   * W_mel (384 x 128 f16, zero past k = 100) lives in VGPRs: each of 12 compute waves holds its 32 output columns as
 //     2 x 4 MFMA fragments (32 VGPRs), loaded once;
-//   * a 13th wave only loads: each tile's x rows (16 x ldx f16, one contiguous span) by LDS-DMA as four 1-KiB pieces
-//     into a ring of MP_D slots, MP_D - 1 tiles ahead (rows past M read 0). Its own counted vmcnt retires a tile before
-//     the barrier the compute waves pass to read it, and the compute waves' vmcnt holds only their stores, which so
-//     never delay a load wait;
+//   * a 13th wave only loads: each tile's x rows (16 x ldx f16) by LDS-DMA as four 1-KiB pieces into a ring of MP_D
+//     slots, MP_D - 1 tiles ahead (rows past M read 0). Its own counted vmcnt retires a tile before the barrier the
+//     compute waves pass to read it, and the compute waves' vmcnt holds only their stores, which so never delay a load
+//     wait. In LDS a row takes MP_RS = 14 16-B chunks (rows of up to 13 chunks, ldx <= 104, then padded; the lane of
+//     each LDS chunk picks its source chunk): the fragment reads (16 rows x one chunk, ds_read_b128 lane groups mixing
+//     rows of two chunk columns) are conflict-free at that stride, where the unpadded 13-chunk rows (ldx 104) put 2-way
+//     conflicts into every group (LDS-conflict share 0.47);
 //   * per tile a compute wave runs 8 swapped v_mfma_f32_16x16x32 (a lane's accumulator holds 4 consecutive columns of
 //     one row; k chunks past the row's ldx / 8 read as zero, as the padded tile does), swaps its two column blocks'
 //     values between lane rows (8 consecutive columns per lane) and stores hi / lo, 16 B per lane and half.
@@ -297,6 +300,7 @@ int res_proj(const f16* g, const f16* Wf, const float* bias, const float* sub, c
 constexpr int MP_NW = 12, MP_NT = 64 * (MP_NW + 1);  // compute waves (32 output columns each) + the loader wave
 constexpr int MP_D = 4;                              // ring slots (16-row tiles)
 constexpr int MP_SLOT = 4096;                        // 16 rows x ldx f16 (ldx <= 128): four 1-KiB DMA pieces
+constexpr int MP_RS = 14;                            // LDS row stride in 16-B chunks when ldx <= 104 (else ldx / 8)
 
 struct MelProjArgs {
   const f16* x;       // [M][ldx] sampler input in the 16-bit operand format
@@ -317,14 +321,24 @@ __global__ __launch_bounds__(MP_NT, 1) void mel_proj_kernel(MelProjArgs p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int G = gridDim.x;
   const int rowb = p.ldx * 2;  // bytes per x row
+  const int qmax = p.ldx / 8;  // 16-B chunks per x row
+  const int rs = qmax <= MP_RS - 1 ? MP_RS : qmax;  // LDS row stride (chunks)
   if (wave == MP_NW) {         // ---- loader
+    // LDS chunk u = 64 v + lane of a slot holds x row u / rs, chunk u % rs (the padding chunks and those past the
+    // 16 rows read nothing: out of the descriptor's range, zeros)
+    uint32_t src[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int u = 64 * v + lane, r = u / rs, c = u - r * rs;
+      src[v] = r < 16 && c < qmax ? (uint32_t)(r * rowb + c * 16) : 0x80000000u;
+    }
     auto issue = [&](int t) {  // tile t of this workgroup into slot t % MP_D (tiles past the end read zeros)
       const int row0 = (blockIdx.x + t * G) * 16;
       const bool live = row0 < p.M;
       const u32x4 d = rp_desc(p.x + (live ? (int64_t)row0 * p.ldx : 0), live ? (int64_t)(p.M - row0) * rowb : 0);
       unsigned char* slot = smm + (t % MP_D) * MP_SLOT;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) rp_dma(d, (uint32_t)(v * 1024 + lane * 16), slot + v * 1024);
+      for (int v = 0; v < 4; ++v) rp_dma(d, src[v], slot + v * 1024);
     };
 #pragma unroll
     for (int t = 0; t < MP_D - 1; ++t) issue(t);
@@ -340,7 +354,6 @@ __global__ __launch_bounds__(MP_NT, 1) void mel_proj_kernel(MelProjArgs p) {
   }
   // ---- compute waves
   const int fr = lane & 15, fk = lane >> 4;
-  const int qmax = p.ldx / 8;  // 16-B chunks per x row
   half8 w[2][4];
   const f16* wf = p.Wf + (size_t)wave * 8 * 512 + lane * 8;
 #pragma unroll
@@ -365,7 +378,7 @@ __global__ __launch_bounds__(MP_NT, 1) void mel_proj_kernel(MelProjArgs p) {
 #pragma unroll
     for (int kc = 0; kc < 4; ++kc) {
       const int q = kc * 4 + fk;
-      half8 a = *reinterpret_cast<const half8*>(slot + fr * rowb + (q < qmax ? q : 0) * 16);
+      half8 a = *reinterpret_cast<const half8*>(slot + (fr * rs + (q < qmax ? q : 0)) * 16);
       if (q >= qmax) a = zero;
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[j] = O::mfma(w[j][kc], a, acc[j]);  // acc[r] = C[row fr][n + r]

@@ -4,8 +4,7 @@
 
 namespace svc {
 
-// Channel pairs on the packed f32 VALU (v_pk_fma_f32 / v_pk_mul_f32: two channels per issue).
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+// Channel pairs on the packed f32 VALU (v_pk_fma_f32 / v_pk_mul_f32: two channels per issue; f32x2 in common.h).
 
 // SnakeBeta constants of channels c, c+1: alpha / 2pi (the sine's argument in revolutions) and 1 / (beta + 1e-9)
 struct SnakeCoef2 {
