@@ -291,26 +291,42 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
     // the PLMS update of these rows and columns in place of plms4_kernel's (the same plms_math4): the history operands
     // of every (row, column group) are loaded first, then eps, x' and its 16-bit copy are stored
     const PlmsArgs& q = p.plms;
-    float4 ev[2][4][4], xv[2][4];
+    // (addresses clamped into the tensors, so the loads need no per-lane branch: rows and columns past the ends are
+    // loaded from a valid place and never stored)
+    float4 ev[2][4][4] = {}, xv[2][4];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int n = wn * 32 + j * 16 + fk * 4;
+      const int n = min(wn * 32 + j * 16 + fk * 4, p.n_out - 4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wm * 64 + i * 16 + fr;
-        if (n >= p.n_out || m >= M) continue;
+        const int m = min(m0 + wm * 64 + i * 16 + fr, M - 1);
         const int64_t o = (int64_t)m * p.ld_eps + n;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (k < q.ne && k != p.plms_cur) ev[j][i][k] = *reinterpret_cast<const float4*>(q.e[k] + o);
+        for (int k = 0; k < 4; ++k)  // (every k: e_k past ne point at e_0 on the host; e_cur is replaced below)
+          ev[j][i][k] = *reinterpret_cast<const float4*>(q.e[k] + o);
         xv[j][i] = *reinterpret_cast<const float4*>(q.xin + o);
+      }
+    }
+    float4 bo[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) bo[j] = *reinterpret_cast<const float4*>(p.bout + min(wn * 32 + j * 16 + fk * 4, p.n_out - 4));
+    // every operand waited for here, once (as in the plain epilogue below: no vmcnt(0) before each store)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      asm volatile("" : "+v"(bo[j].x), "+v"(bo[j].y), "+v"(bo[j].z), "+v"(bo[j].w));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        asm volatile("" : "+v"(xv[j][i].x), "+v"(xv[j][i].y), "+v"(xv[j][i].z), "+v"(xv[j][i].w));
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          asm volatile("" : "+v"(ev[j][i][k].x), "+v"(ev[j][i][k].y), "+v"(ev[j][i][k].z), "+v"(ev[j][i][k].w));
       }
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = wn * 32 + j * 16 + fk * 4;
       if (n >= p.n_out) continue;
-      const float4 bi = *reinterpret_cast<const float4*>(p.bout + n);
+      const float4 bi = bo[j];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + fr;
@@ -335,17 +351,27 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
     }
     return;
   }
+  // both column groups' bias loaded and waited for once, before any store: waited for inside the per-row / per-column
+  // branches, the compiler's wait insertion (conservative at their joins) put a vmcnt(0) before every store, each
+  // draining the stores before it (assembly, r06)
+  float4 bi[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = min(wn * 32 + j * 16 + fk * 4, p.n_out - 4);
+    bi[j] = *reinterpret_cast<const float4*>(p.bout + n);
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(bi[j].x), "+v"(bi[j].y), "+v"(bi[j].z), "+v"(bi[j].w));
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = wn * 32 + j * 16 + fk * 4;
     if (n >= p.n_out) continue;
-    const float4 bi = *reinterpret_cast<const float4*>(p.bout + n);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = m0 + wm * 64 + i * 16 + fr;
       if (m >= M) continue;
-      *reinterpret_cast<float4*>(p.eps + (int64_t)m * p.ld_eps + n) =
-          make_float4(acc2[i][j][0] + bi.x, acc2[i][j][1] + bi.y, acc2[i][j][2] + bi.z, acc2[i][j][3] + bi.w);
+      *reinterpret_cast<float4*>(p.eps + (int64_t)m * p.ld_eps + n) = make_float4(
+          acc2[i][j][0] + bi[j].x, acc2[i][j][1] + bi[j].y, acc2[i][j][2] + bi[j].z, acc2[i][j][3] + bi[j].w);
     }
   }
 }
@@ -376,6 +402,7 @@ int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp
     p.plms_cur = -1;
     for (int k = 0; k < plms->ne; ++k)
       if (plms->e[k] == eps) p.plms_cur = k;
+    for (int k = plms->ne; k < 4; ++k) p.plms.e[k] = plms->e[0];  // (loaded, unused: the epilogue loads every e_k)
   }
   const void* fn = plms ? (bf16 ? (const void*)diff_head_kernel<true, true> : (const void*)diff_head_kernel<false, true>)
                         : (bf16 ? (const void*)diff_head_kernel<true, false> : (const void*)diff_head_kernel<false, false>);
