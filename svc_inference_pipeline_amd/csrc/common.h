@@ -326,7 +326,7 @@ struct PlmsArgs {
 };
 // The PLMS update of 4 consecutive channels of one row, e_k = ev[k] (k < p.ne), x the row's current values:
 // e' = (c_0 e_0 + c_1 e_1 + ...) / div in the reference's left-to-right order, x' = x + d (A x - Bc e') (the x16 copy is
-// the caller's). One definition for plms4_kernel and the fused diff_head epilogue, so both issue the same operations.
+// the caller's; plms4_kernel).
 __device__ __forceinline__ void plms_math4(const PlmsArgs& p, const float4* ev, float4 x, float4& e_out, float4& x_out) {
   float e[4] = {p.c[0] * ev[0].x, p.c[0] * ev[0].y, p.c[0] * ev[0].z, p.c[0] * ev[0].w};
 #pragma unroll
@@ -358,8 +358,7 @@ struct Tuning {
   int whisper_streams = 1;  // Whisper encoder sub-batch streams
   int sampler_streams = 1;  // DiffSVC sampler sub-batch streams (round 4: 1 with gate_ws; 2 was the conv_gemm4 default)
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
-  int diff_head = 2;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip); 2: with the
-                            // PLMS update in its epilogue, 1: the update as its own launch, 0: two GEMMs
+  int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip)
   int amp_maxc = 48;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none)
   int res_proj = 1;         // DiffSVC residual and input projections on the weight-stationary streams (res_proj.hip
                             // res_proj / mel_proj; 0: conv_gemm3;

@@ -11,11 +11,11 @@
 //           K runs hi . W_hi, hi . W_lo, lo . W_hi (the unfused GEMM: hi, lo, hi), so the f32 sum differs from the
 //           unfused path's in rounding order only (tests/test_gpu_stages.py::test_fused_head).
 // Same epilogue expressions as conv_gemm3's LDS epilogue for these two calls (relu(acc + bias), hi = f16(v),
-// lo = f16(v - hi); eps = acc + bias). Epilogue, PLMS instance (round 6, tune.diff_head = 2): the sampler's PLMS update
-// that consumes this eps (modules/diffsvcrepo_inference.py:116-130, plms4_kernel's plms_math4 on the lane's 4 columns),
-// so the update is no launch of its own; bit-identical (tests/test_gpu_stages.py test_head_plms_epilogue_bit_identical).
-// (Round 2 had built the PLMS update and the next denoise's input projection into an earlier form of this head, with
-// the sampler on two streams; both measured slower end to end then and were removed in round 3, DESIGN.md.)
+// lo = f16(v - hi); eps = acc + bias). Round 2 also built the following PLMS update and the next denoise's input
+// projection into this epilogue, and a fused residual layer (gate GEMM + output projection in one launch); all three
+// measured slower end to end and were removed in round 3. Round 6 built the PLMS update into this head's
+// epilogue once more (its operands loaded at once, the stores undrained): bit-identical and 0.1 % slower end to end
+// (2 x 101 fewer launches, but 8 waves per CU leave the epilogue's loads latency-bound), removed.
 #include "common.h"
 
 namespace svc {
@@ -67,13 +67,9 @@ struct DiffHeadArgs {
   const float* bout;
   float* eps;        // [rows][ld_eps]
   int ld_eps, n_out, M;
-  // the PLMS update that consumes this eps, applied in the epilogue (plms_cur >= -1), else -2; plms.e[plms_cur] is eps
-  // itself (its values are taken from registers; -1: none of the e_k is)
-  PlmsArgs plms;
-  int plms_cur;
 };
 
-template <bool BF, bool PLMS>
+template <bool BF>
 __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, const f16* zpage) {
   using O = Op16<BF>;  // operand format (binary16 or bfloat16)
   extern __shared__ __align__(16) unsigned char sm[];
@@ -287,70 +283,6 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
   }
   dl_vmwait<0>();  // the dummy DMAs of the last steps land before the workgroup's LDS is released
   // ---- eps = acc + b_out, columns < n_out
-  if constexpr (PLMS) {
-    // the PLMS update of these rows and columns in place of plms4_kernel's (the same plms_math4): the history operands
-    // of every (row, column group) are loaded first, then eps, x' and its 16-bit copy are stored
-    const PlmsArgs& q = p.plms;
-    // (addresses clamped into the tensors, so the loads need no per-lane branch: rows and columns past the ends are
-    // loaded from a valid place and never stored)
-    float4 ev[2][4][4] = {}, xv[2][4];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = min(wn * 32 + j * 16 + fk * 4, p.n_out - 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = min(m0 + wm * 64 + i * 16 + fr, M - 1);
-        const int64_t o = (int64_t)m * p.ld_eps + n;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)  // (every k: e_k past ne point at e_0 on the host; e_cur is replaced below)
-          ev[j][i][k] = *reinterpret_cast<const float4*>(q.e[k] + o);
-        xv[j][i] = *reinterpret_cast<const float4*>(q.xin + o);
-      }
-    }
-    float4 bo[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) bo[j] = *reinterpret_cast<const float4*>(p.bout + min(wn * 32 + j * 16 + fk * 4, p.n_out - 4));
-    // every operand waited for here, once (as in the plain epilogue below: no vmcnt(0) before each store)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      asm volatile("" : "+v"(bo[j].x), "+v"(bo[j].y), "+v"(bo[j].z), "+v"(bo[j].w));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        asm volatile("" : "+v"(xv[j][i].x), "+v"(xv[j][i].y), "+v"(xv[j][i].z), "+v"(xv[j][i].w));
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          asm volatile("" : "+v"(ev[j][i][k].x), "+v"(ev[j][i][k].y), "+v"(ev[j][i][k].z), "+v"(ev[j][i][k].w));
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = wn * 32 + j * 16 + fk * 4;
-      if (n >= p.n_out) continue;
-      const float4 bi = bo[j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wm * 64 + i * 16 + fr;
-        if (m >= M) continue;
-        const int64_t o = (int64_t)m * p.ld_eps + n;
-        const float4 e = make_float4(acc2[i][j][0] + bi.x, acc2[i][j][1] + bi.y, acc2[i][j][2] + bi.z, acc2[i][j][3] + bi.w);
-        *reinterpret_cast<float4*>(p.eps + o) = e;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (k == p.plms_cur) ev[j][i][k] = e;
-        float4 ea, xn;
-        plms_math4(q, ev[j][i], xv[j][i], ea, xn);
-        if (q.e_avg_out) *reinterpret_cast<float4*>(q.e_avg_out + o) = ea;
-        *reinterpret_cast<float4*>(q.xout + o) = xn;
-        if (q.x16) {
-          union { uint2 u; f16 h[4]; } pk;
-          pk.h[0] = enc16(xn.x, q.bf16); pk.h[1] = enc16(xn.y, q.bf16);
-          pk.h[2] = enc16(xn.z, q.bf16); pk.h[3] = enc16(xn.w, q.bf16);
-          *reinterpret_cast<uint2*>(q.x16 + (int64_t)m * q.ld16 + n) = pk.u;
-        }
-      }
-    }
-    return;
-  }
   // both column groups' bias loaded and waited for once, before any store: waited for inside the per-row / per-column
   // branches, the compiler's wait insertion (conservative at their joins) put a vmcnt(0) before every store, each
   // draining the stores before it (assembly, r06)
@@ -376,39 +308,21 @@ __global__ __launch_bounds__(DL_NT, 1) void diff_head_kernel(DiffHeadArgs p, con
   }
 }
 
-bool plms_vec4_ok(const PlmsArgs& p, int C);
-
-// plms (optional): the PLMS update that consumes eps (modules/diffsvcrepo_inference.py:116-130), applied in the
-// epilogue; its e_k, xin, xout (and x16) are [M][ld_eps] rows like eps, and the 4-channel layout conditions of
-// plms4_kernel hold (diff_head_plms_fits)
-bool diff_head_plms_fits(const PlmsArgs& q, int ld_eps, int Nout) {
-  return ld_eps == Nout && q.ne >= 1 && q.ne <= 4 && plms_vec4_ok(q, Nout);
-}
-
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
               int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
-              bool bf16, const PlmsArgs* plms) {
+              bool bf16) {
   SVC_REQUIRE(Nsp == DL_C && Ksp == 3 * DL_C && Kout == 3 * DL_C && Nout >= 1 && Nout <= 128 && Nout % 4 == 0 &&
                   Npad_out >= 128 && ld_eps % 4 == 0,
               "diff_head: shape (Nsp %d Ksp %d Nout %d Kout %d)", Nsp, Ksp, Nout, Kout);
   const void* ptrs[] = {s16, Wsp, bsp, Wout, bout, eps};
   for (const void* q : ptrs) SVC_REQUIRE(q && ((uintptr_t)q & 15) == 0, "diff_head: operand not 16-B aligned");
-  SVC_REQUIRE(!plms || diff_head_plms_fits(*plms, ld_eps, Nout), "diff_head: PLMS operands' layout");
   const int64_t grid = cdiv64(M, DL_BM);
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "diff_head: bad grid");
-  DiffHeadArgs p{s16, Wsp, bsp, Wout, bout, eps, ld_eps, Nout, M, PlmsArgs{}, -2};
-  if (plms) {
-    p.plms = *plms;
-    p.plms_cur = -1;
-    for (int k = 0; k < plms->ne; ++k)
-      if (plms->e[k] == eps) p.plms_cur = k;
-    for (int k = plms->ne; k < 4; ++k) p.plms.e[k] = plms->e[0];  // (loaded, unused: the epilogue loads every e_k)
-  }
-  const void* fn = plms ? (bf16 ? (const void*)diff_head_kernel<true, true> : (const void*)diff_head_kernel<false, true>)
-                        : (bf16 ? (const void*)diff_head_kernel<true, false> : (const void*)diff_head_kernel<false, false>);
+  DiffHeadArgs p{s16, Wsp, bsp, Wout, bout, eps, ld_eps, Nout, M};
+  const void* fn = bf16 ? (const void*)diff_head_kernel<true> : (const void*)diff_head_kernel<false>;
   if (int st = ensure_dyn_lds(fn, DH_LDS)) return st;
   const double flops = 2.0 * M * (double)DL_C * 3 * DL_C + 2.0 * M * (double)Nout * 3 * DL_C;
-  const int tok = prof_begin(plms ? "diff_head<128+plms>" : "diff_head<128>", flops, 0.0, s);
+  const int tok = prof_begin("diff_head<128>", flops, 0.0, s);
   void* args[] = {&p, const_cast<const f16**>(&zpage)};
   SVC_HIP_CHECK(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(DL_NT), args, DH_LDS, s));
   prof_end(tok, s);

@@ -398,8 +398,8 @@ __global__ void plms4_kernel(PlmsArgs p, int rows, int C) {
   }
 }
 
-// the 4-channel form's layout conditions (plms4_kernel, and the fused diff_head epilogue that uses the same form)
-bool plms_vec4_ok(const PlmsArgs& p, int C) {
+// the 4-channel form's layout conditions (plms4_kernel)
+static bool plms_vec4_ok(const PlmsArgs& p, int C) {
   bool vec = C % 4 == 0 && (!p.x16 || p.ld16 % 4 == 0);
   const void* ptrs[] = {p.e[0], p.ne > 1 ? p.e[1] : nullptr, p.ne > 2 ? p.e[2] : nullptr, p.ne > 3 ? p.e[3] : nullptr,
                         p.xin, p.xout, p.e_avg_out, p.x16};

@@ -124,8 +124,7 @@ int mel_proj_pack(const f16* W, int ldw, f16* Wf, hipStream_t s);
 size_t mel_proj_pack_elems();
 int diff_head(const f16* s16, const f16* Wsp, const float* bsp, int Nsp, int Ksp, const f16* Wout, const float* bout,
               int Nout, int Kout, int Npad_out, float* eps, int ld_eps, int M, const f16* zpage, hipStream_t s,
-              bool bf16, const PlmsArgs* plms = nullptr);
-bool diff_head_plms_fits(const PlmsArgs& q, int ld_eps, int Nout);
+              bool bf16);
 int pitch_shift(double* f0, int B, int T, double target, hipStream_t s);
 int content_map_hubert(const float* src, int B, int src_rows, int ld_src, int T, int D, f16* dst, int ld_dst,
                        hipStream_t s, bool bf);
@@ -2275,14 +2274,11 @@ static int denoise(svc_ctx* c, const DenoiseBufs& bb, const f16* x16, int B, int
   if (tuning().diff_head && H3 == 3 && C == 384 && c->skipproj.N == C && c->skipproj.Npad >= C &&
       c->skipproj.K == 3 * C && c->skipproj.Kpad == 3 * C && c->outproj.K == 3 * C && c->outproj.Kpad == 3 * C &&
       c->outproj.Npad >= 128 && c->outproj.N <= 128 && c->n_mel % 4 == 0) {
-    // tune.diff_head 2 (default): the PLMS update that consumes eps in the head's epilogue (plms4_kernel's operations,
-    // bit-identical); 1: the head alone, the update as its own launch
-    const bool fuse = plms && tuning().diff_head >= 2 && diff_head_plms_fits(*plms, c->n_mel, c->outproj.N);
     if ((st = diff_head(bb.s16, c->skipproj.W, c->skipproj.bias, C, 3 * C, c->outproj.W, c->outproj.bias,
                         c->outproj.N, 3 * C, c->outproj.Npad, eps, c->n_mel, (int)rows, zero_page(), s,
-                        c->skipproj.bf16, fuse ? plms : nullptr)))
+                        c->skipproj.bf16)))
       return st;
-    return plms && !fuse ? plms_update(*plms, rows, c->n_mel, s) : SVC_OK;
+    return plms ? plms_update(*plms, rows, c->n_mel, s) : SVC_OK;
   }
   e = epi();
   e.act = ACT_RELU;

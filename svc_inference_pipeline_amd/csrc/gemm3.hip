@@ -29,8 +29,6 @@
 //    the multi-tap convs yet ran 5-10 % slower; it was removed in round 3, DESIGN.md.)
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
-#include <string>
 #include "common.h"
 #include "epilogue.h"
 
@@ -98,30 +96,10 @@ __device__ __forceinline__ int half_row(int i, int h, int Q, int W) { return (i 
 //   G3_SPLIT: acc + bias, ((acc16_hi + acc16_lo) - acc_sub + v) / acc_div -> out16 = hi(v + add16), lo16 = lo
 enum { G3_LDS = 0, G3_F16 = 1, G3_RES32 = 2, G3_SPLIT = 3 };
 
-// vmcnt(n) for a wave-uniform runtime n (clamped to 63: a smaller count only waits longer)
-template <int I>
-__device__ __forceinline__ void vm_wait_dyn(int n) {
-  if constexpr (I >= 63) {
-    vm_wait<63>();
-  } else {
-    if (n <= I) vm_wait<I>();
-    else vm_wait_dyn<I + 1>(n);
-  }
-}
-
-// PERSIST (register epilogues, Kpad >= 128): grid = the resident slots, each workgroup walks a run of tiles of its XCD's
-// share (tiles t, t + grid / 8, ... of one contiguous eighth of the tile list, so the workgroups of an XCD work on
-// consecutive tiles, as the one-tile-per-workgroup launch places them). The DMA stream does not stop at a tile's end: the
-// last two K-tiles issue the next tile's first two K-tiles where the single-tile form issues dummies (the A / B half
-// states switch to the next tile at their first DMA for it), then the finished tile's epilogue runs while those land,
-// and its stores drain behind the next tile's K-loop. gfx950 counts stores in vmcnt, so the next tile's first three
-// counted waits (whose half-tiles were issued before the epilogue) add the epilogue's stores to their counts instead of
-// waiting for the stores to be acknowledged (the round-5 persistent form waited for them: 3 % slower, r05al).
-template <int BM, int BN, bool CP64, bool PAIR, int FORM = G3_LDS, bool BF = false, bool PERSIST = false>
+template <int BM, int BN, bool CP64, bool PAIR, int FORM = G3_LDS, bool BF = false>
 __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiArgs e, const f16* zpage,
                                                            float inv_cp) {
   static_assert(FORM == G3_LDS || !PAIR, "register epilogues: generic epilogues only");
-  static_assert(!PERSIST || FORM != G3_LDS, "persistent form: register epilogues only (the LDS epilogue needs the ring)");
   using CF = G3<BM, BN>;
   // the paired gate epilogue (epilogue_pass<PAIR>) walks 64-column gate | filter blocks: every LDS pass must hold whole
   // blocks (the 256 x 192 tile's two 96-column passes do not)
@@ -135,26 +113,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
   const bool bfull = CF::BH == CF::BHL || wave < CF::BW;  // this wave issues BH (else BHL) B pieces per half-tile
 
   const int nwg = gridDim.x, orig = blockIdx.x;
-  const int xcd = orig & 7;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tile_n = wgid % a.ntiles_n, tile_m = wgid / a.ntiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int M = a.B * a.T_out;
   const int nk = a.Kpad / 64;
   const f16* zsrc = zpage + lane * 8;
-  // this workgroup's tiles: tile, tile + tile_step, ... < tile_end
-  int tile, tile_end, tile_step;
-  if constexpr (PERSIST) {
-    const int ntiles = ((M + BM - 1) / BM) * a.ntiles_n;  // (host: grid % 8 == 0, ntiles >= grid)
-    tile = (int)((int64_t)ntiles * xcd / 8) + (orig >> 3);
-    tile_end = (int)((int64_t)ntiles * (xcd + 1) / 8);
-    tile_step = nwg >> 3;
-  } else {
-    const int q8 = nwg >> 3, r8 = nwg & 7;
-    tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
-    tile_end = tile + 1;
-    tile_step = 1;
-  }
-  int m0 = (tile / a.ntiles_n) * BM, n0 = (tile % a.ntiles_n) * BN;
-  int nm0 = 0, nn0 = 0;  // the next tile's (PERSIST)
-  bool nxt_ = false;     // PERSIST: this workgroup has a next tile
 
   // ---- DMA slots. A half h, instruction v: image rows rb .. rb+7, lane -> row rb + (lane >> 3),
   // LDS chunk lane & 7 holding logical k-chunk kv = sw3(row, lane & 7).
@@ -167,20 +132,15 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
     for (int v = 0; v < CF::AH; ++v) {
       const int u = wave + 8 * v;
       const int rb = half_row(8 * u, h, CF::QM, CF::WTM);
+      const int row = rb + (lane >> 3);
+      const int kv = sw3(row, lane & 7);
       a_rb[h][v] = rb;
-      a_kv[h][v] = sw3(rb + (lane >> 3), lane & 7);
-    }
-  // the A half h state of the tile whose rows start at mb; tin (optional): the rows' valid input rows, loaded earlier
-  // (PERSIST: a ragged batch's length-table load inside the K-loop would make the compiler drain the DMAs in flight)
-  auto setup_a = [&](int h, int mb, const int* tin) __attribute__((always_inline)) {
-#pragma unroll
-    for (int v = 0; v < CF::AH; ++v) {
-      const int m = mb + a_rb[h][v] + (lane >> 3);
-      const int kv = a_kv[h][v];
+      a_kv[h][v] = kv;
+      const int m = m0 + row;
       if (m < M) {
         const int b = m / a.T_out, t = m - b * a.T_out;
         a_t[h][v] = t * a.istride;
-        a_tin[h][v] = tin ? tin[v] : valid_in_rows(a, b);
+        a_tin[h][v] = valid_in_rows(a, b);
         a_p[h][v] = a.X + (int64_t)b * a.T_in * a.ldx + kv * 8;
         a_row[h][v] = (uint32_t)(((b * a.T_in + a_t[h][v]) * a.ldx + kv * 8) * 2);
       } else {
@@ -191,7 +151,6 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
       }
       a_voff[h][v] = G3_OOR;
     }
-  };
   int b_rb[2][CF::BH];
   const f16* b_p[2][CF::BH];
   uint32_t b_voff[2][CF::BH];
@@ -200,35 +159,22 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
 #pragma unroll
     for (int v = 0; v < CF::BH; ++v) {
       const int u = min(wave + 8 * v, BN / 16 - 1);  // (u past the half-tile: a wave with BHL pieces, never issued)
-      b_rb[h][v] = half_row(8 * u, h, CF::QN, CF::WTN);
+      const int rb = half_row(8 * u, h, CF::QN, CF::WTN);
+      const int row = rb + (lane >> 3);
+      b_rb[h][v] = rb;
+      b_p[h][v] = a.W + (int64_t)(n0 + row) * a.Kpad + sw3(row, lane & 7) * 8;
+      b_voff[h][v] = (uint32_t)(((n0 + row) * a.Kpad + sw3(row, lane & 7) * 8) * 2);
     }
-  // the B half h state of the tile whose columns start at nb
-  auto setup_b = [&](int h, int nb) __attribute__((always_inline)) {
-#pragma unroll
-    for (int v = 0; v < CF::BH; ++v) {
-      const int row = b_rb[h][v] + (lane >> 3);
-      b_p[h][v] = a.W + (int64_t)(nb + row) * a.Kpad + sw3(row, lane & 7) * 8;
-      b_voff[h][v] = (uint32_t)(((nb + row) * a.Kpad + sw3(row, lane & 7) * 8) * 2);
-    }
-  };
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    setup_a(h, m0, nullptr);
-    setup_b(h, n0);
-  }
-  int ntin[2][CF::AH];  // PERSIST: the next tile's valid input rows per A row (loaded at the current tile's start)
   // CP64 descriptors (unused otherwise); extents checked on the host (< 1 GiB: no voffset + soffset wraps)
   const __amdgpu_buffer_rsrc_t rx =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.X), (short)0, a.B * a.T_in * a.ldx * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<f16*>(a.W), (short)0, a.ntiles_n * BN * a.Kpad * 2, 0x00020000);
 
-  // LDS images of stream position g (the workgroup's running K-tile count: g & 1 selects the buffer)
-  auto a_img = [&](int g) { return sm3 + (g & 1) * CF::TILE; };
-  auto b_img = [&](int g) { return sm3 + (g & 1) * CF::TILE + BM * 128; };
-  // half h of the current state's K-tile kt (kt >= nk: zeros) into the images of stream position g
-  auto issue_a = [&](int h, int kt, int g) {
-    unsigned char* dst = a_img(g);
+  auto a_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE; };
+  auto b_img = [&](int kt) { return sm3 + (kt & 1) * CF::TILE + BM * 128; };
+  auto issue_a = [&](int h, int kt) {
+    unsigned char* dst = a_img(kt);
     if constexpr (CP64) {
       // the whole K-tile lies in tap `tap`; columns c0 .. c0+63 of it. Each half sees kt = 0, 1, 2, ... in order, so
       // its voffsets are recomputed at the first K-tile of every tap; past the end (kt >= nk) the DMAs land zeros
@@ -266,8 +212,8 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
       }
     }
   };
-  auto issue_b = [&](int h, int kt, int g) {
-    unsigned char* dst = b_img(g);
+  auto issue_b = [&](int h, int kt) {
+    unsigned char* dst = b_img(kt);
     if constexpr (CP64) {
 #pragma unroll
       for (int v = 0; v < CF::BH; ++v)
@@ -282,44 +228,30 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
     }
   };
 
-  // a phase's wait: this wave's pieces of the two half-tiles issued after the ones to retire (2 AH + 2 B pieces), plus
-  // `extra` younger operations (PERSIST: the previous tile's epilogue stores, issued after those half-tiles)
-  auto g3_wait = [&](int extra) __attribute__((always_inline)) {
-    if (extra == 0) {
-      if (bfull) vm_wait<2 * CF::AH + 2 * CF::BH>();
-      else vm_wait<2 * CF::AH + 2 * CF::BHL>();
-    } else {
-      vm_wait_dyn<0>((bfull ? 2 * CF::AH + 2 * CF::BH : 2 * CF::AH + 2 * CF::BHL) + extra);
-    }
+  // a phase's wait: this wave's pieces of the two half-tiles issued after the ones to retire (2 AH + 2 B pieces)
+  auto g3_wait = [&]() __attribute__((always_inline)) {
+    if (bfull) vm_wait<2 * CF::AH + 2 * CF::BH>();
+    else vm_wait<2 * CF::AH + 2 * CF::BHL>();
   };
   floatx4 acc[2][2][CF::FQM][CF::FQN];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int i = 0; i < CF::FQM; ++i)
+#pragma unroll
+        for (int j = 0; j < CF::FQN; ++j) acc[x][y][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
   half8 af[CF::FQM][2], bfl[CF::FQN][2], bfh[CF::FQN][2];
   const int fr = lane & 15, fk = lane >> 4;
 
-  // one phase: quadrant (QMI, QNI) of stream position g = the current tile's K-tile kt. The restaged half-tiles are
-  // K-tiles kt + 1 / kt + 2 of this tile or, past its end, the next tile's first two (PERSIST, nxt) or dummies; a half's
-  // state switches to the next tile at its first DMA for it (its last use for this tile was two phases or more earlier)
-  auto stream_a = [&](int h, int kq, int g) __attribute__((always_inline)) {  // kq = kt + 1 or kt + 2
-    if (PERSIST && nxt_ && kq >= nk) {
-      if (kq == nk) setup_a(h, nm0, ntin[h]);
-      issue_a(h, kq - nk, g);
-    } else {
-      issue_a(h, kq, g);
-    }
-  };
-  auto stream_b = [&](int h, int kq, int g) __attribute__((always_inline)) {
-    if (PERSIST && nxt_ && kq >= nk) {
-      if (kq == nk) setup_b(h, nn0);
-      issue_b(h, kq - nk, g);
-    } else {
-      issue_b(h, kq, g);
-    }
-  };
-  auto phase = [&](auto QMI_, auto QNI_, int kt, int g, int extra) {
+  // one phase: quadrant (QMI, QNI) of K-tile kt
+  auto phase = [&](auto QMI_, auto QNI_, int kt) {
     constexpr int QMI = decltype(QMI_)::value, QNI = decltype(QNI_)::value;
     constexpr int P = QMI * 2 + QNI;
-    const unsigned char* Ab = a_img(g);
-    const unsigned char* Bb = b_img(g);
+    const unsigned char* Ab = a_img(kt);
+    const unsigned char* Bb = b_img(kt);
     // ---- L section: A-lo + B-lo (phase 0), B-hi (1), A-hi (2); phase 3 reuses A-hi and B-hi
     if constexpr (QNI == 0) {
 #pragma unroll
@@ -346,16 +278,16 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
     }
     // restage one half-tile; each wait retires the half-tiles the next phase reads (3 phases read; phase 3 none)
     if constexpr (P == 0) {
-      stream_b(1, kt + 1, g + 1);
-      g3_wait(extra);
+      issue_b(1, kt + 1);
+      g3_wait();
     } else if constexpr (P == 1) {
-      stream_a(1, kt + 1, g + 1);
-      g3_wait(extra);
+      issue_a(1, kt + 1);
+      g3_wait();
     } else if constexpr (P == 2) {
-      stream_a(0, kt + 2, g + 2);
+      issue_a(0, kt + 2);
     } else {
-      stream_b(0, kt + 2, g + 2);
-      g3_wait(extra);
+      issue_b(0, kt + 2);
+      g3_wait();
     }
     g3_barrier();
     // ---- M section
@@ -375,247 +307,193 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
     __builtin_amdgcn_s_setprio(0);
     g3_barrier();
   };
-  using I0 = std::integral_constant<int, 0>;
-  using I1 = std::integral_constant<int, 1>;
+
   // ---- prologue: A-lo(0), B-lo(0), B-hi(0), A-hi(0), A-lo(1), B-lo(1) in flight; retire the first two (the state
   // phase 3 of K-tile -1 would leave)
-  issue_a(0, 0, 0);
-  issue_b(0, 0, 0);
-  issue_b(1, 0, 0);
-  issue_a(1, 0, 0);
-  issue_a(0, 1, 1);
-  issue_b(0, 1, 1);
-  g3_wait(0);
+  issue_a(0, 0);
+  issue_b(0, 0);
+  issue_b(1, 0);
+  issue_a(1, 0);
+  issue_a(0, 1);
+  issue_b(0, 1);
+  g3_wait();
   g3_barrier();
-  int g0 = 0;     // stream position of the current tile's K-tile 0
-  int extra = 0;  // PERSIST: vector-memory operations of the previous tile's epilogue still counted (its stores)
-  for (;;) {
-    const bool nxt = PERSIST && tile + tile_step < tile_end;
-    nxt_ = nxt;
-    if constexpr (PERSIST) {
-      const int nt = tile + tile_step;
-      nm0 = (nt / a.ntiles_n) * BM;
-      nn0 = (nt % a.ntiles_n) * BN;
+  if (grp == 1) g3_barrier();  // stagger: group 1 runs one barrier behind group 0
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  for (int kt = 0; kt < nk; ++kt) {
+    phase(I0{}, I0{}, kt);
+    phase(I0{}, I1{}, kt);
+    phase(I1{}, I0{}, kt);
+    phase(I1{}, I1{}, kt);
+  }
+  if (grp == 0) g3_barrier();
+  vm_wait<0>();  // trailing dummy DMAs land before the ring is reused for C staging (or the workgroup ends)
+  if constexpr (FORM != G3_LDS) {
+    union H4 { uint2 u; f16 h[4]; };
+    // column groups (y, j): packed columns nq .. nq + 3; their bias (and per-column vectors) loaded once
+    float4 cb[2][CF::FQN], cs[2][CF::FQN], ca[2][CF::FQN];
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+    for (int y = 0; y < 2; ++y)
 #pragma unroll
-        for (int v = 0; v < CF::AH; ++v) {
-          const int m = nm0 + a_rb[h][v] + (lane >> 3);
-          ntin[h][v] = nxt && m < M ? valid_in_rows(a, m / a.T_out) : 0;
+      for (int j = 0; j < CF::FQN; ++j) {
+        const int n = min(n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4, a.N - 4);
+        cb[y][j] = *reinterpret_cast<const float4*>(e.bias + n);
+        if constexpr (FORM == G3_SPLIT) cs[y][j] = *reinterpret_cast<const float4*>(e.acc_sub + n);
+        if constexpr (FORM != G3_F16) {
+          if (e.add16) ca[y][j] = *reinterpret_cast<const float4*>(e.add16 + n);
         }
+      }
+    // G3_F16: wait for the bias here, once. Waited for inside the per-row / per-lane branches below, the compiler's
+    // wait insertion (conservative where those branches join) drains every store issued before, in every row: Whisper
+    // fc1 / qkv 1-2 % faster (r05ai). (The same for the residual forms' row operands measured 2-4 % slower.)
+    if constexpr (FORM == G3_F16) {
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int j = 0; j < CF::FQN; ++j)
+          asm volatile("" : "+v"(cb[y][j].x), "+v"(cb[y][j].y), "+v"(cb[y][j].z), "+v"(cb[y][j].w));
     }
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int i = 0; i < CF::FQM; ++i)
-#pragma unroll
-          for (int j = 0; j < CF::FQN; ++j) acc[x][y][i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    if (grp == 1) g3_barrier();  // stagger: group 1 runs one barrier behind group 0
-    // K-tiles (the first one's waits with the extra count)
-    for (int kt = 0; kt < nk; ++kt) {
-      const int ex = kt == 0 ? extra : 0;
-      phase(I0{}, I0{}, kt, g0 + kt, ex);
-      phase(I0{}, I1{}, kt, g0 + kt, ex);
-      phase(I1{}, I0{}, kt, g0 + kt, ex);
-      phase(I1{}, I1{}, kt, g0 + kt, ex);
-    }
-    if (grp == 0) g3_barrier();
-    if constexpr (!PERSIST) vm_wait<0>();  // trailing dummy DMAs land before the ring is reused for C staging (or the workgroup ends)
-    if constexpr (FORM != G3_LDS) {
-      union H4 { uint2 u; f16 h[4]; };
-      // column groups (y, j): packed columns nq .. nq + 3; their bias (and per-column vectors) loaded once
-      float4 cb[2][CF::FQN], cs[2][CF::FQN], ca[2][CF::FQN];
-#pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int j = 0; j < CF::FQN; ++j) {
-          const int n = min(n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4, a.N - 4);
-          cb[y][j] = *reinterpret_cast<const float4*>(e.bias + n);
-          if constexpr (FORM == G3_SPLIT) cs[y][j] = *reinterpret_cast<const float4*>(e.acc_sub + n);
-          if constexpr (FORM != G3_F16) {
-            if (e.add16) ca[y][j] = *reinterpret_cast<const float4*>(e.add16 + n);
-          }
-        }
-      // G3_F16: wait for the bias here, once. Waited for inside the per-row / per-lane branches below, the compiler's
-      // wait insertion (conservative where those branches join) drains every store issued before, in every row: Whisper
-      // fc1 / qkv 1-2 % faster (r05ai). (The same for the residual forms' row operands measured 2-4 % slower.)
-      if constexpr (FORM == G3_F16) {
-#pragma unroll
-        for (int y = 0; y < 2; ++y)
-#pragma unroll
-          for (int j = 0; j < CF::FQN; ++j)
-            asm volatile("" : "+v"(cb[y][j].x), "+v"(cb[y][j].y), "+v"(cb[y][j].z), "+v"(cb[y][j].w));
-      }
-#pragma unroll
-      for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int i = 0; i < CF::FQM; ++i) {
-          const int m = m0 + wm * CF::WTM + x * CF::QM + i * 16 + fr;
-          if (m >= M) continue;
-          const int b = m / a.T_out, t = m - b * a.T_out;
-          const int64_t orow = (int64_t)b * e.T_ostore + (int64_t)t * e.ostride + e.ophase;
-          // this row's residual operands for every column group, loaded before any of its stores (which may alias
-          // them, so the compiler cannot move a later group's loads above an earlier group's stores)
-          float4 pr[2][CF::FQN], pq[2][CF::FQN];  // RES32: add_row, acc32; SPLIT: the hi / lo halves as raw bits
-          if constexpr (FORM != G3_F16) {
-#pragma unroll
-            for (int y = 0; y < 2; ++y)
-#pragma unroll
-              for (int j = 0; j < CF::FQN; ++j) {
-                const int n = min(n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4, a.N - 4);
-                pr[y][j] = pq[y][j] = make_float4(0.f, 0.f, 0.f, 0.f);
-                if constexpr (FORM == G3_SPLIT) {
-                  const uint2 h = *reinterpret_cast<const uint2*>(e.acc16_hi + orow * e.ld_acc + n);
-                  const uint2 l = *reinterpret_cast<const uint2*>(e.acc16_lo + orow * e.ld_acc + n);
-                  pq[y][j] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x),
-                                         __uint_as_float(l.y));
-                } else {
-                  if (e.add_row) pr[y][j] = *reinterpret_cast<const float4*>(e.add_row + orow * e.ld_add_row + n);
-                  if (e.acc32) pq[y][j] = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
-                }
-              }
-          }
+      for (int i = 0; i < CF::FQM; ++i) {
+        const int m = m0 + wm * CF::WTM + x * CF::QM + i * 16 + fr;
+        if (m >= M) continue;
+        const int b = m / a.T_out, t = m - b * a.T_out;
+        const int64_t orow = (int64_t)b * e.T_ostore + (int64_t)t * e.ostride + e.ophase;
+        // this row's residual operands for every column group, loaded before any of its stores (which may alias
+        // them, so the compiler cannot move a later group's loads above an earlier group's stores)
+        float4 pr[2][CF::FQN], pq[2][CF::FQN];  // RES32: add_row, acc32; SPLIT: the hi / lo halves as raw bits
+        if constexpr (FORM != G3_F16) {
 #pragma unroll
           for (int y = 0; y < 2; ++y)
 #pragma unroll
             for (int j = 0; j < CF::FQN; ++j) {
-              const int n = n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4;
-              if (n >= a.N) continue;
-              const floatx4& c = acc[x][y][i][j];
-              float4 v = make_float4(c[0] + cb[y][j].x, c[1] + cb[y][j].y, c[2] + cb[y][j].z, c[3] + cb[y][j].w);
-              if constexpr (FORM == G3_F16) {
-                if (e.act == ACT_GELU) {  // on value pairs (packed VALU), bit for bit gelu_erf
-                  const f32x2 ge0 = gelu_erf2(f32x2{v.x, v.y}), ge1 = gelu_erf2(f32x2{v.z, v.w});
-                  v = make_float4(ge0.x, ge0.y, ge1.x, ge1.y);
-                } else if (e.act == ACT_RELU) {
-                  v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-                }
-                if (n < e.scale_cols) {
-                  const float cs = n < e.scale_cols2 ? e.col_scale2 : e.col_scale;
-                  v.x *= cs; v.y *= cs; v.z *= cs; v.w *= cs;
-                }
-                H4 pk;
-                pk.h[0] = O::enc(v.x); pk.h[1] = O::enc(v.y); pk.h[2] = O::enc(v.z); pk.h[3] = O::enc(v.w);
-                f16* o = e.out16 + orow * e.ld16 + n;
-                *reinterpret_cast<uint2*>(o) = pk.u;
-                if (e.split16) {
-                  H4 lo;
-                  lo.h[0] = O::enc_lo(v.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(v.y - O::dec(pk.h[1]));
-                  lo.h[2] = O::enc_lo(v.z - O::dec(pk.h[2])); lo.h[3] = O::enc_lo(v.w - O::dec(pk.h[3]));
-                  *reinterpret_cast<uint2*>(o + e.split16) = lo.u;
-                  *reinterpret_cast<uint2*>(o + 2 * e.split16) = pk.u;
-                }
+              const int n = min(n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4, a.N - 4);
+              pr[y][j] = pq[y][j] = make_float4(0.f, 0.f, 0.f, 0.f);
+              if constexpr (FORM == G3_SPLIT) {
+                const uint2 h = *reinterpret_cast<const uint2*>(e.acc16_hi + orow * e.ld_acc + n);
+                const uint2 l = *reinterpret_cast<const uint2*>(e.acc16_lo + orow * e.ld_acc + n);
+                pq[y][j] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x),
+                                       __uint_as_float(l.y));
               } else {
-                if constexpr (FORM == G3_RES32) {
-                  if (e.add_row) {
-                    const float4 ar = pr[y][j];
-                    v.x += ar.x; v.y += ar.y; v.z += ar.z; v.w += ar.w;
-                  }
-                }
-                float4 ac;
-                bool has_acc = true;
-                if constexpr (FORM == G3_SPLIT) {
-                  H4 hi, lo;
-                  hi.u = make_uint2(__float_as_uint(pq[y][j].x), __float_as_uint(pq[y][j].y));
-                  lo.u = make_uint2(__float_as_uint(pq[y][j].z), __float_as_uint(pq[y][j].w));
-                  ac.x = (O::dec(hi.h[0]) + O::dec(lo.h[0])) - cs[y][j].x;
-                  ac.y = (O::dec(hi.h[1]) + O::dec(lo.h[1])) - cs[y][j].y;
-                  ac.z = (O::dec(hi.h[2]) + O::dec(lo.h[2])) - cs[y][j].z;
-                  ac.w = (O::dec(hi.h[3]) + O::dec(lo.h[3])) - cs[y][j].w;
-                } else {
-                  has_acc = e.acc32 != nullptr;
-                  if (has_acc) ac = pq[y][j];
-                }
-                if (has_acc) {
-                  v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
-                  if (e.acc_div != 1.0f) {
-                    v.x = v.x / e.acc_div; v.y = v.y / e.acc_div; v.z = v.z / e.acc_div; v.w = v.w / e.acc_div;
-                  }
-                }
-                if constexpr (FORM == G3_RES32) {
-                  if (e.out32) *reinterpret_cast<float4*>(e.out32 + orow * e.ld32 + n) = v;  // may alias add_row / acc32
-                }
-                if (e.out16) {
-                  float4 w = v;
-                  if (e.add16) {
-                    w.x += ca[y][j].x; w.y += ca[y][j].y; w.z += ca[y][j].z; w.w += ca[y][j].w;
-                  }
-                  H4 pk;
-                  pk.h[0] = O::enc(w.x); pk.h[1] = O::enc(w.y); pk.h[2] = O::enc(w.z); pk.h[3] = O::enc(w.w);
-                  *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
-                  if constexpr (FORM == G3_SPLIT) {
-                    H4 lo;
-                    lo.h[0] = O::enc_lo(w.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(w.y - O::dec(pk.h[1]));
-                    lo.h[2] = O::enc_lo(w.z - O::dec(pk.h[2])); lo.h[3] = O::enc_lo(w.w - O::dec(pk.h[3]));
-                    *reinterpret_cast<uint2*>(e.lo16 + orow * e.ld16 + n) = lo.u;
-                  }
-                }
+                if (e.add_row) pr[y][j] = *reinterpret_cast<const float4*>(e.add_row + orow * e.ld_add_row + n);
+                if (e.acc32) pq[y][j] = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
               }
             }
         }
-      if constexpr (PERSIST) {
-        if (!nxt) break;
-        // the stores this wave issued after its last waited-for load (every row's, for a full tile; a partial tile
-        // counts none: its waves may have skipped rows or columns), which the next tile's first waits do not wait for
-        const bool full = m0 + BM <= M && n0 + BN <= a.N;
-        constexpr int NG = 2 * 2 * CF::FQM * CF::FQN;  // (x, y, i, j) groups per wave
-        int s = 0;
-        if constexpr (FORM == G3_F16) {
-          s = NG * (e.split16 ? 3 : 1);
-        } else if constexpr (FORM == G3_RES32) {
-          const int nout = (e.out32 ? 1 : 0) + (e.out16 ? 1 : 0);
-          s = (e.add_row || e.acc32) ? 2 * CF::FQN * nout : NG * nout;
-        } else {
-          s = 2 * CF::FQN * 2;
-        }
-        extra = full ? s : 0;
-        g0 += nk;
-        tile += tile_step;
-        m0 = nm0;
-        n0 = nn0;
-        continue;
+#pragma unroll
+        for (int y = 0; y < 2; ++y)
+#pragma unroll
+          for (int j = 0; j < CF::FQN; ++j) {
+            const int n = n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4;
+            if (n >= a.N) continue;
+            const floatx4& c = acc[x][y][i][j];
+            float4 v = make_float4(c[0] + cb[y][j].x, c[1] + cb[y][j].y, c[2] + cb[y][j].z, c[3] + cb[y][j].w);
+            if constexpr (FORM == G3_F16) {
+              if (e.act == ACT_GELU) {  // on value pairs (packed VALU), bit for bit gelu_erf
+                const f32x2 g0 = gelu_erf2(f32x2{v.x, v.y}), g1 = gelu_erf2(f32x2{v.z, v.w});
+                v = make_float4(g0.x, g0.y, g1.x, g1.y);
+              } else if (e.act == ACT_RELU) {
+                v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+              }
+              if (n < e.scale_cols) {
+                const float cs = n < e.scale_cols2 ? e.col_scale2 : e.col_scale;
+                v.x *= cs; v.y *= cs; v.z *= cs; v.w *= cs;
+              }
+              H4 pk;
+              pk.h[0] = O::enc(v.x); pk.h[1] = O::enc(v.y); pk.h[2] = O::enc(v.z); pk.h[3] = O::enc(v.w);
+              f16* o = e.out16 + orow * e.ld16 + n;
+              *reinterpret_cast<uint2*>(o) = pk.u;
+              if (e.split16) {
+                H4 lo;
+                lo.h[0] = O::enc_lo(v.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(v.y - O::dec(pk.h[1]));
+                lo.h[2] = O::enc_lo(v.z - O::dec(pk.h[2])); lo.h[3] = O::enc_lo(v.w - O::dec(pk.h[3]));
+                *reinterpret_cast<uint2*>(o + e.split16) = lo.u;
+                *reinterpret_cast<uint2*>(o + 2 * e.split16) = pk.u;
+              }
+            } else {
+              if constexpr (FORM == G3_RES32) {
+                if (e.add_row) {
+                  const float4 ar = pr[y][j];
+                  v.x += ar.x; v.y += ar.y; v.z += ar.z; v.w += ar.w;
+                }
+              }
+              float4 ac;
+              bool has_acc = true;
+              if constexpr (FORM == G3_SPLIT) {
+                H4 hi, lo;
+                hi.u = make_uint2(__float_as_uint(pq[y][j].x), __float_as_uint(pq[y][j].y));
+                lo.u = make_uint2(__float_as_uint(pq[y][j].z), __float_as_uint(pq[y][j].w));
+                ac.x = (O::dec(hi.h[0]) + O::dec(lo.h[0])) - cs[y][j].x;
+                ac.y = (O::dec(hi.h[1]) + O::dec(lo.h[1])) - cs[y][j].y;
+                ac.z = (O::dec(hi.h[2]) + O::dec(lo.h[2])) - cs[y][j].z;
+                ac.w = (O::dec(hi.h[3]) + O::dec(lo.h[3])) - cs[y][j].w;
+              } else {
+                has_acc = e.acc32 != nullptr;
+                if (has_acc) ac = pq[y][j];
+              }
+              if (has_acc) {
+                v.x = ac.x + v.x; v.y = ac.y + v.y; v.z = ac.z + v.z; v.w = ac.w + v.w;
+                if (e.acc_div != 1.0f) {
+                  v.x = v.x / e.acc_div; v.y = v.y / e.acc_div; v.z = v.z / e.acc_div; v.w = v.w / e.acc_div;
+                }
+              }
+              if constexpr (FORM == G3_RES32) {
+                if (e.out32) *reinterpret_cast<float4*>(e.out32 + orow * e.ld32 + n) = v;  // may alias add_row / acc32
+              }
+              if (e.out16) {
+                float4 w = v;
+                if (e.add16) {
+                  w.x += ca[y][j].x; w.y += ca[y][j].y; w.z += ca[y][j].z; w.w += ca[y][j].w;
+                }
+                H4 pk;
+                pk.h[0] = O::enc(w.x); pk.h[1] = O::enc(w.y); pk.h[2] = O::enc(w.z); pk.h[3] = O::enc(w.w);
+                *reinterpret_cast<uint2*>(e.out16 + orow * e.ld16 + n) = pk.u;
+                if constexpr (FORM == G3_SPLIT) {
+                  H4 lo;
+                  lo.h[0] = O::enc_lo(w.x - O::dec(pk.h[0])); lo.h[1] = O::enc_lo(w.y - O::dec(pk.h[1]));
+                  lo.h[2] = O::enc_lo(w.z - O::dec(pk.h[2])); lo.h[3] = O::enc_lo(w.w - O::dec(pk.h[3]));
+                  *reinterpret_cast<uint2*>(e.lo16 + orow * e.ld16 + n) = lo.u;
+                }
+              }
+            }
+          }
       }
-      return;
-    }
-    break;
+    return;
   }
-  if constexpr (FORM == G3_LDS) {
-    __syncthreads();
+  __syncthreads();
 
-    // ---- epilogue: stage C through LDS in EP column passes, then the shared vector epilogue
-    // acc[x][y][i][j][r] = C[wm*WTM + x*QM + i*16 + fk*4 + r][wn*WTN + y*QN + j*16 + fr]
-    constexpr int EP = CF::EP, BNP = BN / EP, LDC = CF::LDC;
-    float* Cs = reinterpret_cast<float*>(sm3);
+  // ---- epilogue: stage C through LDS in EP column passes, then the shared vector epilogue
+  // acc[x][y][i][j][r] = C[wm*WTM + x*QM + i*16 + fk*4 + r][wn*WTN + y*QN + j*16 + fr]
+  constexpr int EP = CF::EP, BNP = BN / EP, LDC = CF::LDC;
+  float* Cs = reinterpret_cast<float*>(sm3);
 #pragma unroll
-    for (int pass = 0; pass < EP; ++pass) {
-      if (wn / (CF::WNW / EP) == pass) {
+  for (int pass = 0; pass < EP; ++pass) {
+    if (wn / (CF::WNW / EP) == pass) {
 #pragma unroll
-        for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < 2; ++x)
 #pragma unroll
-          for (int y = 0; y < 2; ++y)
+        for (int y = 0; y < 2; ++y)
 #pragma unroll
-            for (int i = 0; i < CF::FQM; ++i)
+          for (int i = 0; i < CF::FQM; ++i)
 #pragma unroll
-              for (int j = 0; j < CF::FQN; ++j)
+            for (int j = 0; j < CF::FQN; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                  Cs[(wm * CF::WTM + x * CF::QM + i * 16 + fk * 4 + r) * LDC + wn * CF::WTN - pass * BNP + y * CF::QN +
-                     j * 16 + fr] = acc[x][y][i][j][r];
-      }
-      __syncthreads();
-      epilogue_pass<BM, BNP, LDC, CF::NT, PAIR, BF>(Cs, m0, n0 + pass * BNP, M, a, e, tid);
-      __syncthreads();
+              for (int r = 0; r < 4; ++r)
+                Cs[(wm * CF::WTM + x * CF::QM + i * 16 + fk * 4 + r) * LDC + wn * CF::WTN - pass * BNP + y * CF::QN +
+                   j * 16 + fr] = acc[x][y][i][j][r];
     }
-  } else if constexpr (PERSIST) {
-    vm_wait<0>();  // (the last tile issued only dummy DMAs past its end: they land before the workgroup's LDS is released)
+    __syncthreads();
+    epilogue_pass<BM, BNP, LDC, CF::NT, PAIR, BF>(Cs, m0, n0 + pass * BNP, M, a, e, tid);
+    __syncthreads();
   }
 }
 
 // Register epilogue form of a generic epilogue (G3_LDS when it has none). tuning gemm3_direct is a mask of the forms in
 // use: 1 = G3_F16, 2 = G3_RES32, 4 = G3_SPLIT, 8 = also inside the DiffSVC sampler (run_gemm sets no_reg_epi there
-// otherwise), 16 = the persistent launch of those forms (conv_gemm3_kernel PERSIST); 0 = the LDS epilogue everywhere. Alone every form is as fast or faster (Whisper fc1 12 %,
+// otherwise); default 3, 0 = the LDS epilogue everywhere. Alone every form is as fast or faster (Whisper fc1 12 %,
 // the DiffSVC 3-tap store 12 %, skip sum 3 %); inside the 3-stream sampler the gate GEMMs beside them ran slower.
 static int direct_form3(const ConvGemmArgs& a, const EpiArgs& e) {
   const int mask = tuning().gemm3_direct;
@@ -655,44 +533,15 @@ static int launch3(const ConvGemmArgs& a0, const EpiArgs& e, const f16* zpage, h
     (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_SPLIT, BFV>}}
   const void* fns[2][2][4] = {G3_FORMS(false), G3_FORMS(true)};
 #undef G3_FORMS
-  // persistent register forms (fp16 operands; gemm3_direct bit 16): [cp64][form - 1]
-  const void* pfns[2][3] = {{(const void*)conv_gemm3_kernel<BM, BN, false, false, G3_F16, false, true>,
-                             (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_RES32, false, true>,
-                             (const void*)conv_gemm3_kernel<BM, BN, false, false, G3_SPLIT, false, true>},
-                            {(const void*)conv_gemm3_kernel<BM, BN, true, false, G3_F16, false, true>,
-                             (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_RES32, false, true>,
-                             (const void*)conv_gemm3_kernel<BM, BN, true, false, G3_SPLIT, false, true>}};
   const void* fn = fns[bf][cp64][form];
   // the register forms need only the operand ring (no C staging)
   const int lds = form == G3_LDS ? CF::LDS : CF::RING;
-  int64_t launch_grid = grid;
-  if (form != G3_LDS && !bf && (tuning().gemm3_direct & 16) && a.Kpad >= 128) {
-    // persistent: as many workgroups as are resident at once (a multiple of 8: one run of tiles per XCD slot), when
-    // there are more tiles than that
-    static int ncu_dev[16] = {};
-    int dev = 0;
-    SVC_HIP_CHECK(hipGetDevice(&dev));
-    SVC_REQUIRE(dev >= 0 && dev < 16, "conv_gemm3: device %d", dev);
-    int& ncu = ncu_dev[dev];
-    if (!ncu) SVC_HIP_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    const void* pfn = pfns[cp64][form - 1];
-    if (int st = ensure_dyn_lds(pfn, lds)) return st;
-    int occ = 0;
-    SVC_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, pfn, CF::NT, lds));
-    const int64_t slots = (int64_t)std::max(occ, 1) * ncu / 8 * 8;
-    if (slots >= 8 && grid > slots) {
-      fn = pfn;
-      launch_grid = slots;
-    }
-  }
   if (int st = ensure_dyn_lds(fn, lds)) return st;
   const double kreal = (double)(a.K / a.Cp) * a.Cvalid;
-  // (profile name of the persistent launch: conv_gemm3p<BM,BN>)
-  const std::string ptag = launch_grid != grid ? std::string("conv_gemm3p") + (tag + strlen("conv_gemm3")) : tag;
-  const int tok = prof_begin(ptag.c_str(), 2.0 * M * (double)a.N * kreal, 0.0, s);
+  const int tok = prof_begin(tag, 2.0 * M * (double)a.N * kreal, 0.0, s);
   const float inv = 1.0f / (float)a.Cp;
   void* args[] = {&a, const_cast<EpiArgs*>(&e), const_cast<const f16**>(&zpage), const_cast<float*>(&inv)};
-  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3((unsigned)launch_grid), dim3(CF::NT), args, lds, s));
+  SVC_HIP_CHECK(hipLaunchKernel(fn, dim3((unsigned)grid), dim3(CF::NT), args, lds, s));
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;

@@ -150,29 +150,6 @@ def test_headline_batch_convert(engine, cfg):
         assert torch.equal(one.wav[0], res.wav[k]), k
 
 
-@pytest.mark.timeout(600)
-def test_persistent_gemm_bit_identical(cfg, states):
-    """conv_gemm3's persistent register-epilogue launch (tune.gemm3_direct bit 16) against one workgroup per tile on
-    the production GEMMs where the grid exceeds the resident workgroups: the Whisper-medium encoder at B = 4 (qkv / fc1 /
-    out / fc2, G3_F16 with the packed GELU and the residual forms) and the vocoder at B = 8, T = 937 (every stage's c1
-    G3_F16 and c2 G3_RES32 convs, up-sampling; 256 x 256, 128 x 384, 256 x 192 and 128 x 128 tiles). Bit for bit
-    equal outputs (the same K order and epilogue arithmetic; the launch shape changes only which workgroup runs a
-    tile)."""
-    e = SVCEngine(cfg, 0, whisper_state=states["whisper"], mapper_state=states["mapper"], vocoder_state=states["vocoder"])
-    try:
-        wav16 = np.stack([ON.synth_clip_16k_quantised(20 + b, 10.0) for b in range(4)])
-        _, x = _headline_mels(cfg, [937] * 8)
-        out = {}
-        for direct in (3, 19):
-            e.tune(gemm3_direct=direct)
-            out[direct] = (e.whisper_encode(dev(wav16)).cpu(), e.bigvgan(dev(x)).cpu())
-    finally:
-        e.close()
-    for k in range(2):
-        assert torch.isfinite(out[19][k]).all()
-        assert torch.equal(out[3][k], out[19][k]), (k, float((out[3][k] - out[19][k]).abs().max()))
-
-
 def _headline_mels(cfg, frames):
     """De-normalised ln-mels [100, T_b] of synthetic clips with T_b = frames[b] (utils/mel.py on the oracle), and
     the normalised [B, max T, 100] sampler-output layout svc_bigvgan takes (rows past T_b zero)."""

@@ -14,7 +14,6 @@ pytestmark = pytest.mark.gpu
 
 from gpu_util import call, dev, ptr, rel_l2, stream  # noqa: E402
 from oracle import models as OM  # noqa: E402
-from svc_inference_pipeline_amd import _lib  # noqa: E402
 
 
 def _tm(x):  # [B, C, T] -> time-major [B*T, C]
@@ -63,44 +62,6 @@ def test_conv1d(B, T, Cin, Cout, k, stride, dil, pad, act, variant, direct, tune
     call("svc_op_conv1d", ptr(xd), B, T, Cin, ptr(wd), ptr(bd), Cout, k, stride, dil, pad, act, ptr(y), stream())
     out = y.cpu().view(B, To, Cout).permute(0, 2, 1).numpy()
     assert rel_l2(out, ref.numpy()) < 2e-3
-
-
-@pytest.mark.parametrize("B,T,Cin,Cout,k,stride,dil,pad,act", [
-    (6, 6000, 128, 1024, 1, 1, 1, 0, 1),     # Kpad 128 (two K-tiles: the next tile's DMAs start at K-tile 0), gelu
-    (4, 5001, 384, 768, 3, 1, 4, 4, 0),      # CP64, dilated taps, an M tail in the last tile
-    (6, 4001, 200, 1020, 5, 1, 3, 6, 2),     # Cin % 64 != 0 (per-lane addressing), N tail, relu
-    (16, 5001, 96, 96, 11, 1, 5, 25, 0),     # BigVGAN C = 96 (128 x 128: two workgroups per CU)
-])
-@pytest.mark.parametrize("variant", ["10", "11", "12", "13", "14", "15", "16"])
-def test_conv1d_persistent(B, T, Cin, Cout, k, stride, dil, pad, act, variant, tune):
-    """conv_gemm3's persistent register-epilogue launch (gemm3_direct bit 16: a resident grid walking runs of tiles,
-    the next tile's first K-tiles DMA'd during the current tile's last ones, its epilogue stores counted into the next
-    tile's first waits) on shapes with more tiles than resident workgroups: bit for bit the one-tile-per-workgroup
-    launch (same K order and epilogue arithmetic), and within the conv tolerance of torch."""
-    g = torch.Generator().manual_seed(1)
-    x = torch.randn(B, Cin, T, generator=g)
-    w = torch.randn(Cout, Cin, k, generator=g) / np.sqrt(Cin * k)
-    b = torch.randn(Cout, generator=g) * 0.1
-    xd, wd, bd = dev(_tm(x)), dev(w), dev(b)
-    To = (T + 2 * pad - dil * (k - 1) - 1) // stride + 1
-    out = {}
-    for direct in ("15", "31"):
-        tune(None, gemm_variant=variant, gemm3_direct=direct)
-        y = torch.full((B * To, Cout), float("nan"), device="cuda")
-        _lib.profile_enable(True)
-        try:
-            call("svc_op_conv1d", ptr(xd), B, T, Cin, ptr(wd), ptr(bd), Cout, k, stride, dil, pad, act, ptr(y),
-                 stream())
-            torch.cuda.synchronize()
-            ran = _lib.profile_read()
-        finally:
-            _lib.profile_enable(False)
-        assert any(n.startswith("conv_gemm3p") for n in ran) == (direct == "31"), ran.keys()
-        out[direct] = y.cpu()
-    assert torch.equal(out["15"], out["31"]), float((out["15"] - out["31"]).abs().max())
-    ref = F.conv1d(x, w, b, stride=stride, padding=pad, dilation=dil)
-    ref = [ref, F.gelu(ref), F.relu(ref)][act]
-    assert rel_l2(out["31"].view(B, To, Cout).permute(0, 2, 1).numpy(), ref.numpy()) < 2e-3
 
 
 @pytest.mark.parametrize("B,T,Cin,Cout,k,s", [(2, 25, 768, 384, 8, 4), (1, 40, 96, 48, 4, 2), (2, 33, 48, 24, 4, 2),
