@@ -354,6 +354,13 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
         for (int j = 0; j < CF::FQN; ++j)
           asm volatile("" : "+v"(cb[y][j].x), "+v"(cb[y][j].y), "+v"(cb[y][j].z), "+v"(cb[y][j].w));
     }
+    // RES32: add_row / acc32; SPLIT: acc16_hi / acc16_lo (host: every operand's extent < 2 GiB, 32-bit offsets)
+    const void* opa = FORM == G3_SPLIT ? (const void*)e.acc16_hi : (const void*)e.add_row;
+    const void* opb = FORM == G3_SPLIT ? (const void*)e.acc16_lo : (const void*)e.acc32;
+    const __amdgpu_buffer_rsrc_t rs_a = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(opa ? opa : (const void*)e.bias), (short)0, opa ? 0x7fffffff : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rs_b = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(opb ? opb : (const void*)e.bias), (short)0, opb ? 0x7fffffff : 0, 0x00020000);
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
@@ -366,21 +373,36 @@ __global__ __launch_bounds__(512, 1) void conv_gemm3_kernel(ConvGemmArgs a, EpiA
         // them, so the compiler cannot move a later group's loads above an earlier group's stores)
         float4 pr[2][CF::FQN], pq[2][CF::FQN];  // RES32: add_row, acc32; SPLIT: the hi / lo halves as raw bits
         if constexpr (FORM != G3_F16) {
+          // loaded through the buffer descriptors rs_a / rs_b (a missing operand's range is empty and reads 0) with no
+          // branch, then waited for here, once. Loaded under `if (e.add_row)` / `if (e.acc32)` and waited for at their
+          // uses, the compiler's wait insertion (its state merged at those joins and at each column group's per-lane
+          // branch) put a vmcnt(0) before every column group's arithmetic, each draining the stores of the column
+          // group before it (assembly, r06)
 #pragma unroll
           for (int y = 0; y < 2; ++y)
 #pragma unroll
             for (int j = 0; j < CF::FQN; ++j) {
               const int n = min(n0 + wn * CF::WTN + y * CF::QN + j * 16 + fk * 4, a.N - 4);
-              pr[y][j] = pq[y][j] = make_float4(0.f, 0.f, 0.f, 0.f);
               if constexpr (FORM == G3_SPLIT) {
-                const uint2 h = *reinterpret_cast<const uint2*>(e.acc16_hi + orow * e.ld_acc + n);
-                const uint2 l = *reinterpret_cast<const uint2*>(e.acc16_lo + orow * e.ld_acc + n);
+                const uint32_t vo = (uint32_t)((orow * e.ld_acc + n) * 2);
+                const uint2 h = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_a, vo, 0, 0));
+                const uint2 l = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(rs_b, vo, 0, 0));
                 pq[y][j] = make_float4(__uint_as_float(h.x), __uint_as_float(h.y), __uint_as_float(l.x),
                                        __uint_as_float(l.y));
+                pr[y][j] = make_float4(0.f, 0.f, 0.f, 0.f);
               } else {
-                if (e.add_row) pr[y][j] = *reinterpret_cast<const float4*>(e.add_row + orow * e.ld_add_row + n);
-                if (e.acc32) pq[y][j] = *reinterpret_cast<const float4*>(e.acc32 + orow * e.ld_acc + n);
+                pr[y][j] = __builtin_bit_cast(
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rs_a, (uint32_t)((orow * e.ld_add_row + n) * 4), 0, 0));
+                pq[y][j] = __builtin_bit_cast(
+                    float4, __builtin_amdgcn_raw_buffer_load_b128(rs_b, (uint32_t)((orow * e.ld_acc + n) * 4), 0, 0));
               }
+            }
+#pragma unroll
+          for (int y = 0; y < 2; ++y)
+#pragma unroll
+            for (int j = 0; j < CF::FQN; ++j) {
+              asm volatile("" : "+v"(pr[y][j].x), "+v"(pr[y][j].y), "+v"(pr[y][j].z), "+v"(pr[y][j].w));
+              asm volatile("" : "+v"(pq[y][j].x), "+v"(pq[y][j].y), "+v"(pq[y][j].z), "+v"(pq[y][j].w));
             }
         }
 #pragma unroll
@@ -501,6 +523,11 @@ static int direct_form3(const ConvGemmArgs& a, const EpiArgs& e) {
   const bool acc16 = e.acc16_hi || e.acc16_lo || e.acc_sub || e.lo16;
   if (e.out16 && !e.out32 && !e.add_row && !e.acc32 && !acc16 && !e.add16) return (mask & 1) ? G3_F16 : G3_LDS;
   if (e.act != ACT_NONE || e.scale_cols > 0 || e.split16) return G3_LDS;
+  // the residual forms read their row operands through buffer descriptors with 32-bit byte offsets
+  const int64_t orows = (int64_t)a.B * e.T_ostore;
+  if ((e.add_row && orows * e.ld_add_row * 4 >= (1ll << 31) - 64) ||
+      ((e.acc32 || e.acc16_hi) && orows * e.ld_acc * 4 >= (1ll << 31) - 64))
+    return G3_LDS;
   if (!acc16 && (e.out32 || e.out16)) return (mask & 2) ? G3_RES32 : G3_LDS;
   if (e.acc16_hi && e.acc16_lo && e.acc_sub && e.lo16 && e.out16 && !e.out32 && !e.add_row && !e.acc32)
     return (mask & 4) ? G3_SPLIT : G3_LDS;
