@@ -33,17 +33,25 @@ __device__ __forceinline__ void act_run(__amdgpu_buffer_rsrc_t rx, __amdgpu_buff
     t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
     return act_load<TX>(rx, xo + (uint32_t)t * xs, 0);
   };
+  // prefetched rows stay in their loaded form (f16 input: one raw word per channel pair), converted when used
+  using XR = act_raw_t<TX>;
+  auto xlr = [&](int t) __attribute__((always_inline)) {
+    t = t < 0 ? 0 : (t >= Lb ? Lb - 1 : t);
+    return act_load_raw<TX>(rx, xo + (uint32_t)t * xs, 0);
+  };
   auto s_win = [&](const f32x2* xw, int i) __attribute__((always_inline)) { return snake_up(xw, i, f2, kc); };
   const int t_end = EDGE ? min(t0 + R, Lb) : t0 + R;
-  // f32 input: the next block's rows are loaded while this block computes (106 registers; f32 launches 3 % faster,
-  // the f16 ones 2-3 % slower with it, r04u)
-  constexpr bool PF = sizeof(TX) == 4;
-  f32x2 xw[P + 10], sw[2 * P + 10], xn[PF ? P : 1];
+  // the next block's rows are loaded while this block computes (f32: 106 registers, launches 3 % faster, r04u;
+  // f16 as converted pairs was 2-3 % slower, r04u; as raw words, 98 registers = 4 waves per SIMD instead of 5, its
+  // launches are 5-8 % faster, profiles/r06_ab/r06g_act_f16_prefetch.txt)
+  constexpr bool PF = true;
+  f32x2 xw[P + 10], sw[2 * P + 10];
+  XR xn[PF ? P : 1];
 #pragma unroll
   for (int k = 0; k < 10; ++k) xw[k] = xl(t0 - 5 + k);
   if constexpr (PF) {
 #pragma unroll
-    for (int k = 0; k < P; ++k) xn[k] = xl(t0 + 5 + k);
+    for (int k = 0; k < P; ++k) xn[k] = xlr(t0 + 5 + k);
   }
 #pragma unroll
   for (int i = 0; i < 10; ++i) sw[i] = s_win(xw, i);
@@ -60,10 +68,10 @@ __device__ __forceinline__ void act_run(__amdgpu_buffer_rsrc_t rx, __amdgpu_buff
     const uint32_t xrow = xo + (uint32_t)(t + 5) * xs, yrow = yo + (uint32_t)t * ys;
     if constexpr (PF) {
 #pragma unroll
-      for (int k = 0; k < P; ++k) xw[10 + k] = xn[k];
+      for (int k = 0; k < P; ++k) xw[10 + k] = act_cvt<TX>(xn[k]);
       if (t + P < t_end) {
 #pragma unroll
-        for (int k = 0; k < P; ++k) xn[k] = EDGE ? xl(t + P + 5 + k) : act_load<TX>(rx, xrow, (P + k) * xs);
+        for (int k = 0; k < P; ++k) xn[k] = EDGE ? xlr(t + P + 5 + k) : act_load_raw<TX>(rx, xrow, (P + k) * xs);
       }
     } else {
 #pragma unroll

@@ -43,6 +43,26 @@ __device__ __forceinline__ f32x2 act_load(__amdgpu_buffer_rsrc_t r, uint32_t vo,
     return f32x2{(float)v.h[0], (float)v.h[1]};
   }
 }
+// the loaded form of a channel pair (f32: the pair; f16: one raw word) and its conversion
+template <typename TX>
+using act_raw_t = typename std::conditional<sizeof(TX) == 4, f32x2, unsigned>::type;
+template <typename TX>
+__device__ __forceinline__ act_raw_t<TX> act_load_raw(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+  if constexpr (sizeof(TX) == 4)
+    return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, vo, so, 0));
+  else
+    return __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0);
+}
+template <typename TX>
+__device__ __forceinline__ f32x2 act_cvt(act_raw_t<TX> v) {
+  if constexpr (sizeof(TX) == 4) {
+    return v;
+  } else {
+    union { unsigned u; f16 h[2]; } w;
+    w.u = v;
+    return f32x2{(float)w.h[0], (float)w.h[1]};
+  }
+}
 // s[2tb-5+i] (UpSample1d then SnakeBeta) from the window xw[k] = x[tb-5+k], exact for every index inside [0, 2L-1]:
 //   u[2q] = sum_a x[q-3+a] * 2f[11-2a],  u[2q+1] = sum_a x[q-2+a] * 2f[10-2a]   (f2 = 2f: the factor 2 is exact)
 __device__ __forceinline__ f32x2 snake_up(const f32x2* xw, int i, const float (&f2)[12], const SnakeCoef2& kc) {

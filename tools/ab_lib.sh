@@ -16,6 +16,7 @@ for r in 1 2; do
         gate) SVC_HIP_LIB=$L GEMM_BENCH_SHAPES="dilated(gate)" timeout -k 10 120 python3 tools/gemm_bench.py 24 > $O/m.txt 2>&1 || exit $? ;;
         outproj) SVC_HIP_LIB=$L GEMM_BENCH_TORCH=0 GEMM_BENCH_SHAPES="outproj(split" timeout -k 10 120 python3 tools/gemm_bench.py 15 30 > $O/m.txt 2>&1 || exit $? ;;
         amp) SVC_HIP_LIB=$L timeout -k 10 180 python3 tools/amp_bench.py > $O/m.txt 2>&1 || exit $? ;;
+        act) SVC_HIP_LIB=$L timeout -k 10 180 python3 tools/act_bench.py > $O/m.txt 2>&1 || exit $? ;;
         g3) SVC_HIP_LIB=$L GEMM_BENCH_SHAPES="outproj(split,whisper.fc,skipsum,bigvgan.s2" timeout -k 10 180 python3 tools/gemm_bench.py 15 > $O/m.txt 2>&1 || exit $? ;;
       esac
       grep -v amdgpu $O/m.txt | sed "s/^/$lib $m: /"
