@@ -433,21 +433,13 @@ __global__ __launch_bounds__(GW_NT, 1) void gate_ws_kernel(GateWsArgs a) {
       pf = af;
       end_step(k);
     };
-    // step 0: cp(0); step 1: cp(1), MFMAs of block 0. Each issues the vector-memory operations of a steady step in the
-    // same order (two cp loads, then one store: here a dropped one to GW_OOR, the cp(1) load also when nsub < 2, rows
-    // past M reading 0), so that the state the compiler's wait insertion carries into the unrolled steady loop is the
-    // steady state: with fewer operations in flight at loop entry, its merge at the loop header put a conservative
-    // vmcnt(3) / vmcnt(2) into the first unrolled copy (the cp of block k - 2 waited for the loads of step k - 1 as
-    // well), which made every third step ~350 ticks long (stamps: k % 3 == 2 at M = 29 984)
-    auto dummy_store = [&]() __attribute__((always_inline)) { buffer_store_b64(make_uint2(0u, 0u), ry, GW_OOR); };
-    auto dummy_hook = [&](int s) __attribute__((always_inline)) {
-      if (s == GW_KB - 1) dummy_store();
-    };
+    // step 0: cp(0); step 1: cp(1), MFMAs of block 0 (round 6 tried issuing a steady step's vector-memory operations here
+    // as well, a dropped store and an unconditional cp(1), so that the compiler's waits in the unrolled loop are exact:
+    // the period-3 slow step stayed and the kernel was 0.5 % slower, profiles/r06_ab/r06h_r05_vs_head.txt, r06i_gate_preamble_revert.txt)
     load_cp(0, c0);
-    dummy_store();
     end_step(0);
-    load_cp(1, c1);
-    mfma_blk(0, pg, pf, dummy_hook);
+    if (nsub >= 2) load_cp(1, c1);
+    mfma_blk(0, pg, pf, no_hook);
     end_step(1);
     int k = 2;
     for (; k + 3 <= nsub; k += 3) {  // k = 2 mod 3: loads into c2, c0, c1; epilogues from c0, c1, c2
