@@ -16,6 +16,7 @@ struct AmpConvArgs {
   const int* tv = nullptr;  // ragged batches: utterance b has min(L, tv[b] * tv_mul) rows (NULL = all L)
   int tv_mul = 1;
   const f16* x16 = nullptr;  // when set, the activation input is this f16 tensor instead of x (an AMPBlock1 intermediate)
+  bool noact = false;  // x16 is the conv's input itself, already activated (C = 96): the plain conv, no SnakeBeta
   int dbg = 0;  // (diagnostics, SVC_AMP_DBG) 1 / 2 / 4: skip the activation / conv MFMAs / epilogue; 8: register epilogue
 };
 

@@ -33,9 +33,14 @@ __host__ __device__ constexpr int amp_run_len(int C, int rows) {
   return ((rows + nr_fit - 1) / nr_fit + blk - 1) / blk * blk;
 }
 
-template <int C>
+template <int C, bool NOACT = false>
 struct AmpCfg {
-  static constexpr int BT = C <= 48 ? 256 : 128;    // output rows per workgroup (halo share of the act work)
+  // output rows per workgroup (halo share of the act work). NOACT (the C = 96 plain conv): 256-row tiles on 2 x 2 waves
+  // (each 128 rows x 48 columns), so that the weight fragments a wave reads from L1 / L2 per K-step serve 8 row
+  // fragments instead of 2 (4 waves x the whole W per 128 rows had made the 128-row form L2-bound)
+  static constexpr int BT = NOACT ? 256 : (C <= 48 ? 256 : 128);
+  static constexpr int WN = NOACT ? 2 : 1, WM = 4 / WN;  // wave grid: WM row blocks x WN column blocks
+  static constexpr int NPART = NOACT ? 4 : 2;            // epilogue staging parts (row blocks of BT / NPART)
   static constexpr int MAXP = 32;                   // max conv padding (k-1)/2*d supported
   // f16 row stride (96 / 96 / 224 B). A K-step's ds_read_b128 mixes lanes of two taps (rows tap*d apart) and CPT
   // chunks per tap, so the bank pattern depends on the stride: modelled over k in {3,7,11}, d in {1,3,5} with the
@@ -44,13 +49,15 @@ struct AmpCfg {
   static constexpr int LDA = C == 96 ? 112 : 48;
   static constexpr int ROWS = BT + 2 * MAXP;
   static constexpr int FN = (C + 15) / 16;          // 16-column fragments
-  static constexpr int A_BYTES = (ROWS + amp_run_len(C, ROWS)) * LDA * 2;  // whole runs of the largest image
+  static constexpr int FNW = FN / WN;               // per wave
+  static constexpr int A_BYTES = (NOACT ? ROWS : ROWS + amp_run_len(C, ROWS)) * LDA * 2;  // whole runs of the largest image
   // the epilogue stages the C tile in two row halves through the same LDS (the image is dead by then): C = 48 stays at
   // the image's 31-36 KiB (4 workgroups per CU), C = 24 takes at least the 14 KiB staging half
   static constexpr int LDC = C + 4;  // f32 staging row stride
-  static constexpr int STG_BYTES = BT / 2 * LDC * 4;
+  static constexpr int STG_BYTES = BT / NPART * LDC * 4;
   static constexpr int LDS = A_BYTES > STG_BYTES ? A_BYTES : STG_BYTES;
-  static_assert(C % 8 == 0 && LDA % 8 == 0, "16-B fragment rows");
+  static_assert(C % 8 == 0 && LDA % 8 == 0 && FN % WN == 0 && (BT / 16) % WM == 0, "16-B fragment rows, wave grid");
+  static_assert(BT / WM <= BT / NPART || (BT / WM) % (BT / NPART) == 0, "a wave's rows: within one part or whole parts");
 };
 
 // SnakeBeta of the channel pair (c, c+1) for global rows [rs, re) into the LDS image (row r of the image = global row
@@ -122,9 +129,12 @@ __device__ __forceinline__ void amp_act_pair(__amdgpu_buffer_rsrc_t rx, uint32_t
 // occupancy target it split the file into VGPRs + AGPRs at 5 waves). The activation runs on channel pairs with packed
 // f32 ops in 4-row blocks for every C (round 4: C = 96 had a single-channel 8-row form, removed with the packed
 // clamp-free form).
-template <int C, bool X16 = false>
-__global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
-  using CF = AmpCfg<C>;
+// NOACT: the plain conv of an input already activated (activation1d's f16 output, p.x16): phase 1 copies the rows into
+// the image (16-B loads, zeros outside [0, Lb)) and the conv reads every tap from it, so each input row leaves HBM / L2
+// once per workgroup instead of once per tap as in conv_gemm3's implicit GEMM.
+template <int C, bool X16 = false, bool NOACT = false>
+__global__ __launch_bounds__(AMP_NT, NOACT ? 2 : 4) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
+  using CF = AmpCfg<C, NOACT>;
   extern __shared__ __align__(16) unsigned char amp_sm[];
   f16* As = reinterpret_cast<f16*>(amp_sm);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -139,7 +149,28 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
   const int rows = CF::BT + 2 * P;
 
   // ------------------------------------------------------------------ 1. SnakeBeta -> LDS (f16)
-  if (!(p.dbg & 1)) {
+  if constexpr (NOACT) {
+    if (!(p.dbg & 1)) {
+      constexpr int CH = C / 8;                                      // 16-B chunks per row
+      constexpr int IT = ((CF::BT + 2 * CF::MAXP) * CH + AMP_NT - 1) / AMP_NT;  // chunks per thread, largest image
+      const int r0 = t0 - P, n = rows * CH;
+      const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<f16*>(p.x16 + (int64_t)b * L * C), (short)0, Lb * C * 2, 0x00020000);
+      uint4 v[IT];
+      // rows outside [0, Lb) lie outside the descriptor's range (a negative row wraps past it): they load as zeros
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * AMP_NT, r = idx / CH, q = idx - r * CH;
+        const uint32_t vo = (idx < n && r0 + r >= 0) ? (uint32_t)(((r0 + r) * C + q * 8) * 2) : 0x80000000u;
+        v[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, 0, 0));
+      }
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * AMP_NT, r = idx / CH, q = idx - r * CH;
+        if (idx < n) *reinterpret_cast<uint4*>(As + r * CF::LDA + q * 8) = v[it];
+      }
+    }
+  } else if (!(p.dbg & 1)) {
     constexpr int BLK = 4;
     using TX = typename std::conditional<X16, f16, float>::type;
     float f[12], f2[12];  // f2: the up-sampling taps with its factor 2 (exact)
@@ -171,40 +202,42 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
   __syncthreads();
 
   // ------------------------------------------------------------------ 2. conv on the matrix pipe
-  constexpr int MW = CF::BT / 16 / 4;  // 16-row fragments per wave
-  constexpr int CPT = C / 8;           // 8-wide k chunks per tap
-  floatx4 acc[MW][CF::FN];
+  constexpr int MW = CF::BT / 16 / CF::WM;  // 16-row fragments per wave
+  constexpr int FNW = CF::FNW;              // 16-column fragments per wave
+  constexpr int CPT = C / 8;                // 8-wide k chunks per tap
+  const int wm = wave / CF::WN, wn = wave - wm * CF::WN;
+  floatx4 acc[MW][FNW];
 #pragma unroll
   for (int i = 0; i < MW; ++i)
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < FNW; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   const int ks = (p.k * C + 31) / 32;
   const int fr = lane & 15, fk = lane >> 4;
-  const f16* wrow = p.W + (int64_t)fr * p.Kpad + fk * 8;
-  half8 bn[CF::FN];  // weight fragments of the next k-step, loaded one step ahead (L2 latency off the MFMA path)
+  const f16* wrow = p.W + (int64_t)(wn * FNW * 16 + fr) * p.Kpad + fk * 8;
+  half8 bn[FNW];  // weight fragments of the next k-step, loaded one step ahead (L2 latency off the MFMA path)
 #pragma unroll
-  for (int j = 0; j < CF::FN; ++j) bn[j] = *reinterpret_cast<const half8*>(wrow + (int64_t)j * 16 * p.Kpad);
+  for (int j = 0; j < FNW; ++j) bn[j] = *reinterpret_cast<const half8*>(wrow + (int64_t)j * 16 * p.Kpad);
   for (int s = 0; s < ((p.dbg & 2) ? 0 : ks); ++s) {
     const int q = 4 * s + fk;
     int tap = q / CPT, cc = q - tap * CPT;
     if (tap >= p.k) tap = cc = 0;  // K tail: zero weights, any finite A
-    half8 af[MW], bf[CF::FN];
+    half8 af[MW], bf[FNW];
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j) bf[j] = bn[j];
+    for (int j = 0; j < FNW; ++j) bf[j] = bn[j];
     if (s + 1 < ks) {
 #pragma unroll
-      for (int j = 0; j < CF::FN; ++j)
+      for (int j = 0; j < FNW; ++j)
         bn[j] = *reinterpret_cast<const half8*>(wrow + (int64_t)j * 16 * p.Kpad + (s + 1) * 32);
     }
 #pragma unroll
     for (int i = 0; i < MW; ++i) {
-      const int r = (wave * MW + i) * 16 + fr + tap * p.d;
+      const int r = (wm * MW + i) * 16 + fr + tap * p.d;
       af[i] = *reinterpret_cast<const half8*>(As + r * CF::LDA + cc * 8);
     }
 #pragma unroll
     for (int i = 0; i < MW; ++i)
 #pragma unroll
-      for (int j = 0; j < CF::FN; ++j)  // C^T fragment: acc[i][j][r] = C[row fr of block i][channel j*16 + fk*4 + r]
+      for (int j = 0; j < FNW; ++j)  // C^T fragment: acc[i][j][r] = C[row fr of block i][channel j*16 + fk*4 + r]
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
   }
   // ------------------------------------------------------------------ 3. epilogue: each lane owns 4 consecutive
@@ -235,7 +268,7 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
   };
   if (!(p.dbg & 8)) {
     float* stg = reinterpret_cast<float*>(amp_sm);
-    constexpr int HB = CF::BT / 2, C4 = C / 4;
+    constexpr int HB = CF::BT / CF::NPART, C4 = C / 4;
     // A half's epilogue operands (add_row / acc32 rows) are loaded for all of the thread's chunks at once, through
     // buffer descriptors over this workgroup's block (a missing operand or a row past nvalid reads 0: no per-lane or
     // per-operand branch), and waited for once. Loaded chunk by chunk inside the loop, each chunk's load waited for every
@@ -268,7 +301,8 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
     };
     const bool has_ops = e.add_row || e.acc32;  // (the c1 convs have none: no loads at all)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < CF::NPART; ++h) {
+      if (h * HB >= nvalid) break;  // (block-uniform)
       float4 ar[IT], ac[IT];
 #pragma unroll
       for (int it = 0; it < IT; ++it) ar[it] = ac[it] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -285,19 +319,19 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
           asm volatile("" : "+v"(ac[it].x), "+v"(ac[it].y), "+v"(ac[it].z), "+v"(ac[it].w));
         }
       }
-      __syncthreads();  // h = 0: the k-loop's image reads are done; h = 1: the first half has been consumed
-      if ((wave >> 1) == h) {
+      __syncthreads();  // h = 0: the k-loop's image reads are done; h > 0: the previous part has been consumed
 #pragma unroll
-        for (int j = 0; j < CF::FN; ++j) {
-          const int c0 = j * 16 + fk * 4;
-          if (c0 >= C) continue;
-          const float4 bi = *reinterpret_cast<const float4*>(p.bias + c0);
+      for (int j = 0; j < FNW; ++j) {
+        const int c0 = (wn * FNW + j) * 16 + fk * 4;
+        if (c0 >= C) continue;
+        const float4 bi = *reinterpret_cast<const float4*>(p.bias + c0);
 #pragma unroll
-          for (int i = 0; i < MW; ++i) {
-            const int r = ((wave & 1) * MW + i) * 16 + fr;
-            *reinterpret_cast<float4*>(stg + r * CF::LDC + c0) =
-                make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w);
-          }
+        for (int i = 0; i < MW; ++i) {
+          const int rt = (wm * MW + i) * 16;  // the fragment's first tile row (wave-uniform)
+          if (rt / HB != h) continue;
+          const int r = rt - h * HB + fr;
+          *reinterpret_cast<float4*>(stg + r * CF::LDC + c0) =
+              make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w);
         }
       }
       __syncthreads();
@@ -320,13 +354,13 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < CF::FN; ++j) {
-      const int c0 = j * 16 + fk * 4;
+    for (int j = 0; j < FNW; ++j) {
+      const int c0 = (wn * FNW + j) * 16 + fk * 4;
       if (c0 >= C) continue;
       const float4 bi = *reinterpret_cast<const float4*>(p.bias + c0);
 #pragma unroll
       for (int i = 0; i < MW; ++i) {
-        const int row = (wave * MW + i) * 16 + fr;
+        const int row = (wm * MW + i) * 16 + fr;
         if (row >= nvalid) continue;
         epi(make_float4(acc[i][j][0] + bi.x, acc[i][j][1] + bi.y, acc[i][j][2] + bi.z, acc[i][j][3] + bi.w),
             base + (int64_t)row * C + c0);
@@ -335,27 +369,28 @@ __global__ __launch_bounds__(AMP_NT, 4) void amp_conv_kernel(AmpConvArgs p, EpiA
   }
 }
 
-template <int C, bool X16>
+template <int C, bool X16, bool NOACT = false>
 static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
-  using CF = AmpCfg<C>;
-  if (int st = ensure_dyn_lds((const void*)amp_conv_kernel<C, X16>, CF::LDS)) return st;
+  using CF = AmpCfg<C, NOACT>;
+  if (int st = ensure_dyn_lds((const void*)amp_conv_kernel<C, X16, NOACT>, CF::LDS)) return st;
   const int64_t grid = (int64_t)p.B * cdiv(p.L, CF::BT);
   SVC_REQUIRE(grid > 0 && grid < (1ll << 31), "amp_conv: bad grid");
   const double elems = (double)p.B * p.L * C;
   // algorithmic bytes: x in (f32 or f16), output out (f32 and/or f16), epilogue operands in (f32)
   const double bytes =
       elems * ((X16 ? 2.0 : 4.0) + (e.out32 ? 4 : 0) + (e.out16 ? 2 : 0) + (e.add_row ? 4 : 0) + (e.acc32 ? 4 : 0));
-  const char* tag = C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>");
+  const char* tag = NOACT ? "amp_conv<96,conv>" : (C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>"));
   const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
   // the activation image needs BT + 2P rows, not BT + 2 MAXP: sized per launch, C = 48 fits 5 workgroups per CU
   // (instead of 4) for every conv with P <= 15
   const int P = (p.k - 1) / 2 * p.d;
   const int rows = CF::BT + 2 * P, run = amp_run_len(C, rows);
-  const int lds = std::max((rows + run - 1) / run * run * CF::LDA * 2, CF::STG_BYTES);
+  const int img_rows = NOACT ? rows : (rows + run - 1) / run * run;
+  const int lds = std::max(img_rows * CF::LDA * 2, CF::STG_BYTES);
   static const int dbg = getenv("SVC_AMP_DBG") ? atoi(getenv("SVC_AMP_DBG")) : 0;
   AmpConvArgs pa = p;
   pa.dbg = dbg;
-  hipLaunchKernelGGL((amp_conv_kernel<C, X16>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, pa, e);
+  hipLaunchKernelGGL((amp_conv_kernel<C, X16, NOACT>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, pa, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
@@ -367,7 +402,8 @@ bool amp_conv_supported(int C, int k, int d) {
 
 // act + conv + epilogue; e uses out32 / out16 / add_row / acc32 with leading dimension C (contiguous rows)
 int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
-  SVC_REQUIRE(amp_conv_supported(C, p.k, p.d), "amp_conv: C=%d k=%d d=%d unsupported", C, p.k, p.d);
+  SVC_REQUIRE(amp_conv_supported(C, p.k, p.d) && (!p.noact || (C == 96 && p.x16)),
+              "amp_conv: C=%d k=%d d=%d noact=%d unsupported", C, p.k, p.d, (int)p.noact);
   SVC_REQUIRE(p.L >= 1 && p.Kpad >= p.k * C && p.Kpad % 32 == 0, "amp_conv: L=%d Kpad=%d", p.L, p.Kpad);
   SVC_REQUIRE((!e.out32 || e.ld32 == C) && (!e.out16 || e.ld16 == C) && (!e.add_row || e.ld_add_row == C) &&
                   (!e.acc32 || e.ld_acc == C) && !e.add16 && e.act == ACT_NONE && e.kind == EPI_GENERIC,
@@ -398,6 +434,8 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
       st = q.x16 ? launch_amp<24, true>(q, f, s) : launch_amp<24, false>(q, f, s);
     else if (C == 48)
       st = q.x16 ? launch_amp<48, true>(q, f, s) : launch_amp<48, false>(q, f, s);
+    else if (q.noact)
+      st = launch_amp<96, true, true>(q, f, s);
     else
       st = q.x16 ? launch_amp<96, true>(q, f, s) : launch_amp<96, false>(q, f, s);
     if (st) return st;

@@ -353,6 +353,22 @@ def test_bigvgan_variants(cfg, states, golden, variant, tune):
         e.close()
 
 
+def test_bigvgan_plain_conv_c96(engine, tune):
+    """The C = 96 AMPBlock convs (modules/bigvgan.py:424-433) on amp_conv's plain-conv form (tune.amp_conv_maxc = 96:
+    activation1d's f16 output staged once into an LDS row image, every tap read from it) against conv_gemm3's implicit
+    GEMM (amp_conv_maxc = 0), for equal and ragged lengths. Both run one 32-deep MFMA chain per accumulator over the same
+    packed K order and the same epilogue arithmetic, so the waveforms are identical."""
+    rng = np.random.default_rng(7)
+    x = dev(rng.uniform(-1, 1, (3, 37, 100)).astype(np.float32))
+    outs = {}
+    for maxc in ("0", "96"):
+        tune(engine, amp_conv_maxc=maxc)
+        outs[maxc] = (engine.bigvgan(x).cpu().numpy(), engine.bigvgan(x, frames=[37, 21, 30]).cpu().numpy())
+    for i in range(2):
+        a, b = outs["0"][i], outs["96"][i]
+        assert np.array_equal(a, b), (i, float(np.abs(a - b).max()), float(np.abs(a).max()))
+
+
 def test_vocoder_sub_streams_bit_identical(engine, tune):
     """BigVGAN with utterance-aligned sub-batches on 1, 2 or 3 streams: identical waveforms."""
     rng = np.random.default_rng(1)
