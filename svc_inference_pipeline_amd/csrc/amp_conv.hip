@@ -35,12 +35,15 @@ __host__ __device__ constexpr int amp_run_len(int C, int rows) {
 
 template <int C, bool NOACT = false>
 struct AmpCfg {
-  // output rows per workgroup (halo share of the act work). NOACT (the C = 96 plain conv): 256-row tiles on 2 x 2 waves
+  // 256 output rows per workgroup (halo share of the act work). C = 96 (fused, and NOACT, the plain conv) on 2 x 2 waves
   // (each 128 rows x 48 columns), so that the weight fragments a wave reads from L1 / L2 per K-step serve 8 row
-  // fragments instead of 2 (4 waves x the whole W per 128 rows had made the 128-row form L2-bound)
-  static constexpr int BT = NOACT ? 256 : (C <= 48 ? 256 : 128);
-  static constexpr int WN = NOACT ? 2 : 1, WM = 4 / WN;  // wave grid: WM row blocks x WN column blocks
-  static constexpr int NPART = NOACT ? 4 : 2;            // epilogue staging parts (row blocks of BT / NPART)
+  // fragments: the round-5 128-row tiles on 4 x 1 waves (every wave reading all of W per k-loop, 2 row fragments each)
+  // were L2-bound, 11.5 against 8.3 ms per step for the C = 96 convs (profiles/r06_ab/r06v_*, r06w_*)
+  static constexpr bool WIDE = NOACT || C == 96;
+  static constexpr int BT = 256;
+  static constexpr int WN = WIDE ? 2 : 1, WM = 4 / WN;  // wave grid: WM row blocks x WN column blocks
+  static constexpr int NPART = WIDE ? 4 : 2;            // epilogue staging parts (row blocks of BT / NPART)
+  static constexpr int OCC = WIDE ? 2 : 4;              // workgroups per CU (launch bound)
   static constexpr int MAXP = 32;                   // max conv padding (k-1)/2*d supported
   // f16 row stride (96 / 96 / 224 B). A K-step's ds_read_b128 mixes lanes of two taps (rows tap*d apart) and CPT
   // chunks per tap, so the bank pattern depends on the stride: modelled over k in {3,7,11}, d in {1,3,5} with the
@@ -133,7 +136,7 @@ __device__ __forceinline__ void amp_act_pair(__amdgpu_buffer_rsrc_t rx, uint32_t
 // the image (16-B loads, zeros outside [0, Lb)) and the conv reads every tap from it, so each input row leaves HBM / L2
 // once per workgroup instead of once per tap as in conv_gemm3's implicit GEMM.
 template <int C, bool X16 = false, bool NOACT = false>
-__global__ __launch_bounds__(AMP_NT, NOACT ? 2 : 4) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
+__global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
   using CF = AmpCfg<C, NOACT>;
   extern __shared__ __align__(16) unsigned char amp_sm[];
   f16* As = reinterpret_cast<f16*>(amp_sm);

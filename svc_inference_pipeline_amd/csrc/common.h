@@ -359,10 +359,13 @@ struct Tuning {
   int sampler_streams = 1;  // DiffSVC sampler sub-batch streams (round 4: 1 with gate_ws; 2 was the conv_gemm4 default)
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
   int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip)
-  int amp_maxc = 48;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none)
+  int amp_maxc = 96;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none). C = 96 on
+                            // the 256-row 2 x 2-wave tiles: BigVGAN -1.0 ms per step against activation1d + the plain
+                            // conv (profiles/r06_ab/r06x_amp_fused_c96.txt)
   int amp_conv_maxc = 96;   // widest unfused BigVGAN conv (activation1d first) run by amp_conv's plain-conv form (the
-                            // LDS-resident row image, every tap read from it) instead of conv_gemm3 (0: none). C = 96:
-                            // 11.5 -> 8.3 ms per step, +0.8 % end to end (profiles/r06_ab/r06w_amp_plain_conv_c96.txt)
+                            // LDS-resident row image, every tap read from it) instead of conv_gemm3 (0: none). C = 96
+                            // with amp_maxc 48: 11.5 -> 8.3 ms per step, +0.8 % end to end
+                            // (profiles/r06_ab/r06w_amp_plain_conv_c96.txt); the unfused path of AMPBlock2 generators
   int res_proj = 1;         // DiffSVC residual and input projections on the weight-stationary streams (res_proj.hip
                             // res_proj / mel_proj; 0: conv_gemm3;
                             // > 1: that many row lanes of 2 workgroups instead of 1/2 (one sampler stream) or 3/8

@@ -2599,9 +2599,10 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
   WS_GET(float, XS, big);
   WS_GET(f16, a16, big);
   WS_GET(f16, next16, big);
-  // amp_maxc: widest channel count that takes the fused kernel (0: activation1d + GEMM everywhere). C = 96 measured 1.2 % faster end to end as
-  // activation1d + conv_gemm3 (736 vs 727 audio-s/s, same box); C = 48 unfused is 9 % slower (its N = 48 GEMMs are too
-  // narrow for the MFMA tiles)
+  // amp_maxc: widest channel count that takes the fused kernel (0: activation1d + GEMM everywhere). C = 48 unfused is
+  // 9 % slower (its N = 48 GEMMs are too narrow for the MFMA tiles); C = 96 fused is 1.0 ms per step faster than
+  // activation1d + amp_conv's plain conv since both run on 256-row tiles of 2 x 2 waves (round 6; on the round-5 128-row
+  // tiles, where every wave read all of W per k-loop, fused C = 96 had been 1 % slower end to end)
   const int amp_maxc = tuning().amp_maxc;
   const int ns = (int)c->vstages.size();
 

@@ -114,7 +114,7 @@ def test_activation1d(B, L, C, x16):
                                      (3, 257, 11, 1), (2, 600, 3, 5)])
 def test_amp_conv(B, L, k, d, C):
     """Fused SnakeBeta Activation1d -> dilated conv -> bias + residual (BigVGAN C <= 96 stages; C <= 48 run the
-    packed channel-pair activation, C = 96 the single-channel one)."""
+    packed channel-pair activation; C = 96 on 256-row tiles of 2 x 2 waves)."""
     from svc_inference_pipeline_amd import weights as W
     g = torch.Generator().manual_seed(5)
     x = torch.randn(B, C, L, generator=g) * 2

@@ -327,8 +327,8 @@ def test_bigvgan(engine, cfg, states, golden, direct, tune):
 @pytest.mark.parametrize("variant", list(W.VOCODER_VARIANTS))
 def test_bigvgan_variants(cfg, states, golden, variant, tune):
     """F4: AMPBlock2 / Snake (log and linear scale) generators against the oracle, which
-    tests/test_oracle_golden.py::test_bigvgan_variants pins to the reference's own Generator. Both the fused
-    small-channel path (amp_conv, C <= 48) and the unfused activation1d + GEMM path (amp_maxc = 0) are checked,
+    tests/test_oracle_golden.py::test_bigvgan_variants pins to the reference's own Generator. The fused
+    small-channel path (amp_conv, C <= 48 or C <= 96) and the unfused activation1d + GEMM path (amp_maxc = 0) are checked,
     with test_bigvgan's tolerance (1.5 x the fp16-operand emulation's distance + 1e-3)."""
     import copy
     g = golden("bigvgan_variants")
@@ -345,7 +345,7 @@ def test_bigvgan_variants(cfg, states, golden, variant, tune):
     budget = 1.5 * rel_l2(OF.synthesis_fade(emu[0, 0], T).numpy(), ref) + 1e-3
     e = SVCEngine(c2, 0, mapper_state=states["mapper"], vocoder_state=vsd)
     try:
-        for maxc in ("48", "0"):
+        for maxc in ("48", "96", "0"):
             tune(e, amp_maxc=maxc)
             wav = e.bigvgan(dev(x_norm.T[None].astype(np.float32)))[0].cpu().numpy()
             assert rel_l2(wav, ref) < budget, (maxc, rel_l2(wav, ref), budget)
@@ -362,7 +362,7 @@ def test_bigvgan_plain_conv_c96(engine, tune):
     x = dev(rng.uniform(-1, 1, (3, 37, 100)).astype(np.float32))
     outs = {}
     for maxc in ("0", "96"):
-        tune(engine, amp_conv_maxc=maxc)
+        tune(engine, amp_maxc="48", amp_conv_maxc=maxc)  # C = 96 unfused (activation1d first)
         outs[maxc] = (engine.bigvgan(x).cpu().numpy(), engine.bigvgan(x, frames=[37, 21, 30]).cpu().numpy())
     for i in range(2):
         a, b = outs["0"][i], outs["96"][i]
