@@ -11,7 +11,7 @@
 //   2. conv: v_mfma_f32_16x16x32_f16 with A fragments read from the LDS image at row r + tap*d (row stride
 //      padded so 16-row fragment reads are conflict-free) and B = the packed weights [Npad][Kpad] (L1/L2).
 //   3. epilogue: bias, residual add (add_row), resblock mean accumulation (acc32 / acc_div), f32 and/or f16 stores
-//      as 16-B / 8-B vectors over whole contiguous rows (the C tile staged through the dead image's LDS in halves).
+//      as 16-B / 8-B vectors over whole contiguous rows (the C tile staged through the dead image's LDS in row blocks).
 // The activation never round-trips through HBM, and every HBM access is a coalesced 16-byte stream.
 #include <type_traits>
 
@@ -39,11 +39,13 @@ struct AmpCfg {
   // (each 128 rows x 48 columns), so that the weight fragments a wave reads from L1 / L2 per K-step serve 8 row
   // fragments: the round-5 128-row tiles on 4 x 1 waves (every wave reading all of W per k-loop, 2 row fragments each)
   // were L2-bound, 11.5 against 8.3 ms per step for the C = 96 convs (profiles/r06_ab/r06v_*, r06w_*)
+  // C = 24 / 48: 512-row tiles on 4 x 1 waves (128 rows each, the same weight reuse), 2 workgroups per CU: against the
+  // round-5 256-row tiles at 4 per CU, 16.95 -> 16.0 ms per step (profiles/r06_ab/r06y_amp_narrow_512rows.txt)
   static constexpr bool WIDE = NOACT || C == 96;
-  static constexpr int BT = 256;
+  static constexpr int BT = WIDE ? 256 : 512;
   static constexpr int WN = WIDE ? 2 : 1, WM = 4 / WN;  // wave grid: WM row blocks x WN column blocks
-  static constexpr int NPART = WIDE ? 4 : 2;            // epilogue staging parts (row blocks of BT / NPART)
-  static constexpr int OCC = WIDE ? 2 : 4;              // workgroups per CU (launch bound)
+  static constexpr int NPART = 4;                       // epilogue staging parts (row blocks of BT / NPART)
+  static constexpr int OCC = 2;                         // workgroups per CU (launch bound)
   static constexpr int MAXP = 32;                   // max conv padding (k-1)/2*d supported
   // f16 row stride (96 / 96 / 224 B). A K-step's ds_read_b128 mixes lanes of two taps (rows tap*d apart) and CPT
   // chunks per tap, so the bank pattern depends on the stride: modelled over k in {3,7,11}, d in {1,3,5} with the
@@ -54,8 +56,7 @@ struct AmpCfg {
   static constexpr int FN = (C + 15) / 16;          // 16-column fragments
   static constexpr int FNW = FN / WN;               // per wave
   static constexpr int A_BYTES = (NOACT ? ROWS : ROWS + amp_run_len(C, ROWS)) * LDA * 2;  // whole runs of the largest image
-  // the epilogue stages the C tile in two row halves through the same LDS (the image is dead by then): C = 48 stays at
-  // the image's 31-36 KiB (4 workgroups per CU), C = 24 takes at least the 14 KiB staging half
+  // the epilogue stages the C tile in NPART row blocks through the same LDS (the image is dead by then)
   static constexpr int LDC = C + 4;  // f32 staging row stride
   static constexpr int STG_BYTES = BT / NPART * LDC * 4;
   static constexpr int LDS = A_BYTES > STG_BYTES ? A_BYTES : STG_BYTES;
@@ -128,8 +129,8 @@ __device__ __forceinline__ void amp_act_pair(__amdgpu_buffer_rsrc_t rx, uint32_t
   }
 }
 
-// Launch bound: 4 waves per SIMD, under which the compiler keeps the accumulators in the unified VGPR file (without an
-// occupancy target it split the file into VGPRs + AGPRs at 5 waves). The activation runs on channel pairs with packed
+// Launch bound: AmpCfg::OCC workgroups (waves per SIMD), under which the compiler keeps the accumulators in the unified
+// VGPR file (round 5, 4 per CU: without an occupancy target it split the file into VGPRs + AGPRs at 5 waves). The activation runs on channel pairs with packed
 // f32 ops in 4-row blocks for every C (round 4: C = 96 had a single-channel 8-row form, removed with the packed
 // clamp-free form).
 // NOACT: the plain conv of an input already activated (activation1d's f16 output, p.x16): phase 1 copies the rows into
@@ -245,7 +246,7 @@ __global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kern
   }
   // ------------------------------------------------------------------ 3. epilogue: each lane owns 4 consecutive
   // channels of one row (operand-swapped MFMAs). The workgroup's output block is [BT][C] contiguous in every tensor, so
-  // the C tile goes through LDS in two row halves (the activation image is dead after the k-loop) and the epilogue
+  // the C tile goes through LDS in NPART row blocks (the activation image is dead after the k-loop) and the epilogue
   // operands and outputs move as whole contiguous rows: a wave's 16-B accesses cover 1 KiB in a row instead of 16
   // pieces of 64 B at the row stride (SVC_AMP_DBG 4: no epilogue; 8: that register epilogue instead).
   const int nvalid = (p.dbg & 4) ? 0 : min(CF::BT, Lb - t0);

@@ -1,11 +1,11 @@
 # Alternating end-to-end A/B of environment settings with the bench line's per-kernel split (run from the repo root via
 # gpurun). SETTINGS: space-separated "VAR=val,VAR=val" ("-" = defaults); ROUNDS: rounds; KPAT: regex of the `kernels`
-# entries to print; TESTK: optional GPU tests (-k expression) first. Exit codes 0 / 1 of the tests (pass / assertion
+# entries to print; TESTK: optional GPU tests (-k expression) first, under TESTENV ("VAR=val ..."). Exit codes 0 / 1 of the tests (pass / assertion
 # failures) go on to the benches; anything else (a fault, an abort, a time limit) stops the script.
 set -o pipefail
 O=gpurun_out/${TAG:-ab_kern}; mkdir -p $O
 if [ -n "${TESTK:-}" ]; then
-  timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -k "$TESTK" > $O/tests.log 2>&1
+  env ${TESTENV:-} timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread -k "$TESTK" > $O/tests.log 2>&1
   rc=$?; tail -3 $O/tests.log
   [ $rc -eq 1 ] && grep -E "^E |assert" $O/tests.log | head -20
   [ $rc -gt 1 ] && exit $rc
