@@ -27,9 +27,9 @@ constexpr int AMP_NT = 256;
 // (channel group, run) task to its own thread (one exposed load latency per thread). The image is allocated for
 // whole runs (nruns * RUN rows), so that no run is partial: a partial run would take the edge form of the channel-pair
 // activation, and its lanes would make their whole wave run both forms before the barrier.
-__host__ __device__ constexpr int amp_run_len(int C, int rows) {
+__host__ __device__ constexpr int amp_run_len(int C, int rows, int nt = AMP_NT) {
   const int blk = 4, ngrp = C / 2;
-  const int nr_fit = AMP_NT / ngrp > 1 ? AMP_NT / ngrp : 1;
+  const int nr_fit = nt / ngrp > 1 ? nt / ngrp : 1;
   return ((rows + nr_fit - 1) / nr_fit + blk - 1) / blk * blk;
 }
 
@@ -41,21 +41,27 @@ struct AmpCfg {
   // were L2-bound, 11.5 against 8.3 ms per step for the C = 96 convs (profiles/r06_ab/r06v_*, r06w_*)
   // C = 24 / 48: 512-row tiles on 4 x 1 waves (128 rows each, the same weight reuse), 2 workgroups per CU: against the
   // round-5 256-row tiles at 4 per CU, 16.95 -> 16.0 ms per step (profiles/r06_ab/r06y_amp_narrow_512rows.txt)
-  static constexpr bool WIDE = NOACT || C == 96;
-  static constexpr int BT = WIDE ? 256 : 512;
-  static constexpr int WN = WIDE ? 2 : 1, WM = 4 / WN;  // wave grid: WM row blocks x WN column blocks
+  // C = 192: 8 waves on 2 x 4 (each 128 rows x 48 columns), one workgroup per CU (the image is 127-133 KiB).
+  static constexpr bool WIDE = NOACT || C >= 96;
+  static constexpr int NT = C == 192 ? 512 : AMP_NT;    // threads
+#ifndef AMP_BT192
+#define AMP_BT192 256
+#endif
+  static constexpr int BT = C == 192 ? AMP_BT192 : (WIDE ? 256 : 512);
+  static constexpr int WN = C == 192 ? 4 : (WIDE ? 2 : 1), WM = NT / 64 / WN;  // wave grid: WM row x WN column blocks
   static constexpr int NPART = 4;                       // epilogue staging parts (row blocks of BT / NPART)
-  static constexpr int OCC = 2;                         // workgroups per CU (launch bound)
+  static constexpr int OCC = (C == 192 && BT == 256) ? 1 : 2;  // workgroups per CU (launch bound)
   static constexpr int MAXP = 32;                   // max conv padding (k-1)/2*d supported
   // f16 row stride (96 / 96 / 224 B). A K-step's ds_read_b128 mixes lanes of two taps (rows tap*d apart) and CPT
   // chunks per tap, so the bank pattern depends on the stride: modelled over k in {3,7,11}, d in {1,3,5} with the
   // guide's 4 x 16 lane groups, the round-4 strides 24 / 56 / 104 cost 1.94 / 1.94 / 2.0 LDS cycles per ideal one,
   // these 1.44 / 1.06 / 1.0 (r05 search; C = 24 takes 48 halves, twice its row: the image stays within 4 WGs per CU)
-  static constexpr int LDA = C == 96 ? 112 : 48;
+  // (C = 192: 26 chunks, the stride class of C = 96's 14: 8 consecutive rows on distinct bank slots)
+  static constexpr int LDA = C == 192 ? 208 : (C == 96 ? 112 : 48);
   static constexpr int ROWS = BT + 2 * MAXP;
   static constexpr int FN = (C + 15) / 16;          // 16-column fragments
   static constexpr int FNW = FN / WN;               // per wave
-  static constexpr int A_BYTES = (NOACT ? ROWS : ROWS + amp_run_len(C, ROWS)) * LDA * 2;  // whole runs of the largest image
+  static constexpr int A_BYTES = (NOACT ? ROWS : ROWS + amp_run_len(C, ROWS, NT)) * LDA * 2;  // whole runs of the largest image
   // the epilogue stages the C tile in NPART row blocks through the same LDS (the image is dead by then)
   static constexpr int LDC = C + 4;  // f32 staging row stride
   static constexpr int STG_BYTES = BT / NPART * LDC * 4;
@@ -137,7 +143,7 @@ __device__ __forceinline__ void amp_act_pair(__amdgpu_buffer_rsrc_t rx, uint32_t
 // the image (16-B loads, zeros outside [0, Lb)) and the conv reads every tap from it, so each input row leaves HBM / L2
 // once per workgroup instead of once per tap as in conv_gemm3's implicit GEMM.
 template <int C, bool X16 = false, bool NOACT = false>
-__global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
+__global__ __launch_bounds__((AmpCfg<C, NOACT>::NT), (AmpCfg<C, NOACT>::OCC)) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
   using CF = AmpCfg<C, NOACT>;
   extern __shared__ __align__(16) unsigned char amp_sm[];
   f16* As = reinterpret_cast<f16*>(amp_sm);
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kern
   if constexpr (NOACT) {
     if (!(p.dbg & 1)) {
       constexpr int CH = C / 8;                                      // 16-B chunks per row
-      constexpr int IT = ((CF::BT + 2 * CF::MAXP) * CH + AMP_NT - 1) / AMP_NT;  // chunks per thread, largest image
+      constexpr int IT = ((CF::BT + 2 * CF::MAXP) * CH + CF::NT - 1) / CF::NT;  // chunks per thread, largest image
       const int r0 = t0 - P, n = rows * CH;
       const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<f16*>(p.x16 + (int64_t)b * L * C), (short)0, Lb * C * 2, 0x00020000);
@@ -164,13 +170,13 @@ __global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kern
       // rows outside [0, Lb) lie outside the descriptor's range (a negative row wraps past it): they load as zeros
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
-        const int idx = tid + it * AMP_NT, r = idx / CH, q = idx - r * CH;
+        const int idx = tid + it * CF::NT, r = idx / CH, q = idx - r * CH;
         const uint32_t vo = (idx < n && r0 + r >= 0) ? (uint32_t)(((r0 + r) * C + q * 8) * 2) : 0x80000000u;
         v[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rx, vo, 0, 0));
       }
 #pragma unroll
       for (int it = 0; it < IT; ++it) {
-        const int idx = tid + it * AMP_NT, r = idx / CH, q = idx - r * CH;
+        const int idx = tid + it * CF::NT, r = idx / CH, q = idx - r * CH;
         if (idx < n) *reinterpret_cast<uint4*>(As + r * CF::LDA + q * 8) = v[it];
       }
     }
@@ -186,12 +192,12 @@ __global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kern
     constexpr int ngrp = C / 2;
     // (LDS conflicts, VERDICT r03 item 4: making the activation stores conflict-free by the choice of RUN moved the
     // kernel's conflict share only 0.47 -> 0.41 and no timing, r04q; the rest are the conv phase's fragment reads)
-    const int RUN = amp_run_len(C, rows);
+    const int RUN = amp_run_len(C, rows, CF::NT);
     const int nruns = (rows + RUN - 1) / RUN;
     const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<void*>(X16 ? (const void*)p.x16 : (const void*)p.x), (short)0,
         (int)((int64_t)p.B * L * C * sizeof(TX)), 0x00020000);
-    for (int task = tid; task < ngrp * nruns; task += AMP_NT) {
+    for (int task = tid; task < ngrp * nruns; task += CF::NT) {
       const int cg = task % ngrp, ru = task / ngrp;
       const int c = cg * 2;
       const int rs = t0 - P + ru * RUN, re = rs + RUN;  // global rows of this run (whole runs: the image has room)
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kern
     // per-operand branch), and waited for once. Loaded chunk by chunk inside the loop, each chunk's load waited for every
     // store before it (in-order vmcnt) and the branches made the compiler's wait a vmcnt(0) before every use: two load
     // round trips and a store drain per chunk (assembly, r06).
-    constexpr int IT = (HB * C4 + AMP_NT - 1) / AMP_NT;  // chunks per thread and half
+    constexpr int IT = (HB * C4 + CF::NT - 1) / CF::NT;  // chunks per thread and half
     const int blk_bytes = nvalid * C * 4;
     const __amdgpu_buffer_rsrc_t r_ar =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(e.add_row ? e.add_row + base : e.bias), (short)0,
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kern
       if (has_ops) {
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-          const uint32_t vo = (uint32_t)((h * HB * C4 + tid + it * AMP_NT) * 16);  // chunk h * HB * C4 + idx
+          const uint32_t vo = (uint32_t)((h * HB * C4 + tid + it * CF::NT) * 16);  // chunk h * HB * C4 + idx
           ar[it] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_ar, vo, 0, 0));
           ac[it] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r_ac, vo, 0, 0));
         }
@@ -343,14 +349,14 @@ __global__ __launch_bounds__(AMP_NT, (AmpCfg<C, NOACT>::OCC)) void amp_conv_kern
       if (has_ops) {
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
-          const int idx = tid + it * AMP_NT;
+          const int idx = tid + it * CF::NT;
           if (idx >= nv * C4) break;
           const int r = idx / C4, c4 = idx - r * C4;
           epi2(*reinterpret_cast<const float4*>(stg + r * CF::LDC + 4 * c4), ar[it], ac[it],
                base + (int64_t)(h * HB + r) * C + 4 * c4);
         }
       } else {  // (c1: stores only; the rolled loop measured 3-5 % faster than the unrolled one here, r06e)
-        for (int idx = tid; idx < nv * C4; idx += AMP_NT) {
+        for (int idx = tid; idx < nv * C4; idx += CF::NT) {
           const int r = idx / C4, c4 = idx - r * C4;
           epi(*reinterpret_cast<const float4*>(stg + r * CF::LDC + 4 * c4), base + (int64_t)(h * HB + r) * C + 4 * c4);
         }
@@ -383,30 +389,31 @@ static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   // algorithmic bytes: x in (f32 or f16), output out (f32 and/or f16), epilogue operands in (f32)
   const double bytes =
       elems * ((X16 ? 2.0 : 4.0) + (e.out32 ? 4 : 0) + (e.out16 ? 2 : 0) + (e.add_row ? 4 : 0) + (e.acc32 ? 4 : 0));
-  const char* tag = NOACT ? "amp_conv<96,conv>" : (C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : "amp_conv<96>"));
+  const char* tag = NOACT ? (C == 96 ? "amp_conv<96,conv>" : "amp_conv<192,conv>")
+                          : (C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : (C == 96 ? "amp_conv<96>" : "amp_conv<192>")));
   const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
   // the activation image needs BT + 2P rows, not BT + 2 MAXP: sized per launch, C = 48 fits 5 workgroups per CU
   // (instead of 4) for every conv with P <= 15
   const int P = (p.k - 1) / 2 * p.d;
-  const int rows = CF::BT + 2 * P, run = amp_run_len(C, rows);
+  const int rows = CF::BT + 2 * P, run = amp_run_len(C, rows, CF::NT);
   const int img_rows = NOACT ? rows : (rows + run - 1) / run * run;
   const int lds = std::max(img_rows * CF::LDA * 2, CF::STG_BYTES);
   static const int dbg = getenv("SVC_AMP_DBG") ? atoi(getenv("SVC_AMP_DBG")) : 0;
   AmpConvArgs pa = p;
   pa.dbg = dbg;
-  hipLaunchKernelGGL((amp_conv_kernel<C, X16, NOACT>), dim3((unsigned)grid), dim3(AMP_NT), lds, s, pa, e);
+  hipLaunchKernelGGL((amp_conv_kernel<C, X16, NOACT>), dim3((unsigned)grid), dim3(CF::NT), lds, s, pa, e);
   prof_end(tok, s);
   SVC_LAUNCH_CHECK();
   return SVC_OK;
 }
 
 bool amp_conv_supported(int C, int k, int d) {
-  return (C == 24 || C == 48 || C == 96) && k >= 1 && k % 2 == 1 && (k - 1) / 2 * d <= AmpCfg<24>::MAXP;
+  return (C == 24 || C == 48 || C == 96 || C == 192) && k >= 1 && k % 2 == 1 && (k - 1) / 2 * d <= AmpCfg<24>::MAXP;
 }
 
 // act + conv + epilogue; e uses out32 / out16 / add_row / acc32 with leading dimension C (contiguous rows)
 int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
-  SVC_REQUIRE(amp_conv_supported(C, p.k, p.d) && (!p.noact || (C == 96 && p.x16)),
+  SVC_REQUIRE(amp_conv_supported(C, p.k, p.d) && (!p.noact || ((C == 96 || C == 192) && p.x16)),
               "amp_conv: C=%d k=%d d=%d noact=%d unsupported", C, p.k, p.d, (int)p.noact);
   SVC_REQUIRE(p.L >= 1 && p.Kpad >= p.k * C && p.Kpad % 32 == 0, "amp_conv: L=%d Kpad=%d", p.L, p.Kpad);
   SVC_REQUIRE((!e.out32 || e.ld32 == C) && (!e.out16 || e.ld16 == C) && (!e.add_row || e.ld_add_row == C) &&
@@ -438,10 +445,14 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
       st = q.x16 ? launch_amp<24, true>(q, f, s) : launch_amp<24, false>(q, f, s);
     else if (C == 48)
       st = q.x16 ? launch_amp<48, true>(q, f, s) : launch_amp<48, false>(q, f, s);
-    else if (q.noact)
+    else if (C == 96 && q.noact)
       st = launch_amp<96, true, true>(q, f, s);
-    else
+    else if (C == 96)
       st = q.x16 ? launch_amp<96, true>(q, f, s) : launch_amp<96, false>(q, f, s);
+    else if (q.noact)
+      st = launch_amp<192, true, true>(q, f, s);
+    else
+      st = q.x16 ? launch_amp<192, true>(q, f, s) : launch_amp<192, false>(q, f, s);
     if (st) return st;
   }
   return SVC_OK;

@@ -359,9 +359,10 @@ struct Tuning {
   int sampler_streams = 1;  // DiffSVC sampler sub-batch streams (round 4: 1 with gate_ws; 2 was the conv_gemm4 default)
   int vocoder_streams = 1;  // BigVGAN sub-batch streams
   int diff_head = 1;        // DiffSVC skip_projection + output_projection as one launch (diff_head.hip)
-  int amp_maxc = 96;        // widest BigVGAN channel count on the fused activation + conv kernel (0: none). C = 96 on
+  int amp_maxc = 192;       // widest BigVGAN channel count on the fused activation + conv kernel (0: none). C = 96 on
                             // the 256-row 2 x 2-wave tiles: BigVGAN -1.0 ms per step against activation1d + the plain
-                            // conv (profiles/r06_ab/r06x_amp_fused_c96.txt)
+                            // conv (profiles/r06_ab/r06x_amp_fused_c96.txt); C = 192 on 2 x 4 waves: -0.6 ms against
+                            // activation1d + conv_gemm3<256,192> (r06z_amp_c192.txt)
   int amp_conv_maxc = 96;   // widest unfused BigVGAN conv (activation1d first) run by amp_conv's plain-conv form (the
                             // LDS-resident row image, every tap read from it) instead of conv_gemm3 (0: none). C = 96
                             // with amp_maxc 48: 11.5 -> 8.3 ms per step, +0.8 % end to end

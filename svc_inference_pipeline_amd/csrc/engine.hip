@@ -2683,7 +2683,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
           // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
           const bool fuse = ch <= amp_maxc && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
           // unfused C = 96: the plain conv on amp_conv's LDS row image instead of conv_gemm3 (tune.amp_conv_maxc)
-          const bool plain = !fuse && ch == 96 && ch <= tuning().amp_conv_maxc &&
+          const bool plain = !fuse && (ch == 96 || ch == 192) && ch <= tuning().amp_conv_maxc &&
                              amp_conv_supported(ch, S.rk[j], S.rd[j][l]) && amp_conv_supported(ch, S.rk[j], d2);
           auto plain_conv = [&](const PackedGemm& g, int dil, const EpiArgs& ep, const char* site) {
             AmpConvArgs q{nullptr, Bh, L, S.rk[j], dil, nullptr, nullptr, nullptr, g.W, g.Kpad, g.bias};

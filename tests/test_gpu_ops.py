@@ -109,12 +109,12 @@ def test_activation1d(B, L, C, x16):
     assert np.max(np.abs(out - ref.numpy()) / (np.abs(ref.numpy()) + 1e-2)) < 5e-3
 
 
-@pytest.mark.parametrize("C", [24, 48, 96])
+@pytest.mark.parametrize("C", [24, 48, 96, 192])
 @pytest.mark.parametrize("B,L,k,d", [(2, 37, 3, 1), (1, 1, 11, 5), (1, 5, 7, 3), (2, 130, 11, 5), (1, 300, 7, 3),
                                      (3, 257, 11, 1), (2, 600, 3, 5)])
 def test_amp_conv(B, L, k, d, C):
     """Fused SnakeBeta Activation1d -> dilated conv -> bias + residual (BigVGAN C <= 96 stages; C <= 48 run the
-    packed channel-pair activation; C = 96 on 256-row tiles of 2 x 2 waves)."""
+    packed channel-pair activation; C = 96 on 256-row tiles of 2 x 2 waves, C = 192 of 2 x 4)."""
     from svc_inference_pipeline_amd import weights as W
     g = torch.Generator().manual_seed(5)
     x = torch.randn(B, C, L, generator=g) * 2
