@@ -42,7 +42,7 @@ struct AmpCfg {
   // C = 24 / 48: 512-row tiles on 4 x 1 waves (128 rows each, the same weight reuse), 2 workgroups per CU: against the
   // round-5 256-row tiles at 4 per CU, 16.95 -> 16.0 ms per step (profiles/r06_ab/r06y_amp_narrow_512rows.txt)
   // C = 192: 8 waves on 2 x 4 (each 128 rows x 48 columns), one workgroup per CU (the image is 127-133 KiB).
-  static constexpr bool WIDE = NOACT || C >= 96;
+  static constexpr bool WIDE = C >= 96;
   static constexpr int NT = C == 192 ? 512 : AMP_NT;    // threads
 #ifndef AMP_BT192
 #define AMP_BT192 256
@@ -155,8 +155,12 @@ __global__ __launch_bounds__((AmpCfg<C, NOACT>::NT), (AmpCfg<C, NOACT>::OCC)) vo
   // batch stride L. Tiles wholly past Lb have nothing to compute (block-uniform exit before any barrier).
   const int Lb = p.tv ? min(L, p.tv[b] * p.tv_mul) : L;
   if (t0 >= Lb) return;
-  const int P = (p.k - 1) / 2 * p.d;
+  // a negative dilation walks the taps downwards (tap 0 reads row t + P): the ConvTranspose phase pairs of
+  // svc_bigvgan's combined up-sampling conv, whose per-phase tap order this keeps
+  const int ad = p.d < 0 ? -p.d : p.d;
+  const int P = (p.k - 1) / 2 * ad;
   const int rows = CF::BT + 2 * P;
+  const int tap0 = p.d < 0 ? 2 * P : 0;
 
   // ------------------------------------------------------------------ 1. SnakeBeta -> LDS (f16)
   if constexpr (NOACT) {
@@ -241,7 +245,7 @@ __global__ __launch_bounds__((AmpCfg<C, NOACT>::NT), (AmpCfg<C, NOACT>::OCC)) vo
     }
 #pragma unroll
     for (int i = 0; i < MW; ++i) {
-      const int r = (wm * MW + i) * 16 + fr + tap * p.d;
+      const int r = (wm * MW + i) * 16 + fr + tap0 + tap * p.d;
       af[i] = *reinterpret_cast<const half8*>(As + r * CF::LDA + cc * 8);
     }
 #pragma unroll
@@ -389,12 +393,12 @@ static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
   // algorithmic bytes: x in (f32 or f16), output out (f32 and/or f16), epilogue operands in (f32)
   const double bytes =
       elems * ((X16 ? 2.0 : 4.0) + (e.out32 ? 4 : 0) + (e.out16 ? 2 : 0) + (e.add_row ? 4 : 0) + (e.acc32 ? 4 : 0));
-  const char* tag = NOACT ? (C == 96 ? "amp_conv<96,conv>" : "amp_conv<192,conv>")
+  const char* tag = NOACT ? (C == 48 ? "amp_conv<48,conv>" : (C == 96 ? "amp_conv<96,conv>" : "amp_conv<192,conv>"))
                           : (C == 24 ? "amp_conv<24>" : (C == 48 ? "amp_conv<48>" : (C == 96 ? "amp_conv<96>" : "amp_conv<192>")));
   const int tok = prof_begin(tag, 2.0 * elems * C * p.k, bytes, s);
   // the activation image needs BT + 2P rows, not BT + 2 MAXP: sized per launch, C = 48 fits 5 workgroups per CU
   // (instead of 4) for every conv with P <= 15
-  const int P = (p.k - 1) / 2 * p.d;
+  const int P = (p.k - 1) / 2 * (p.d < 0 ? -p.d : p.d);
   const int rows = CF::BT + 2 * P, run = amp_run_len(C, rows, CF::NT);
   const int img_rows = NOACT ? rows : (rows + run - 1) / run * run;
   const int lds = std::max(img_rows * CF::LDA * 2, CF::STG_BYTES);
@@ -408,12 +412,13 @@ static int launch_amp(const AmpConvArgs& p, const EpiArgs& e, hipStream_t s) {
 }
 
 bool amp_conv_supported(int C, int k, int d) {
-  return (C == 24 || C == 48 || C == 96 || C == 192) && k >= 1 && k % 2 == 1 && (k - 1) / 2 * d <= AmpCfg<24>::MAXP;
+  return (C == 24 || C == 48 || C == 96 || C == 192) && k >= 1 && k % 2 == 1 && d != 0 &&
+         (k - 1) / 2 * (d < 0 ? -d : d) <= AmpCfg<24>::MAXP;
 }
 
 // act + conv + epilogue; e uses out32 / out16 / add_row / acc32 with leading dimension C (contiguous rows)
 int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
-  SVC_REQUIRE(amp_conv_supported(C, p.k, p.d) && (!p.noact || ((C == 96 || C == 192) && p.x16)),
+  SVC_REQUIRE(amp_conv_supported(C, p.k, p.d) && (!p.noact || ((C == 48 || C == 96 || C == 192) && p.x16)) && (p.noact || p.d > 0),
               "amp_conv: C=%d k=%d d=%d noact=%d unsupported", C, p.k, p.d, (int)p.noact);
   SVC_REQUIRE(p.L >= 1 && p.Kpad >= p.k * C && p.Kpad % 32 == 0, "amp_conv: L=%d Kpad=%d", p.L, p.Kpad);
   SVC_REQUIRE((!e.out32 || e.ld32 == C) && (!e.out16 || e.ld16 == C) && (!e.add_row || e.ld_add_row == C) &&
@@ -443,6 +448,8 @@ int amp_conv(const AmpConvArgs& p, int C, const EpiArgs& e, hipStream_t s) {
     int st;
     if (C == 24)
       st = q.x16 ? launch_amp<24, true>(q, f, s) : launch_amp<24, false>(q, f, s);
+    else if (C == 48 && q.noact)
+      st = launch_amp<48, true, true>(q, f, s);
     else if (C == 48)
       st = q.x16 ? launch_amp<48, true>(q, f, s) : launch_amp<48, false>(q, f, s);
     else if (C == 96 && q.noact)

@@ -363,6 +363,8 @@ struct Tuning {
                             // the 256-row 2 x 2-wave tiles: BigVGAN -1.0 ms per step against activation1d + the plain
                             // conv (profiles/r06_ab/r06x_amp_fused_c96.txt); C = 192 on 2 x 4 waves: -0.6 ms against
                             // activation1d + conv_gemm3<256,192> (r06z_amp_c192.txt)
+  int amp_ups = 1;          // BigVGAN rate-2 ConvTranspose with cin 48 / 96 / 192 as one amp_conv plain conv (VStage::upc;
+                            // 0: phase GEMMs): those stages 1.93 -> 0.89 ms per step (profiles/r06_ab/r06zc_amp_ups.txt)
   int amp_conv_maxc = 96;   // widest unfused BigVGAN conv (activation1d first) run by amp_conv's plain-conv form (the
                             // LDS-resident row image, every tap read from it) instead of conv_gemm3 (0: none). C = 96
                             // with amp_maxc 48: 11.5 -> 8.3 ms per step, +0.8 % end to end

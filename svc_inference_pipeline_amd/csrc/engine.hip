@@ -312,6 +312,11 @@ struct ActP {
 struct VStage {
   int cin, cout, rate, k;
   std::vector<PackedGemm> phases;
+  // rate-2 ConvTranspose as ONE conv over the input rows (tune.amp_ups): output columns r * cout + n of input row t are
+  // output row 2t + r, so [L][2 cout] is the time-major output; 3 taps at offsets +1, 0, -1 (each phase's two taps in
+  // its own GEMM's order, zeros for the tap it lacks); run by amp_conv's plain-conv form (cin = 2 cout = 48 / 96 / 192)
+  PackedGemm upc;
+  bool up_comb = false;
   // resblocks j: convs1[l], convs2[l], acts[2l], acts[2l+1]
   std::vector<std::vector<PackedGemm>> c1, c2;
   std::vector<std::vector<ActP>> acts;
@@ -332,7 +337,8 @@ static int* tuning_field(T& t, const char* name) {
               {"whisper_streams", &t.whisper_streams}, {"sampler_streams", &t.sampler_streams},
               {"vocoder_streams", &t.vocoder_streams}, {"diff_head", &t.diff_head},
               {"amp_maxc", &t.amp_maxc},               {"res_proj", &t.res_proj},
-              {"gate_ws", &t.gate_ws},                 {"amp_conv_maxc", &t.amp_conv_maxc}};
+              {"gate_ws", &t.gate_ws},                 {"amp_conv_maxc", &t.amp_conv_maxc},
+              {"amp_ups", &t.amp_ups}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) return it.v;
   return nullptr;
@@ -340,7 +346,7 @@ static int* tuning_field(T& t, const char* name) {
 
 void Tuning::from_env() {
   for (const char* name : {"gemm_variant", "gemm3_direct", "whisper_streams", "sampler_streams", "vocoder_streams",
-                           "diff_head", "amp_maxc", "res_proj", "gate_ws", "amp_conv_maxc"}) {
+                           "diff_head", "amp_maxc", "res_proj", "gate_ws", "amp_conv_maxc", "amp_ups"}) {
     std::string env = "SVC_";
     for (const char* q = name; *q; ++q) env += (char)toupper((unsigned char)*q);
     if (const char* v = getenv(env.c_str())) *tuning_field(*this, name) = atoi(v);
@@ -705,6 +711,45 @@ int pack_conv_transpose(svc_ctx* c, std::vector<PackedGemm>& phases, const float
     phases[r].tap_add = add;
     phases[r].istride = 1;
   }
+  return SVC_OK;
+}
+
+// The combined form of a rate-2 ConvTranspose (VStage::upc): phase r's tap j reads input row t + add_r - j with weight
+// tap base_r + 2j (pack_conv_transpose); here tap q reads row t + 1 - q (amp_conv with k = 3, d = -1), so q = 1 - add_r + j.
+// Built only where each phase's taps lie within offsets -1..1 and cin = 2 cout is an amp_conv plain-conv width. At cin 96 /
+// 192 every 32-deep MFMA step lies within one tap, so each phase sums exactly its GEMM's products in its GEMM's order;
+// at cin 48 the steps straddle taps and the zero tap shifts phase 0's grouping (fp32 summation order only).
+int pack_conv_transpose_comb(svc_ctx* c, VStage& S, const float* v, const float* wn_g, const float* bias) {
+  const int Cin = S.cin, Cout = S.cout, k = S.k, s = S.rate, pad = (S.k - S.rate) / 2;
+  S.up_comb = false;
+  if (s != 2 || k % s != 0 || Cin != 2 * Cout || !(Cin == 48 || Cin == 96 || Cin == 192)) return SVC_OK;
+  for (int r = 0; r < s; ++r) {
+    const int add = (r + pad) / s;
+    if (add > 1 || add - (k / s - 1) < -1) return SVC_OK;
+  }
+  std::vector<double> scale(Cin, 1.0);
+  if (wn_g) {
+    for (int i = 0; i < Cin; ++i) {
+      double acc = 0;
+      for (int64_t j = 0; j < (int64_t)Cout * k; ++j) {
+        double x = v[(int64_t)i * Cout * k + j];
+        acc += x * x;
+      }
+      scale[i] = (double)wn_g[i] / sqrt(acc);
+    }
+  }
+  int st = pack_gemm(
+      c, S.upc, 2 * Cout, Cin, Cin, 3,
+      [&](int n, int ci, int q) {
+        const int r = n / Cout, o = n - r * Cout;
+        const int base = (r + pad) % s, add = (r + pad) / s;
+        const int j = q - 1 + add;
+        if (j < 0 || j >= k / s) return 0.0f;
+        return (float)((double)v[((int64_t)ci * Cout + o) * k + base + s * j] * scale[ci]);
+      },
+      [&](int n) { return bias ? bias[n % Cout] : 0.0f; });
+  if (st) return st;
+  S.up_comb = true;
   return SVC_OK;
 }
 
@@ -1347,6 +1392,7 @@ int build_vocoder(svc_ctx* c) {
     if ((st = pack_conv_transpose(c, S.phases, uv->host, ug->host, ub->host, S.cin, S.cout, S.k, S.rate,
                                   (S.k - S.rate) / 2)))
       return st;
+    if ((st = pack_conv_transpose_comb(c, S, uv->host, ug->host, ub->host))) return st;
     S.c1.resize(nk);
     S.c2.resize(nk);
     S.acts.resize(nk);
@@ -2652,7 +2698,19 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
       f16* a16h = a16 + ro;
       const f16* in16 = i == 0 ? pre16 + (size_t)b0[h] * T * c->v_c0 : next16 + ro;
       f16* next16h = next16 + ro;
-      // ConvTranspose1d as `rate` phase GEMMs writing rows t*rate + r
+      // ConvTranspose1d as `rate` phase GEMMs writing rows t*rate + r, or (rate 2, tune.amp_ups) as one conv
+      if (S.up_comb && tuning().amp_ups) {
+        AmpConvArgs q{nullptr, Bh, Lin, 3, -1, nullptr, nullptr, nullptr, S.upc.W, S.upc.Kpad, S.upc.bias};
+        q.x16 = in16;
+        q.noact = true;
+        q.tv = tvh;
+        q.tv_mul = mul_in;
+        EpiArgs u = epi();
+        u.out32 = Xh;
+        u.ld32 = S.cin;
+        prof_site("bigvgan.ups");
+        if ((st = amp_conv(q, S.cin, u, sh))) return st;
+      } else
       for (int r = 0; r < S.rate; ++r) {
         EpiArgs u = epi();
         u.T_ostore = L;

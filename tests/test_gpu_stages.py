@@ -370,6 +370,27 @@ def test_bigvgan_plain_conv_c96(engine, tune):
             assert np.array_equal(a, b), (maxc, i, float(np.abs(a - b).max()), float(np.abs(a).max()))
 
 
+def test_bigvgan_ups_combined(engine, tune):
+    """The rate-2 up-sampling ConvTranspose1d stages with 48 / 96 / 192 input channels (modules/bigvgan.py ups, `rate`
+    phase GEMMs with tune.amp_ups = 0) as ONE conv over the input rows on amp_conv's plain-conv form (amp_ups = 1: 3 taps
+    walked downwards, each phase's two taps in its GEMM's order, a zero tap for the one it lacks), for equal and ragged
+    lengths. At 96 / 192 input channels each phase sums exactly its GEMM's products in the same order; at 48 the
+    32-deep MFMA steps straddle taps and one phase's fp32 summation grouping moves, so the waveforms agree to fp32
+    rounding (rel-L2 < 1e-5), not bit for bit."""
+    rng = np.random.default_rng(11)
+    x = dev(rng.uniform(-1, 1, (3, 41, 100)).astype(np.float32))
+    outs = {}
+    for v in ("0", "1"):
+        tune(engine, amp_ups=v)
+        outs[v] = (engine.bigvgan(x).cpu().numpy(), engine.bigvgan(x, frames=[41, 23, 33]).cpu().numpy())
+    for i in range(2):
+        a, b = outs["0"][i], outs["1"][i]
+        assert rel_l2(b, a) < 1e-5, (i, rel_l2(b, a))
+        if i == 1:
+            for u, n in enumerate([41, 23, 33]):  # ragged: each utterance's samples past its end stay untouched
+                assert np.array_equal(a[u, n * 256:], b[u, n * 256:])
+
+
 def test_vocoder_sub_streams_bit_identical(engine, tune):
     """BigVGAN with utterance-aligned sub-batches on 1, 2 or 3 streams: identical waveforms."""
     rng = np.random.default_rng(1)
