@@ -62,7 +62,7 @@ svc_status svc_ctx_destroy(svc_ctx* ctx);
    v_mfma_f32_16x16x32_bf16, and content features cross svc_map_content* / svc_condition as bfloat16; BigVGAN stays
    fp16), "hubert.output_layer"). An unknown key is SVC_ERR_INVALID (a misspelt key must not leave a default in place).
    "tune.<name>" keys set a kernel switch of this context at any time (gemm_variant, gemm3_direct, whisper_streams,
-   sampler_streams, vocoder_streams, diff_head, amp_maxc, amp_conv_maxc, amp_ups, res_proj, gate_ws; "tune.reset" restores the creation-time values). Defaults
+   sampler_streams, vocoder_streams, diff_head, amp_maxc, amp_ups, res_proj, gate_ws; "tune.reset" restores the creation-time values). Defaults
    are the measured production kernels; at creation an SVC_<NAME> environment variable overrides each. ctx may be
    NULL for "tune.*" keys: the switches of the op-level entry points (svc_op_*, svc_gemm_bench). */
 svc_status svc_ctx_set_config(svc_ctx* ctx, const char* key, double value);

@@ -139,9 +139,11 @@ __device__ __forceinline__ void amp_act_pair(__amdgpu_buffer_rsrc_t rx, uint32_t
 // VGPR file (round 5, 4 per CU: without an occupancy target it split the file into VGPRs + AGPRs at 5 waves). The activation runs on channel pairs with packed
 // f32 ops in 4-row blocks for every C (round 4: C = 96 had a single-channel 8-row form, removed with the packed
 // clamp-free form).
-// NOACT: the plain conv of an input already activated (activation1d's f16 output, p.x16): phase 1 copies the rows into
-// the image (16-B loads, zeros outside [0, Lb)) and the conv reads every tap from it, so each input row leaves HBM / L2
-// once per workgroup instead of once per tap as in conv_gemm3's implicit GEMM.
+// NOACT: the plain conv of an f16 input with no activation before it (p.x16; svc_bigvgan's rate-2 up-sampling as one
+// conv, VStage::upc): phase 1 copies the rows into the image (16-B loads, zeros outside [0, Lb)) and the conv reads
+// every tap from it, so each input row leaves HBM / L2 once per workgroup instead of once per tap as in conv_gemm3's
+// implicit GEMM. (Round 6 also ran the C = 96 / 192 resblock convs after activation1d this way: 8.3 against conv_gemm3's
+// 11.5 ms per step at C = 96, but fused with the activation it is faster still, r06w / r06x / r06z.)
 template <int C, bool X16 = false, bool NOACT = false>
 __global__ __launch_bounds__((AmpCfg<C, NOACT>::NT), (AmpCfg<C, NOACT>::OCC)) void amp_conv_kernel(AmpConvArgs p, EpiArgs e) {
   using CF = AmpCfg<C, NOACT>;

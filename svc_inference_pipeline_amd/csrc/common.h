@@ -365,10 +365,6 @@ struct Tuning {
                             // activation1d + conv_gemm3<256,192> (r06z_amp_c192.txt)
   int amp_ups = 1;          // BigVGAN rate-2 ConvTranspose with cin 48 / 96 / 192 as one amp_conv plain conv (VStage::upc;
                             // 0: phase GEMMs): those stages 1.93 -> 0.89 ms per step (profiles/r06_ab/r06zc_amp_ups.txt)
-  int amp_conv_maxc = 96;   // widest unfused BigVGAN conv (activation1d first) run by amp_conv's plain-conv form (the
-                            // LDS-resident row image, every tap read from it) instead of conv_gemm3 (0: none). C = 96
-                            // with amp_maxc 48: 11.5 -> 8.3 ms per step, +0.8 % end to end
-                            // (profiles/r06_ab/r06w_amp_plain_conv_c96.txt); the unfused path of AMPBlock2 generators
   int res_proj = 1;         // DiffSVC residual and input projections on the weight-stationary streams (res_proj.hip
                             // res_proj / mel_proj; 0: conv_gemm3;
                             // > 1: that many row lanes of 2 workgroups instead of 1/2 (one sampler stream) or 3/8

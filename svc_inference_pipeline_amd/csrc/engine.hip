@@ -337,8 +337,7 @@ static int* tuning_field(T& t, const char* name) {
               {"whisper_streams", &t.whisper_streams}, {"sampler_streams", &t.sampler_streams},
               {"vocoder_streams", &t.vocoder_streams}, {"diff_head", &t.diff_head},
               {"amp_maxc", &t.amp_maxc},               {"res_proj", &t.res_proj},
-              {"gate_ws", &t.gate_ws},                 {"amp_conv_maxc", &t.amp_conv_maxc},
-              {"amp_ups", &t.amp_ups}};
+              {"gate_ws", &t.gate_ws},                 {"amp_ups", &t.amp_ups}};
   for (auto& it : ints)
     if (strcmp(it.name, name) == 0) return it.v;
   return nullptr;
@@ -346,7 +345,7 @@ static int* tuning_field(T& t, const char* name) {
 
 void Tuning::from_env() {
   for (const char* name : {"gemm_variant", "gemm3_direct", "whisper_streams", "sampler_streams", "vocoder_streams",
-                           "diff_head", "amp_maxc", "res_proj", "gate_ws", "amp_conv_maxc", "amp_ups"}) {
+                           "diff_head", "amp_maxc", "res_proj", "gate_ws", "amp_ups"}) {
     std::string env = "SVC_";
     for (const char* q = name; *q; ++q) env += (char)toupper((unsigned char)*q);
     if (const char* v = getenv(env.c_str())) *tuning_field(*this, name) = atoi(v);
@@ -2740,18 +2739,6 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
           const f16* act_in16 = rb2 ? nullptr : tmp16;
           // small channel counts: SnakeBeta fused into the conv (amp_conv.hip); otherwise activation1d + GEMM
           const bool fuse = ch <= amp_maxc && amp_conv_supported(ch, S.rk[j], S.rd[j][l]);
-          // unfused C = 96: the plain conv on amp_conv's LDS row image instead of conv_gemm3 (tune.amp_conv_maxc)
-          const bool plain = !fuse && (ch == 96 || ch == 192) && ch <= tuning().amp_conv_maxc &&
-                             amp_conv_supported(ch, S.rk[j], S.rd[j][l]) && amp_conv_supported(ch, S.rk[j], d2);
-          auto plain_conv = [&](const PackedGemm& g, int dil, const EpiArgs& ep, const char* site) {
-            AmpConvArgs q{nullptr, Bh, L, S.rk[j], dil, nullptr, nullptr, nullptr, g.W, g.Kpad, g.bias};
-            q.x16 = a16h;
-            q.noact = true;
-            q.tv = tvh;
-            q.tv_mul = mul;
-            prof_site(site);
-            return amp_conv(q, ch, ep, sh);
-          };
           if (!rb2) {
             EpiArgs e1 = epi();
             e1.out16 = tmp16;
@@ -2765,9 +2752,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
               if ((st = amp_conv(p1, ch, e1, sh))) return st;
             } else {
               if ((st = activation1d(src, a16h, Bh, L, ch, ch, a1.alpha, a1.beta, a1.filt, sh, tvh, mul))) return st;
-              if ((st = plain ? plain_conv(S.c1[j][l], S.rd[j][l], e1, "bigvgan.amp_c1")
-                              : run_gemm(S.c1[j][l], a16h, ch, ch, Bh, L, L, e1, sh, "bigvgan.amp_c1", tvh, mul)))
-                return st;
+              if ((st = run_gemm(S.c1[j][l], a16h, ch, ch, Bh, L, L, e1, sh, "bigvgan.amp_c1", tvh, mul))) return st;
             }
           }
           if (!fuse &&
@@ -2807,8 +2792,7 @@ svc_status svc_bigvgan(svc_ctx* c, const float* x0, int B, int T, const int32_t*
             p2.x16 = act_in16;
             prof_site("bigvgan.amp_c2");
             if ((st = amp_conv(p2, ch, e2, sh))) return st;
-          } else if ((st = plain ? plain_conv(S.c2[j][l], d2, e2, "bigvgan.amp_c2")
-                                 : run_gemm(S.c2[j][l], a16h, ch, ch, Bh, L, L, e2, sh, "bigvgan.amp_c2", tvh, mul))) {
+          } else if ((st = run_gemm(S.c2[j][l], a16h, ch, ch, Bh, L, L, e2, sh, "bigvgan.amp_c2", tvh, mul))) {
             return st;
           }
         }

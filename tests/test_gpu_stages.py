@@ -353,23 +353,6 @@ def test_bigvgan_variants(cfg, states, golden, variant, tune):
         e.close()
 
 
-def test_bigvgan_plain_conv_c96(engine, tune):
-    """The C = 96 (and C = 192) AMPBlock convs (modules/bigvgan.py:424-433) on amp_conv's plain-conv form (tune.amp_conv_maxc = 96:
-    activation1d's f16 output staged once into an LDS row image, every tap read from it) against conv_gemm3's implicit
-    GEMM (amp_conv_maxc = 0), for equal and ragged lengths. Both run one 32-deep MFMA chain per accumulator over the same
-    packed K order and the same epilogue arithmetic, so the waveforms are identical."""
-    rng = np.random.default_rng(7)
-    x = dev(rng.uniform(-1, 1, (3, 37, 100)).astype(np.float32))
-    outs = {}
-    for maxc in ("0", "96", "192"):
-        tune(engine, amp_maxc="48", amp_conv_maxc=maxc)  # C = 96 / 192 unfused (activation1d first)
-        outs[maxc] = (engine.bigvgan(x).cpu().numpy(), engine.bigvgan(x, frames=[37, 21, 30]).cpu().numpy())
-    for maxc in ("96", "192"):
-        for i in range(2):
-            a, b = outs["0"][i], outs[maxc][i]
-            assert np.array_equal(a, b), (maxc, i, float(np.abs(a - b).max()), float(np.abs(a).max()))
-
-
 def test_bigvgan_ups_combined(engine, tune):
     """The rate-2 up-sampling ConvTranspose1d stages with 48 / 96 / 192 input channels (modules/bigvgan.py ups, `rate`
     phase GEMMs with tune.amp_ups = 0) as ONE conv over the input rows on amp_conv's plain-conv form (amp_ups = 1: 3 taps
